@@ -1,0 +1,395 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE.
+
+Run only in the build container, where the reference is importable:
+
+    PYTHONPATH=/root/reference/src python3 tests/golden/make_golden.py
+
+The reference never ships with this repository and never runs on the GPU box;
+what is committed is data only: the seeded inputs each case was built from and
+the exact output the reference printed for them (plus unit-level known-answer
+vectors for its helper functions).  The case generator below is this build's
+own code.
+"""
+
+from __future__ import annotations
+
+import gzip
+import hashlib
+import io
+import json
+import logging
+import os
+import random
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DATA = os.path.join(HERE, "data")
+
+IUPAC_EXTRA = "RYMKSWBDHVN"
+
+
+def _ref():
+    from merpcr import MerPCR  # noqa: F401  (reference, build container only)
+    from merpcr.core.models import FASTARecord
+    return MerPCR, FASTARecord
+
+
+# --------------------------------------------------------------------------
+# seeded case generator (this build's own code)
+# --------------------------------------------------------------------------
+
+def _rc(s):
+    comp = {"A": "T", "C": "G", "G": "C", "T": "A", "U": "A", "B": "V", "V": "B",
+            "D": "H", "H": "D", "K": "M", "M": "K", "R": "Y", "Y": "R",
+            "N": "N", "S": "S", "W": "W", "X": "X"}
+    return "".join(comp.get(c.upper(), "N") for c in reversed(s))
+
+
+def _rand_seq(rng, n, mode):
+    if n <= 0:
+        return ""
+    if mode == "acgt":
+        return "".join(rng.choice("ACGT") for _ in range(n))
+    if mode == "lowcomplex":
+        alpha = rng.choice(["AT", "GC", "AC", "ACG", "A"])
+        return "".join(rng.choice(alpha) for _ in range(n))
+    if mode == "nruns":
+        out = []
+        while len(out) < n:
+            if rng.random() < 0.08:
+                out.extend("N" * rng.randint(1, 40))
+            else:
+                out.extend(rng.choice("ACGT") for _ in range(rng.randint(5, 120)))
+        return "".join(out[:n])
+    if mode == "iupac":
+        return "".join(rng.choice("ACGT" * 6 + IUPAC_EXTRA + "X") for _ in range(n))
+    if mode == "mixedcase":
+        return "".join(rng.choice("ACGTacgt") for _ in range(n))
+    if mode == "rna":
+        return "".join(rng.choice("ACGU" + "ACGT" * 3) for _ in range(n))
+    if mode == "junk":
+        return "".join(rng.choice("ACGT" * 8 + "Nn*-.Z0x ") for _ in range(n))
+    raise ValueError(mode)
+
+
+def _mutate(rng, s, k, protect_tail=0, protect_head=0):
+    s = list(s)
+    L = len(s)
+    for _ in range(k):
+        lo = protect_head
+        hi = L - 1 - protect_tail
+        if hi < lo:
+            break
+        i = rng.randint(lo, hi)
+        s[i] = rng.choice([c for c in "ACGT" if c != s[i].upper()] or ["A"])
+    return "".join(s)
+
+
+def _primer(rng, L, style):
+    if style == "acgt":
+        return "".join(rng.choice("ACGT") for _ in range(L))
+    if style == "lower":
+        return "".join(rng.choice("ACGTacgt") for _ in range(L))
+    if style == "iupac":
+        p = [rng.choice("ACGT") for _ in range(L)]
+        for _ in range(rng.randint(1, max(1, L // 5))):
+            p[rng.randrange(L)] = rng.choice(IUPAC_EXTRA)
+        return "".join(p)
+    if style == "rna":
+        return "".join(rng.choice("ACGU") for _ in range(L))
+    if style == "weird":
+        p = [rng.choice("ACGT") for _ in range(L)]
+        for _ in range(rng.randint(1, 3)):
+            p[rng.randrange(L)] = rng.choice("XZ-*nr")
+        return "".join(p)
+    raise ValueError(style)
+
+
+def _size_field(rng, size):
+    r = rng.random()
+    if r < 0.65:
+        return str(size)
+    if r < 0.8:
+        a = max(1, size - rng.randint(0, 30))
+        return f"{a}-{2 * size - a}"
+    return rng.choice(["-5", "0", "abc", "10-", "-", "1-2-3", "x-y", " 7", "150", "3"])
+
+
+def gen_case(rng, idx):
+    W = rng.choice([3, 4, 5, 6, 7, 8, 8, 9, 10, 11, 11, 11, 12, 13, 14, 16])
+    M = rng.choice([0, 1, 3, 10, 50, 50])
+    N = rng.choice([0, 0, 1, 1, 2, 3])
+    X = rng.choice([0, 1, 1, 2, 4, 40])
+    I = rng.choice([0, 0, 1])
+    Z = rng.choice([240, 240, 100, 60])
+    mode = rng.choice(["acgt", "acgt", "acgt", "nruns", "iupac", "mixedcase",
+                       "lowcomplex", "rna", "junk"])
+    n_sts = rng.randint(1, 10)
+    sts_lines = []
+    planted = []
+    for s in range(n_sts):
+        L1 = rng.randint(W, max(W, 26))
+        L2 = rng.randint(W, max(W, 26))
+        style = rng.choice(["acgt"] * 6 + ["lower", "iupac", "rna", "weird"])
+        p1 = _primer(rng, L1, style)
+        p2 = _primer(rng, L2, rng.choice(["acgt", "acgt", style]))
+        size = rng.randint(max(1, L1 + L2 - 10), L1 + L2 + 250)
+        field = _size_field(rng, size)
+        alias = rng.choice(["", "alias%d" % s, "(D17S%d)  Chr.1, 2.0 cM" % s])
+        cols = [f"STS{idx}_{s}", p1, p2, field]
+        if alias or rng.random() < 0.3:
+            cols.append(alias)
+        if rng.random() < 0.05:
+            cols.append("extra")
+        sts_lines.append("\t".join(cols))
+        if rng.random() < 0.08:
+            sts_lines.append(sts_lines[-1])  # duplicate line -> duplicate hits
+        planted.append((p1, p2, size))
+    if rng.random() < 0.2:
+        sts_lines.insert(rng.randrange(len(sts_lines) + 1), "# comment line")
+    if rng.random() < 0.15:
+        sts_lines.insert(rng.randrange(len(sts_lines) + 1), "")
+    if rng.random() < 0.02:
+        sts_lines.append("BAD\tONLY\tTHREE")
+
+    if rng.random() < 0.08:
+        # dense case: tiny word, low-complexity genome and primers -> many hits per seed
+        W = rng.choice([3, 4, 5])
+        alpha = rng.choice(["AT", "ACG", "GC"])
+        sts_lines = []
+        for s in range(rng.randint(1, 4)):
+            p1 = "".join(rng.choice(alpha) for _ in range(rng.randint(W, 8)))
+            p2 = "".join(rng.choice(alpha) for _ in range(rng.randint(W, 8)))
+            sts_lines.append(f"D{idx}_{s}\t{p1}\t{p2}\t{rng.randint(10, 60)}\tdense")
+        seq = "".join(rng.choice(alpha) for _ in range(rng.randint(100, 700)))
+        params = dict(wordsize=W, margin=rng.choice([0, 3, 10]), mismatches=N,
+                      three_prime_match=X, iupac_mode=I, default_pcr_size=Z)
+        return params, "\n".join(sts_lines) + "\n", [(f">dense{idx}", seq)]
+
+    n_rec = rng.choice([1, 1, 1, 2, 3])
+    records = []
+    for r in range(n_rec):
+        n = rng.choice([0, W - 1, W, W + 1, rng.randint(50, 600), rng.randint(600, 4000)])
+        if mode in ("lowcomplex",) or (I and mode in ("iupac", "nruns")):
+            n = min(n, 800)
+        seq = list(_rand_seq(rng, n, mode))
+        # plant amplicons in the orientations merpcr finds
+        for p1, p2, size in planted:
+            if rng.random() < 0.8 and n > 0:
+                prod = max(len(p1) + len(p2), size + rng.randint(-M - 2, M + 2))
+                fill = max(0, prod - len(p1) - len(p2))
+                form = rng.choice(["plus", "minus", "minus"])
+                if form == "plus":
+                    a, b = p1, p2
+                else:
+                    a, b = p2, _rc(p1)
+                if N and rng.random() < 0.6:
+                    a = _mutate(rng, a, rng.randint(1, N), protect_tail=min(X, len(a)))
+                amp = a + _rand_seq(rng, fill, "acgt") + b
+                if rng.random() < 0.3:
+                    amp = amp.lower()
+                start = rng.randint(0, max(0, n - 1))
+                if rng.random() < 0.15:
+                    start = max(0, n - len(amp) + rng.randint(-5, 5))
+                seq[start:start + len(amp)] = list(amp)
+        records.append((f">rec{idx}_{r} desc {r}", "".join(seq)))
+    params = dict(wordsize=W, margin=M, mismatches=N, three_prime_match=X,
+                  iupac_mode=I, default_pcr_size=Z)
+    return params, "\n".join(sts_lines) + "\n", records
+
+
+def gen_fasta_text(rng, records):
+    out = []
+    if rng.random() < 0.2:
+        out.append("ACGTACGT orphan line before header")
+    nl = rng.choice(["\n", "\r\n", "\n", "\r"])
+    for head, seq in records:
+        out.append(head + rng.choice(["", "  ", "\t"]))
+        w = rng.choice([60, 70, 13, 1000])
+        for i in range(0, len(seq), w):
+            chunk = seq[i:i + w]
+            if rng.random() < 0.1:
+                chunk = chunk + rng.choice([" 123", "*", "  ", "-", "U", "ſ", "\t9"])
+            if rng.random() < 0.05:
+                out.append("")
+            out.append(rng.choice(["", " "]) + chunk)
+    return nl.join(out) + nl
+
+
+# --------------------------------------------------------------------------
+# running the reference
+# --------------------------------------------------------------------------
+
+def run_ref(params, sts_text, records=None, fasta_text=None, threads=1):
+    MerPCR, FASTARecord = _ref()
+    eng = MerPCR(threads=threads, **params)
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "x.sts")
+        with open(sp, "w") as fh:
+            fh.write(sts_text)
+        ok = eng.load_sts_file(sp)
+        if not ok:
+            return {"load_ok": False}
+        if fasta_text is not None:
+            fp = os.path.join(td, "x.fa")
+            with open(fp, "w", newline="") as fh:
+                fh.write(fasta_text)
+            recs = eng.load_fasta_file(fp)
+            loaded = [[r.defline, r.sequence, r.label] for r in recs]
+        else:
+            recs = [FASTARecord(defline=d, sequence=s) for d, s in records]
+            loaded = None
+        op = os.path.join(td, "out.txt")
+        n = eng.search(recs, op)
+        with open(op) as fh:
+            out = fh.read()
+    res = {"load_ok": True, "n_hits": n, "output": out,
+           "max_pcr_size": eng.max_pcr_size,
+           "n_records": len(eng.sts_records)}
+    if loaded is not None:
+        res["fasta"] = loaded
+    return res
+
+
+def unit_kats(rng):
+    MerPCR, _ = _ref()
+    kat = {"hash": [], "revcomp": [], "compare": [], "pcr_size": []}
+    for _ in range(400):
+        W = rng.randint(3, 16)
+        L = rng.randint(0, 30)
+        p = "".join(rng.choice("ACGTUacgtuNRYX-") if rng.random() < 0.15 else rng.choice("ACGT")
+                    for _ in range(L))
+        kat["hash"].append([p, W, list(MerPCR(wordsize=W)._hash_value(p))])
+    eng = MerPCR()
+    for _ in range(200):
+        s = "".join(rng.choice("ACGTUBDHKMNRSVWXYacgtubdhkmnrsvwxyZ-*1") for _ in range(rng.randint(0, 20)))
+        kat["revcomp"].append([s, eng._reverse_complement(s)])
+    alpha = "ACGTUacgtuRYMKSWBDHVNXZ-"
+    for _ in range(1500):
+        L = rng.randint(1, 12)
+        a = "".join(rng.choice(alpha) if rng.random() < 0.3 else rng.choice("ACGT") for _ in range(L))
+        b = list(a) if rng.random() < 0.7 else [rng.choice("ACGT") for _ in range(L)]
+        for _ in range(rng.randint(0, 3)):
+            b[rng.randrange(L)] = rng.choice(alpha)
+        b = "".join(b)
+        if rng.random() < 0.03:
+            b = b + "A"
+        N = rng.randint(0, 3)
+        X = rng.randint(0, 5)
+        I = rng.randint(0, 1)
+        strand = rng.choice("+-")
+        e = MerPCR(mismatches=N, three_prime_match=X, iupac_mode=I)
+        kat["compare"].append([a, b, strand, N, X, I, e._compare_seqs(a, b, strand)])
+    for f in ["100", "150-250", "0", "-5", "abc", "10-", "-", "1-2-3", "x-y", " 7", "7 ", "3",
+              "+9", "1_000", "٣", "100-200", "201-200", "5-5"]:
+        kat["pcr_size"].append([f, MerPCR(default_pcr_size=240)._parse_pcr_size(f)])
+    return kat
+
+
+def main():
+    logging.disable(logging.CRITICAL)
+    rng = random.Random(20261015)
+    sts_path = os.path.join(DATA, "test.sts")
+    fa_path = os.path.join(DATA, "test.fa")
+    with open(sts_path) as fh:
+        sts_text = fh.read()
+    with open(fa_path) as fh:
+        fa_text = fh.read()
+
+    bundled = []
+    variants = [{}, {"mismatches": 1}, {"mismatches": 2}, {"mismatches": 3, "three_prime_match": 0},
+                {"iupac_mode": 1, "mismatches": 2}, {"wordsize": 8}, {"wordsize": 16},
+                {"wordsize": 8, "mismatches": 3, "margin": 200}, {"margin": 0},
+                {"wordsize": 3, "margin": 10}]
+    for v in variants:
+        params = dict(wordsize=11, margin=50, mismatches=0, three_prime_match=1,
+                      iupac_mode=0, default_pcr_size=240)
+        params.update(v)
+        res = run_ref(params, sts_text, fasta_text=fa_text)
+        res.pop("fasta", None)
+        bundled.append({"params": params, **res})
+        print("bundled", v, res["n_hits"], file=sys.stderr)
+
+    repeat = {"params": dict(wordsize=4, margin=50, mismatches=0, three_prime_match=1,
+                             iupac_mode=0, default_pcr_size=240),
+              "sts_text": "REPEAT\tATCG\tCGAT\t20\n",
+              "records": [[">repeat", "ATCGCGAT" * 1000]]}
+    r = run_ref(repeat["params"], repeat["sts_text"], records=repeat["records"])
+    repeat.update(r)
+    repeat["sha256"] = hashlib.sha256(r["output"].encode()).hexdigest()
+    print("repeat", r["n_hits"], repeat["sha256"][:16], file=sys.stderr)
+
+    cases = []
+    for i in range(700):
+        params, sts, recs = gen_case(rng, i)
+        use_fasta = rng.random() < 0.25
+        if use_fasta:
+            ft = gen_fasta_text(rng, recs)
+            res = run_ref(params, sts, fasta_text=ft)
+            case = {"params": params, "sts_text": sts, "fasta_text": ft, **res}
+        else:
+            res = run_ref(params, sts, records=recs)
+            case = {"params": params, "sts_text": sts, "records": [list(x) for x in recs], **res}
+        cases.append(case)
+    tot = sum(c.get("n_hits", 0) for c in cases)
+    print("random cases", len(cases), "hits", tot, file=sys.stderr)
+
+    # IUPAC N-run explosion and record-end truncation, hand-built
+    special = []
+    p1, p2 = "ACGTTGCAAGCTTAGC", "GGATCCTTAGGCATCA"
+    seq = "ACGT" * 10 + p1 + "N" * 300 + "ACGT" * 10
+    for I in (0, 1):
+        prm = dict(wordsize=11, margin=50, mismatches=0, three_prime_match=1, iupac_mode=I,
+                   default_pcr_size=240)
+        st = f"NRUN\t{p1}\t{p2}\t200\n"
+        special.append({"params": prm, "sts_text": st, "records": [[">nrun", seq]],
+                        **run_ref(prm, st, records=[(">nrun", seq)])})
+    g = random.Random(7)
+    body = "".join(g.choice("ACGT") for _ in range(300))
+    tail = p2 + "".join(g.choice("ACGT") for _ in range(60)) + _rc(p1)
+    for cut in range(0, 40, 3):
+        s = body + tail[:len(tail) - cut] if cut else body + tail
+        prm = dict(wordsize=8, margin=50, mismatches=1, three_prime_match=1, iupac_mode=0,
+                   default_pcr_size=240)
+        st = f"END\t{p1}\t{p2}\t150\n"
+        special.append({"params": prm, "sts_text": st, "records": [[">end", s]],
+                        **run_ref(prm, st, records=[(">end", s)])})
+
+    # T>1 chunking artefacts (documentation of reference behaviour, not a parity target)
+    threaded = []
+    g = random.Random(11)
+    big = "".join(g.choice("ACGT") for _ in range(400000))
+    pp1, pp2 = "TTGACCGATAGCTAGGCA", "CATGCTAGGATCCAGTTA"
+    amp = pp2 + "".join(g.choice("ACGT") for _ in range(164)) + _rc(pp1)
+    big = list(big)
+    for pos in (1000, 99950, 199880, 299830, 399700):
+        big[pos:pos + len(amp)] = list(amp)
+    big = "".join(big)
+    prm = dict(wordsize=11, margin=50, mismatches=0, three_prime_match=1, iupac_mode=0,
+               default_pcr_size=240)
+    st = f"CHUNK\t{pp1}\t{pp2}\t200\n"
+    for T in (1, 4):
+        threaded.append({"params": prm, "threads": T, "sts_text": st,
+                         "records": [[">big", big]],
+                         **run_ref(prm, st, records=[(">big", big)], threads=T)})
+        print("threaded", T, threaded[-1]["n_hits"], file=sys.stderr)
+
+    kats = unit_kats(rng)
+
+    def dump(name, obj):
+        with gzip.open(os.path.join(HERE, name), "wt") as fh:
+            json.dump(obj, fh, separators=(",", ":"))
+
+    dump("bundled.json.gz", {"sts_sha256": hashlib.sha256(sts_text.encode()).hexdigest(),
+                             "fa_sha256": hashlib.sha256(fa_text.encode()).hexdigest(),
+                             "cases": bundled})
+    dump("repeat.json.gz", repeat)
+    dump("random_cases.json.gz", {"cases": cases})
+    dump("special_cases.json.gz", {"cases": special})
+    dump("threaded.json.gz", {"cases": threaded})
+    dump("unit_kats.json.gz", kats)
+
+
+if __name__ == "__main__":
+    main()
