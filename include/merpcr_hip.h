@@ -1,0 +1,126 @@
+/*
+ * merpcr_hip.h -- C ABI of libmerpcr_hip.so, the MI355X (gfx950) STS-search engine.
+ *
+ * The reference (FOI-Bioinformatics/merpcr) has no FFI layer; its hot path is the
+ * Python call chain MerPCR.search -> _process_thread -> _match_sts -> _compare_seqs
+ * (src/merpcr/core/engine.py:365-642), fed by the seed table that load_sts_file
+ * builds (engine.py:193-329) and by FASTALoader's filtered sequences
+ * (src/merpcr/io/fasta.py:18-71).  This header is the seam that replaces that chain:
+ * each entry point names the reference routine it stands in for.
+ *
+ * Conventions: plain pointers and sizes, no C++ or torch types.  Every function
+ * returns 0 on success and a negative MP_E* code on failure; mp_last_error()
+ * returns a thread-local message for the last failure.  `stream` is a hipStream_t
+ * passed as void* (NULL = the legacy default stream).  Handles are opaque and own
+ * their device memory; the caller owns every host buffer for the duration of a call.
+ */
+#ifndef MERPCR_HIP_H
+#define MERPCR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MP_ABI_VERSION 1
+
+#define MP_OK 0
+#define MP_E_ARG (-1)     /* bad argument (maps to ValueError) */
+#define MP_E_HIP (-2)     /* HIP runtime / device failure (RuntimeError) */
+#define MP_E_NOMEM (-3)   /* device or host allocation failed */
+#define MP_E_STATE (-4)   /* handle used out of order (e.g. search before seal) */
+#define MP_E_CAP (-5)     /* caller's output buffer too small; *n_hits has the need */
+
+/* Search parameters: the MerPCR constructor arguments that reach the hot path
+ * (engine.py:47-97).  Bounds are the reference's (W 3..16, N 0..10, M 0..10000,
+ * X >= 0, I 0/1). */
+typedef struct mp_params {
+    int32_t wordsize;          /* W  (-W) */
+    int32_t margin;            /* M  (-M) */
+    int32_t mismatches;        /* N  (-N) */
+    int32_t three_prime_match; /* X  (-X) */
+    int32_t iupac_mode;        /* I  (-I) */
+} mp_params;
+
+/* One hit in the reference's output order (engine.py:434-444): 0-based pos1/pos2
+ * relative to its sequence, the sequence's index in the genome handle, and the
+ * oriented STS record's index in MerPCR.sts_records. */
+typedef struct mp_hit {
+    uint64_t pos1;
+    uint64_t pos2;
+    uint32_t seq;
+    uint32_t rec;
+} mp_hit;
+
+/* Owned range of a search, in (sequence, amplicon start k) order: hits whose
+ * (seq, k) is >= (seq_begin, k_begin) and < (seq_end, k_end) are produced.  This is
+ * the unit of multi-GPU sharding; {0,0,n_seq,0} is the whole genome. */
+typedef struct mp_range {
+    uint32_t seq_begin;
+    uint32_t seq_end;      /* exclusive; k_end applies inside sequence seq_end */
+    uint64_t k_begin;
+    uint64_t k_end;
+} mp_range;
+
+/* ---- library ------------------------------------------------------------- */
+int32_t mp_abi_version(void);
+const char* mp_last_error(void);
+/* Number of visible HIP devices (0 on a host without a GPU). */
+int mp_device_count(int32_t* n);
+
+/* ---- seed table (replaces MerPCR.sts_table / sts_records, engine.py:193-329) --
+ * Records are the oriented STS records in sts_records order ('+' then '-' per STS
+ * line).  key/hash_off are _hash_value()'s (offset, value) for primer1
+ * (engine.py:331-355); pcr_size is the adjusted expected size (engine.py:245-247).
+ * primer1/primer2 bytes are the upper-cased primers of each record ('-' records
+ * carry primer2 = reverse complement, engine.py:272-279), concatenated, with
+ * CSR offsets p1_off[n_rec+1] / p2_off[n_rec+1].  Bytes >= 0x80 are opaque codes
+ * that match only an identical genome byte. */
+int mp_table_create(const mp_params* params, int32_t device, uint32_t n_rec,
+                    const uint32_t* key, const uint32_t* hash_off,
+                    const uint64_t* pcr_size,
+                    const uint8_t* primer1, const uint64_t* p1_off,
+                    const uint8_t* primer2, const uint64_t* p2_off,
+                    void** table_out);
+/* Table statistics: distinct keys, largest bucket, device bytes. */
+int mp_table_stats(void* table, uint64_t* n_keys, uint64_t* max_bucket, uint64_t* dev_bytes);
+void mp_table_destroy(void* table);
+
+/* ---- genome (replaces the per-record sequence strings that search() walks,
+ * engine.py:373-411, after FASTALoader filtering, fasta.py:60) ---------------
+ * Sequences are resident in HBM as a 2-bit plane + two 1-bit exception planes
+ * (0.375 B/base) + a sparse index of non-ACGT runs. */
+int mp_genome_create(int32_t device, uint32_t n_seq, const uint64_t* seq_len, void** genome_out);
+/* Pack bytes [offset, offset+nbytes) of sequence `seq` from HOST memory.  offset
+ * must be a multiple of 64.  Lower-case a-z is upper-cased (engine.py:455). */
+int mp_genome_put(void* genome, uint32_t seq, uint64_t offset, const uint8_t* host_bytes,
+                  uint64_t nbytes, void* stream);
+/* Same, from DEVICE memory on the genome's device. */
+int mp_genome_put_device(void* genome, uint32_t seq, uint64_t offset, const uint8_t* dev_bytes,
+                         uint64_t nbytes, void* stream);
+/* Build the exception-run index; required once after the last put. */
+int mp_genome_seal(void* genome, void* stream);
+int mp_genome_stats(void* genome, uint64_t* total_bases, uint64_t* n_exc_runs, uint64_t* dev_bytes);
+void mp_genome_destroy(void* genome);
+
+/* ---- search (replaces _process_thread/_match_sts/_compare_seqs and the
+ * sort of engine.py:434; T=1 semantics) ---------------------------------------
+ * A search handle owns the hit buffers for one (table, genome) pair. */
+int mp_search_create(void* table, void* genome, void** search_out);
+/* Scan, verify, pair-check and sort.  *n_hits receives the number of hits of
+ * the owned range (range NULL = whole genome).  Synchronises `stream`. */
+int mp_search_run(void* search, const mp_range* range, void* stream, uint64_t* n_hits);
+/* Copy the sorted hits of the last run to host memory (cap entries). */
+int mp_search_fetch(void* search, mp_hit* out, uint64_t cap, void* stream);
+/* Device pointer to the sorted hits of the last run (n_hits entries of mp_hit). */
+int mp_search_device_hits(void* search, const mp_hit** dev_hits);
+/* Duration of the last run's scan kernel (HIP events on the run's stream), the
+ * number of candidate seeds it verified and the windows it scanned. */
+int mp_search_last_stats(void* search, float* scan_ms, uint64_t* n_windows, uint64_t* n_candidates);
+void mp_search_destroy(void* search);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MERPCR_HIP_H */

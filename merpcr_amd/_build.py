@@ -1,0 +1,71 @@
+"""Build libmerpcr_hip.so in-tree with hipcc for gfx950 (no JIT cache, no torch)."""
+
+from __future__ import annotations
+
+import concurrent.futures
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(LIBDIR, "libmerpcr_hip.so")
+SOURCES = ["mp_table.hip", "mp_genome.hip", "mp_search.hip", "mp_sort.hip"]
+HEADERS = ["mp_internal.h", os.path.join("..", "..", "include", "merpcr_hip.h")]
+ARCH = os.environ.get("MERPCR_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the MI355X engine needs ROCm's hipcc to build")
+
+
+def _flags():
+    return ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+            "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include")]
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_native(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    cc = hipcc()
+    hdrs = [os.path.normpath(os.path.join(CSRC, h)) for h in HEADERS]
+    objs = []
+    jobs = []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        op = os.path.join(LIBDIR, src.replace(".hip", ".o"))
+        objs.append(op)
+        if force or _stale(op, [sp] + hdrs):
+            jobs.append([cc] + _flags() + ["-c", sp, "-o", op])
+    if jobs:
+        with concurrent.futures.ThreadPoolExecutor(max_workers=min(4, len(jobs))) as ex:
+            for cmd, res in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):
+                if verbose or res.returncode:
+                    print(" ".join(cmd))
+                    print(res.stdout + res.stderr)
+                if res.returncode:
+                    raise RuntimeError(f"hipcc failed for {cmd[-3]}")
+    if force or jobs or _stale(LIB, objs):
+        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode:
+            print(" ".join(cmd))
+            print(res.stdout + res.stderr)
+            raise RuntimeError("hipcc link failed")
+    return LIB
+
+
+if __name__ == "__main__":
+    import sys
+    print(build_native(force="--force" in sys.argv, verbose="-v" in sys.argv))

@@ -1,0 +1,234 @@
+"""ctypes binding of libmerpcr_hip.so (include/merpcr_hip.h).
+
+The engine has no CPU fallback: if the library is missing, or no HIP device is
+visible when a search runs, the calls raise.  Nothing here imports torch.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_uint8, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "_lib", "libmerpcr_hip.so")
+
+MP_OK = 0
+MP_E_ARG = -1
+MP_E_HIP = -2
+MP_E_NOMEM = -3
+MP_E_STATE = -4
+MP_E_CAP = -5
+
+# every symbol include/merpcr_hip.h declares
+EXPORTS = (
+    "mp_abi_version", "mp_last_error", "mp_device_count",
+    "mp_table_create", "mp_table_stats", "mp_table_destroy",
+    "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
+    "mp_genome_stats", "mp_genome_destroy",
+    "mp_search_create", "mp_search_run", "mp_search_fetch", "mp_search_device_hits",
+    "mp_search_last_stats", "mp_search_destroy",
+)
+
+
+class MPParams(ctypes.Structure):
+    _fields_ = [("wordsize", c_int32), ("margin", c_int32), ("mismatches", c_int32),
+                ("three_prime_match", c_int32), ("iupac_mode", c_int32)]
+
+
+class MPRange(ctypes.Structure):
+    _fields_ = [("seq_begin", c_uint32), ("seq_end", c_uint32),
+                ("k_begin", c_uint64), ("k_end", c_uint64)]
+
+
+HIT_DTYPE = np.dtype([("pos1", "<u8"), ("pos2", "<u8"), ("seq", "<u4"), ("rec", "<u4")])
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libmerpcr_hip error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def _sig(lib):
+    P = c_void_p
+    u64p = POINTER(c_uint64)
+    lib.mp_abi_version.restype = c_int32
+    lib.mp_last_error.restype = c_char_p
+    lib.mp_device_count.argtypes = [POINTER(c_int32)]
+    lib.mp_table_create.argtypes = [POINTER(MPParams), c_int32, c_uint32, P, P, P, P, P, P, P,
+                                    POINTER(c_void_p)]
+    lib.mp_table_stats.argtypes = [P, u64p, u64p, u64p]
+    lib.mp_table_destroy.argtypes = [P]
+    lib.mp_table_destroy.restype = None
+    lib.mp_genome_create.argtypes = [c_int32, c_uint32, P, POINTER(c_void_p)]
+    lib.mp_genome_put.argtypes = [P, c_uint32, c_uint64, P, c_uint64, P]
+    lib.mp_genome_put_device.argtypes = [P, c_uint32, c_uint64, P, c_uint64, P]
+    lib.mp_genome_seal.argtypes = [P, P]
+    lib.mp_genome_stats.argtypes = [P, u64p, u64p, u64p]
+    lib.mp_genome_destroy.argtypes = [P]
+    lib.mp_genome_destroy.restype = None
+    lib.mp_search_create.argtypes = [P, P, POINTER(c_void_p)]
+    lib.mp_search_run.argtypes = [P, POINTER(MPRange), P, u64p]
+    lib.mp_search_fetch.argtypes = [P, P, c_uint64, P]
+    lib.mp_search_device_hits.argtypes = [P, POINTER(c_void_p)]
+    lib.mp_search_last_stats.argtypes = [P, POINTER(c_float), u64p, u64p]
+    lib.mp_search_destroy.argtypes = [P]
+    lib.mp_search_destroy.restype = None
+    for name in EXPORTS:
+        f = getattr(lib, name)
+        if f.restype is ctypes.c_int and name not in ("mp_abi_version",):
+            f.restype = c_int
+
+
+def lib():
+    """The loaded library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(the MI355X engine has no CPU fallback)")
+        l = ctypes.CDLL(LIB_PATH)
+        _sig(l)
+        if l.mp_abi_version() != 1:
+            raise RuntimeError("libmerpcr_hip ABI version mismatch")
+        _lib = l
+    return _lib
+
+
+def check(rc: int):
+    if rc != MP_OK:
+        msg = lib().mp_last_error().decode(errors="replace")
+        if rc == MP_E_ARG:
+            raise ValueError(msg)
+        raise NativeError(rc, msg)
+
+
+def device_count() -> int:
+    n = c_int32(0)
+    check(lib().mp_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def ptr(a: np.ndarray) -> c_void_p:
+    return c_void_p(a.ctypes.data) if a.size else c_void_p(0)
+
+
+class Table:
+    """Device seed table (owns the native handle)."""
+
+    def __init__(self, params: MPParams, device: int, key, hash_off, pcr_size, p1, p1_off, p2, p2_off):
+        self._h = c_void_p()
+        self.n_rec = len(key)
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        hash_off = np.ascontiguousarray(hash_off, dtype=np.uint32)
+        pcr_size = np.ascontiguousarray(pcr_size, dtype=np.uint64)
+        p1 = np.ascontiguousarray(p1, dtype=np.uint8)
+        p2 = np.ascontiguousarray(p2, dtype=np.uint8)
+        p1_off = np.ascontiguousarray(p1_off, dtype=np.uint64)
+        p2_off = np.ascontiguousarray(p2_off, dtype=np.uint64)
+        self.params = params
+        check(lib().mp_table_create(ctypes.byref(params), device, self.n_rec, ptr(key), ptr(hash_off),
+                                    ptr(pcr_size), ptr(p1), ptr(p1_off), ptr(p2), ptr(p2_off),
+                                    ctypes.byref(self._h)))
+
+    def stats(self):
+        a, b, c = c_uint64(), c_uint64(), c_uint64()
+        check(lib().mp_table_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return {"n_keys": a.value, "max_bucket": b.value, "dev_bytes": c.value}
+
+    def close(self):
+        if self._h:
+            lib().mp_table_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Genome:
+    """Sequences resident in HBM as 2-bit + exception planes."""
+
+    def __init__(self, device: int, lengths):
+        self._h = c_void_p()
+        self.lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        check(lib().mp_genome_create(device, len(self.lengths), ptr(self.lengths), ctypes.byref(self._h)))
+
+    def put(self, seq: int, data: bytes, offset: int = 0, stream=None):
+        buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        check(lib().mp_genome_put(self._h, seq, offset, ptr(buf), buf.size, c_void_p(stream or 0)))
+
+    def put_device(self, seq: int, dev_ptr: int, nbytes: int, offset: int = 0, stream=None):
+        check(lib().mp_genome_put_device(self._h, seq, offset, c_void_p(dev_ptr), nbytes, c_void_p(stream or 0)))
+
+    def seal(self, stream=None):
+        check(lib().mp_genome_seal(self._h, c_void_p(stream or 0)))
+
+    def stats(self):
+        a, b, c = c_uint64(), c_uint64(), c_uint64()
+        check(lib().mp_genome_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return {"bases": a.value, "exc_runs": b.value, "dev_bytes": c.value}
+
+    def close(self):
+        if self._h:
+            lib().mp_genome_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Search:
+    def __init__(self, table: Table, genome: Genome):
+        self._h = c_void_p()
+        self.table = table
+        self.genome = genome
+        check(lib().mp_search_create(table._h, genome._h, ctypes.byref(self._h)))
+
+    def run(self, rng=None, stream=None) -> int:
+        n = c_uint64(0)
+        r = None
+        if rng is not None:
+            r = MPRange(*rng)
+        check(lib().mp_search_run(self._h, ctypes.byref(r) if r is not None else None,
+                                  c_void_p(stream or 0), ctypes.byref(n)))
+        return n.value
+
+    def fetch(self, n: int, stream=None) -> np.ndarray:
+        out = np.empty(n, dtype=HIT_DTYPE)
+        check(lib().mp_search_fetch(self._h, ptr(out), n, c_void_p(stream or 0)))
+        return out
+
+    def device_hits(self) -> int:
+        p = c_void_p()
+        check(lib().mp_search_device_hits(self._h, ctypes.byref(p)))
+        return p.value or 0
+
+    def last_stats(self):
+        ms, nw, nc = c_float(), c_uint64(), c_uint64()
+        check(lib().mp_search_last_stats(self._h, ctypes.byref(ms), ctypes.byref(nw), ctypes.byref(nc)))
+        return {"scan_ms": ms.value, "windows": nw.value, "candidates": nc.value}
+
+    def close(self):
+        if self._h:
+            lib().mp_search_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,381 @@
+"""MerPCR -- drop-in search engine whose hot path runs on MI355X.
+
+Same constructor, attributes and methods as the reference class
+(src/merpcr/core/engine.py:44-642).  ``load_sts_file`` and the primer helpers
+are host-side bookkeeping with the reference's exact semantics; ``search``
+hands the seed table and the sequences to libmerpcr_hip.so (HIP kernels on the
+GPU) and only formats the sorted hits it gets back.  There is no CPU search
+path: without the library or a HIP device, ``search`` raises.
+
+Output order and content follow the reference's single-chunk (``-T 1``)
+semantics for every record; see DESIGN.md ("Threads") for the documented
+difference from the reference's multi-process chunking when threads > 1.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import sys
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..io.fasta import FASTALoader
+from .encode import CharCodes
+from .models import FASTARecord, STSHit, STSRecord, ThreadData
+
+AMBIG = 100
+MIN_FILESIZE_FOR_THREADING = 100000
+
+DEFAULT_MARGIN = 50
+DEFAULT_WORDSIZE = 11
+DEFAULT_MISMATCHES = 0
+DEFAULT_THREE_PRIME_MATCH = 1
+DEFAULT_IUPAC_MODE = 0
+DEFAULT_THREADS = 1
+DEFAULT_PCR_SIZE = 240
+
+MIN_WORDSIZE = 3
+MAX_WORDSIZE = 16
+MIN_MISMATCHES = 0
+MAX_MISMATCHES = 10
+MIN_MARGIN = 0
+MAX_MARGIN = 10000
+MIN_THREE_PRIME_MATCH = 0
+MIN_PCR_SIZE = 1
+MAX_PCR_SIZE = 10000
+
+logger = logging.getLogger(__name__)
+
+_CODE2 = {"A": 0, "C": 1, "G": 2, "T": 3, "U": 3}
+_COMPL_BASE = {"A": "T", "C": "G", "G": "C", "T": "A", "U": "A", "B": "V", "D": "H",
+               "H": "D", "K": "M", "M": "K", "N": "N", "R": "Y", "S": "S", "V": "B",
+               "W": "W", "X": "X", "Y": "R"}
+_IUPAC_SETS = {"A": "A", "C": "C", "G": "G", "T": "TU", "U": "TU", "R": "AGR", "Y": "CTUY",
+               "M": "ACM", "K": "GTUK", "S": "CGS", "W": "ATUW", "B": "CGTUYKSB",
+               "D": "AGTURKWD", "H": "ACTUYMWH", "V": "ACGRMSV", "N": "ACGTURYMKSWBDHVN"}
+
+
+class MerPCR:
+    """Electronic-PCR STS search (reference: core/engine.py:44)."""
+
+    def __init__(self, wordsize: int = DEFAULT_WORDSIZE, margin: int = DEFAULT_MARGIN,
+                 mismatches: int = DEFAULT_MISMATCHES,
+                 three_prime_match: int = DEFAULT_THREE_PRIME_MATCH,
+                 iupac_mode: int = DEFAULT_IUPAC_MODE, default_pcr_size: int = DEFAULT_PCR_SIZE,
+                 threads: int = DEFAULT_THREADS, max_sts_line_length: int = 1022,
+                 device: Optional[int] = None):
+        self.wordsize = wordsize
+        self.margin = margin
+        self.mismatches = mismatches
+        self.three_prime_match = three_prime_match
+        self.iupac_mode = iupac_mode
+        self.default_pcr_size = default_pcr_size
+        self.threads = threads
+        self.max_sts_line_length = max_sts_line_length
+        self.device = 0 if device is None else int(device)
+
+        self.sts_records: List[STSRecord] = []
+        self.sts_table: Dict[int, List[STSRecord]] = {}
+        self.max_pcr_size = 0
+        self.total_hits = 0
+        self._sts_keys: List[int] = []
+        self._dev_table = None
+        self._dev_table_sig = None
+        self._codes = CharCodes()
+        self.last_search_stats: dict = {}
+
+        self._init_lookup_tables()
+        self._validate_parameters()
+
+    # ------------------------------------------------------------------ setup
+    def _validate_parameters(self):
+        """Parameter bounds and messages of engine.py:80-97."""
+        if not (MIN_WORDSIZE <= self.wordsize <= MAX_WORDSIZE):
+            raise ValueError(f"Word size must be between {MIN_WORDSIZE} and {MAX_WORDSIZE}")
+        if not (MIN_MISMATCHES <= self.mismatches <= MAX_MISMATCHES):
+            raise ValueError(f"Number of mismatches must be between {MIN_MISMATCHES} and {MAX_MISMATCHES}")
+        if not (MIN_MARGIN <= self.margin <= MAX_MARGIN):
+            raise ValueError(f"Margin must be between {MIN_MARGIN} and {MAX_MARGIN}")
+        if self.three_prime_match < MIN_THREE_PRIME_MATCH:
+            raise ValueError(f"Three prime match must be at least {MIN_THREE_PRIME_MATCH}")
+        if not (MIN_PCR_SIZE <= self.default_pcr_size <= MAX_PCR_SIZE):
+            raise ValueError(f"Default PCR size must be between {MIN_PCR_SIZE} and {MAX_PCR_SIZE}")
+
+    def _init_lookup_tables(self):
+        """Host tables of engine.py:99-191 (scode, compl, iupac_mapping, ambig)."""
+        self.scode = [AMBIG] * 256
+        for ch, c in _CODE2.items():
+            self.scode[ord(ch)] = self.scode[ord(ch.lower())] = c
+        self.compl = {}
+        for k, v in _COMPL_BASE.items():
+            self.compl[k] = v
+            self.compl[k.lower()] = v.lower()
+        self.iupac_mapping = dict(_IUPAC_SETS)
+        self.iupac_mapping.update({k.lower(): v for k, v in _IUPAC_SETS.items()})
+        self.ambig = {b: True for b in "BDHKMNRSVWXYbdhkmnrsvwxy"}
+
+    # ------------------------------------------------------------------ STS file
+    def load_sts_file(self, filename: str) -> bool:
+        """Parse an STS file into oriented records (engine.py:193-302)."""
+        start = time.time()
+        if os.path.getsize(filename) == 0:
+            logger.error(f"STS file '{filename}' is empty")
+            return False
+        logger.info(f"Reading STS file: {filename}")
+        self.sts_records = []
+        self.sts_table = {}
+        self._sts_keys = []
+        self.max_pcr_size = 0
+        self._dev_table = None
+        short = ambig = badsize = 0
+        W = self.wordsize
+        with open(filename, "r") as fh:
+            lines = fh.readlines()
+        for line_no, raw in enumerate(lines, 1):
+            line = raw.strip()
+            if not line or line.startswith("#"):
+                continue
+            fields = line.split("\t")
+            if len(fields) < 4:
+                logger.error(f"Bad STS file format at line {line_no}. Expected at least 4 fields.")
+                return False
+            sts_id = fields[0]
+            p1 = fields[1].upper()
+            p2 = fields[2].upper()
+            size = self._parse_pcr_size(fields[3])
+            alias = fields[4] if len(fields) > 4 else ""
+            if len(p1) < W or len(p2) < W:
+                short += 1
+                continue
+            if len(p1) + len(p2) > size:
+                badsize += 1
+                size = len(p1) + len(p2)
+            if size > self.max_pcr_size:
+                self.max_pcr_size = size
+            off1, key1 = self._hash_value(p1)
+            if off1 >= 0:
+                self._insert_sts(STSRecord(id=sts_id, primer1=p1, primer2=p2, pcr_size=size,
+                                           alias=alias, offset=line_no, hash_offset=off1,
+                                           direct="+"), key1)
+            else:
+                ambig += 1
+            rc1 = self._reverse_complement(p1)
+            off2, key2 = self._hash_value(p2)
+            if off2 >= 0:
+                self._insert_sts(STSRecord(id=sts_id, primer1=p2, primer2=rc1, pcr_size=size,
+                                           alias=alias, offset=line_no, hash_offset=off2,
+                                           direct="-"), key2)
+            else:
+                ambig += 1
+        if short:
+            logger.warning(f"{short} STSs have primer shorter than word size ({W}): not included in search")
+        if ambig:
+            logger.warning(f"{ambig} primers have ambiguities which prevent computation of a hash value: "
+                           "not included in search")
+        if badsize:
+            logger.warning(f"{badsize} STSs have a primer length sum greater than the pcr size: "
+                           "expected pcr size adjusted")
+        logger.info(f"Loaded {len(self.sts_records)} STS records in {time.time() - start:.2f} seconds")
+        return True
+
+    def _parse_pcr_size(self, pcr_size_str: str) -> int:
+        """'a-b' -> midpoint, int > 0 as is, else the default (engine.py:304-322)."""
+        if "-" in pcr_size_str:
+            parts = pcr_size_str.split("-")
+            if len(parts) == 2 and parts[0] and parts[1]:
+                try:
+                    return (int(parts[0]) + int(parts[1])) // 2
+                except ValueError:
+                    return self.default_pcr_size
+            return self.default_pcr_size
+        try:
+            v = int(pcr_size_str)
+        except ValueError:
+            return self.default_pcr_size
+        return v if v > 0 else self.default_pcr_size
+
+    def _insert_sts(self, sts: STSRecord, hash_value: int):
+        """Append to the key's bucket and the flat record list (engine.py:324-329)."""
+        self.sts_table.setdefault(hash_value, []).append(sts)
+        self.sts_records.append(sts)
+        self._sts_keys.append(hash_value)
+
+    def _hash_value(self, primer: str) -> Tuple[int, int]:
+        """(offset, value) of the first all-ACGTU W-mer (engine.py:331-355)."""
+        p = primer.upper()
+        W = self.wordsize
+        if len(p) < W:
+            return -1, 0
+        run = 0
+        v = 0
+        mask = (1 << (2 * W)) - 1
+        for i, ch in enumerate(p):
+            c = _CODE2.get(ch)
+            if c is None:
+                run = 0
+                v = 0
+                continue
+            v = ((v << 2) | c) & mask
+            run += 1
+            if run >= W:
+                return i - W + 1, v
+        return -1, 0
+
+    def _reverse_complement(self, sequence: str) -> str:
+        """Reverse complement, unknown characters -> 'N' (engine.py:357-359)."""
+        compl = self.compl
+        return "".join(compl.get(b, "N") for b in reversed(sequence))
+
+    def _compare_seqs(self, seq1: str, seq2: str, strand: str) -> bool:
+        """Host copy of the primer compare rule (engine.py:599-642).
+
+        Kept for API compatibility; the search itself runs this rule on the GPU
+        (merpcr_amd/csrc/mp_search.hip, primer_ok)."""
+        if len(seq1) != len(seq2):
+            return False
+        L = len(seq1)
+        X = self.three_prime_match
+        mm = 0
+        for i in range(L):
+            a = seq1[i].upper()
+            b = seq2[i].upper()
+            if self.iupac_mode and a in self.iupac_mapping and b in self.iupac_mapping:
+                ok = not set(self.iupac_mapping[a]).isdisjoint(self.iupac_mapping[b])
+            else:
+                ok = a == b
+            if not ok:
+                if (strand == "+" and i >= L - X) or (strand == "-" and i < X):
+                    return False
+                mm += 1
+                if mm > self.mismatches:
+                    return False
+        return True
+
+    def load_fasta_file(self, filename: str) -> List[FASTARecord]:
+        """FASTA records with the reference's filter (io/fasta.py:18-71)."""
+        return FASTALoader.load_file(filename)
+
+    # ------------------------------------------------------------------ device
+    def _params(self):
+        from .._native import MPParams
+        return MPParams(self.wordsize, self.margin, self.mismatches, self.three_prime_match,
+                        self.iupac_mode)
+
+    def _table_arrays(self):
+        """Record arrays for mp_table_create in sts_records order."""
+        recs = self.sts_records
+        if len(self._sts_keys) != len(recs):
+            self._sts_keys = [self._hash_value(r.primer1)[1] for r in recs]
+        key = np.asarray(self._sts_keys, dtype=np.uint32)
+        hash_off = np.fromiter((r.hash_offset for r in recs), dtype=np.uint32, count=len(recs))
+        size = np.fromiter((r.pcr_size for r in recs), dtype=np.uint64, count=len(recs))
+        p1 = [self._codes.primer_bytes(r.primer1) for r in recs]
+        p2 = [self._codes.primer_bytes(r.primer2) for r in recs]
+        p1_off = np.zeros(len(recs) + 1, dtype=np.uint64)
+        p2_off = np.zeros(len(recs) + 1, dtype=np.uint64)
+        if recs:
+            np.cumsum([len(b) for b in p1], out=p1_off[1:])
+            np.cumsum([len(b) for b in p2], out=p2_off[1:])
+        return (key, hash_off, size, np.frombuffer(b"".join(p1), dtype=np.uint8), p1_off,
+                np.frombuffer(b"".join(p2), dtype=np.uint8), p2_off)
+
+    def device_table(self):
+        """The seed table resident on this engine's GPU (rebuilt when stale)."""
+        from .. import _native
+        sig = (id(self.sts_records), len(self.sts_records), self.wordsize, self.margin,
+               self.mismatches, self.three_prime_match, self.iupac_mode, self.device)
+        if self._dev_table is None or self._dev_table_sig != sig:
+            self._dev_table = _native.Table(self._params(), self.device, *self._table_arrays())
+            self._dev_table_sig = sig
+        return self._dev_table
+
+    def encode_sequences(self, sequences: Sequence[str]) -> List[np.ndarray]:
+        return [self._codes.sequence_bytes(s) for s in sequences]
+
+    def find_hits(self, fasta_records: Sequence[FASTARecord]) -> np.ndarray:
+        """All hits of all records on the GPU, in output order.
+
+        Returns the structured array of mp_hit (pos1, pos2, seq, rec)."""
+        from .. import _native
+        table = self.device_table()
+        data = self.encode_sequences([r.sequence for r in fasta_records])
+        genome = _native.Genome(self.device, [len(d) for d in data])
+        for i, d in enumerate(data):
+            if len(d):
+                genome.put(i, d)
+        genome.seal()
+        search = _native.Search(table, genome)
+        t0 = time.time()
+        n = search.run()
+        hits = search.fetch(n)
+        self.last_search_stats = dict(search.last_stats(), wall_s=time.time() - t0, hits=n)
+        search.close()
+        genome.close()
+        return hits
+
+    # ------------------------------------------------------------------ search
+    def _log_thread_plan(self, seq_len: int):
+        """Reference's per-record thread-planning log lines (engine.py:380-392)."""
+        t = self.threads
+        if seq_len < MIN_FILESIZE_FOR_THREADING:
+            logger.info("Sequence too small for threading, using single thread.")
+            t = 1
+        overlap = self.max_pcr_size + self.margin - 1
+        while t > 1 and (t + 1) * overlap > seq_len:
+            t -= 1
+            logger.info(f"Reduced threads to {t} due to sequence size limitations")
+
+    def format_hits(self, fasta_records: Sequence[FASTARecord], hits: np.ndarray) -> List[str]:
+        """Output lines exactly as engine.py:437-443 prints them."""
+        recs = self.sts_records
+        tails = {}
+        labels = [r.label for r in fasta_records]
+        out = []
+        for p1, p2, sq, ri in zip(hits["pos1"].tolist(), hits["pos2"].tolist(),
+                                  hits["seq"].tolist(), hits["rec"].tolist()):
+            tail = tails.get(ri)
+            if tail is None:
+                r = recs[ri]
+                tail = tails[ri] = f"\t{r.id}\t{r.alias}\t({r.direct})"
+            out.append(f"{labels[sq]}\t{p1 + 1}..{p2 + 1}{tail}")
+        return out
+
+    def hits_as_objects(self, hits: np.ndarray) -> List[STSHit]:
+        recs = self.sts_records
+        return [STSHit(pos1=int(h["pos1"]), pos2=int(h["pos2"]), sts=recs[int(h["rec"])]) for h in hits]
+
+    def search(self, fasta_records: List[FASTARecord], output_file: str = None) -> int:
+        """Search every record; print one line per hit (engine.py:365-451)."""
+        to_file = bool(output_file) and output_file.lower() != "stdout"
+        output = open(output_file, "w") if to_file else sys.stdout
+        try:
+            for rec in fasta_records:
+                logger.info(f"Processing sequence: {rec.label} ({len(rec.sequence)} bp)")
+                self._log_thread_plan(len(rec.sequence))
+            total = 0
+            if fasta_records:
+                hits = self.find_hits(fasta_records)
+                lines = self.format_hits(fasta_records, hits)
+                total = len(lines)
+                if lines:
+                    output.write("\n".join(lines) + "\n")
+        finally:
+            if to_file:
+                output.close()
+        logger.info(f"Total hits found: {total}")
+        self.total_hits = total
+        return total
+
+    # kept for surface compatibility with code that drives one chunk by hand
+    def _process_thread(self, thread_data: ThreadData) -> ThreadData:
+        """One chunk scanned as its own sequence (engine.py:453-505), on the GPU."""
+        rec = FASTARecord(defline=">chunk", sequence=thread_data.sequence, label="chunk")
+        hits = self.find_hits([rec])
+        for h in self.hits_as_objects(hits):
+            h.pos1 += thread_data.offset
+            h.pos2 += thread_data.offset
+            thread_data.hits.append(h)
+        return thread_data

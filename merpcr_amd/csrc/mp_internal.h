@@ -1,0 +1,199 @@
+// Internal definitions shared by the libmerpcr_hip translation units.
+//
+// Data layout in HBM (DESIGN.md "Data layout"):
+//   genome  g2   : 2 bits/base, big-endian inside each u64 (base j of a word at
+//                  bits [63-2j, 62-2j]), A=0 C=1 G=2 T=U=3, other = 0
+//           ginv : 1 bit/base, big-endian (bit 63-j), set where the base is not
+//                  A/C/G/T/U: such a base makes every W-mer through it unseeded
+//                  (engine.py:464-503)
+//           gexc : 1 bit/base, set where the base is not exactly A/C/G/T: the
+//                  primer compare must look the character up (engine.py:599-642)
+//           xr_* : sorted run index of the exception characters (start, char)
+//   Sequences are laid end to end, each padded to a multiple of 64 bases; the
+//   padding is marked ginv = gexc = 1.  A "global" coordinate is the index in
+//   that padded space.
+//   table   filt : seed-presence bitmap (direct 4^W bits for W <= 13, else a
+//                  hashed 2^27-bit filter), slots: open-addressed key -> bucket,
+//                  boff/blist: bucket CSR of record indices (insertion order),
+//                  recs: one 32-B DevRec per oriented STS record, primer accept
+//                  planes (4 x u64 per 32 primer bases) and raw primer bytes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/merpcr_hip.h"
+
+#define MP_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace mp {
+
+// ---------------------------------------------------------------- errors
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define MP_HIP_CHECK(expr)                                                     \
+    do {                                                                       \
+        hipError_t _e = (expr);                                                \
+        if (_e != hipSuccess)                                                  \
+            return ::mp::fail(MP_E_HIP, std::string(#expr) + ": " +            \
+                                            hipGetErrorString(_e));            \
+    } while (0)
+
+// ---------------------------------------------------------------- constants
+constexpr uint64_t kEven = 0x5555555555555555ull;  // the low bit of every 2-bit slot
+constexpr uint64_t kEmptySlot = ~0ull;
+constexpr int kHashedFilterLog2 = 27;               // 16 MiB hashed filter for W >= 14
+constexpr int kDirectFilterMaxW = 13;               // 4^13 bits = 8 MiB direct bitmap
+constexpr int kBlock = 256;                         // threads per scan workgroup
+constexpr int kWaves = kBlock / 64;
+constexpr int kStepsPerWave = 16;                   // 64-position steps per wave per tile
+constexpr uint32_t kTile = kWaves * 64 * kStepsPerWave;  // window positions per workgroup
+
+struct DevRec {            // one oriented STS record, 32 bytes
+    uint32_t hash_off;     // offset of the seed W-mer inside primer1
+    uint32_t l1, l2;       // primer lengths
+    uint32_t size;         // expected product size (clamped to u32)
+    uint32_t p1_pl, p2_pl; // first 32-base chunk of each primer in the plane array
+    uint32_t p1_ch, p2_ch; // byte offset of each primer in the raw primer array
+};
+static_assert(sizeof(DevRec) == 32, "DevRec layout");
+
+struct SeqSpan {           // per-sequence work description for one search run
+    uint64_t tile0;        // first workgroup index of this sequence
+    uint32_t seq;          // sequence index in the genome handle
+    uint32_t p_lo, p_hi;   // window positions [p_lo, p_hi) scanned
+    uint32_t pad;
+};
+
+// ---------------------------------------------------------------- handles
+struct Table {
+    mp_params prm{};
+    int device = 0;
+    uint32_t n_rec = 0;
+    uint64_t n_keys = 0, max_bucket = 0, dev_bytes = 0;
+    uint32_t max_hash_off = 0;
+    int filt_direct = 1;
+    uint32_t filt_log2 = 0;   // log2(filter bits)
+    uint32_t slot_log2 = 0;
+    uint32_t* filt = nullptr;
+    uint64_t* slots = nullptr;
+    uint32_t* boff = nullptr;
+    uint32_t* blist = nullptr;
+    DevRec* recs = nullptr;
+    uint32_t* rank = nullptr;      // rec -> position in (hash_off, rec) order
+    uint32_t* inv_rank = nullptr;  // position -> rec
+    uint64_t* planes = nullptr;    // 4 u64 per 32-base primer chunk
+    uint8_t* pchars = nullptr;
+    uint32_t rank_bits = 1;
+};
+
+struct Genome {
+    int device = 0;
+    uint32_t n_seq = 0;
+    std::vector<uint64_t> len, base;  // host copies
+    uint64_t total = 0;               // padded bases
+    uint64_t* g2 = nullptr;
+    uint64_t* gexc = nullptr;
+    uint64_t* ginv = nullptr;
+    uint64_t* d_base = nullptr;
+    uint64_t* d_len = nullptr;
+    uint64_t* xr_start = nullptr;
+    uint8_t* xr_char = nullptr;
+    uint64_t xr_cap = 0, n_xr = 0;
+    unsigned long long* d_counter = nullptr;  // run-count scratch
+    uint8_t* staging = nullptr;
+    uint64_t staging_cap = 0;
+    bool sealed = false;
+    uint64_t dev_bytes = 0;
+};
+
+struct Search {
+    Table* table = nullptr;
+    Genome* genome = nullptr;
+    uint64_t cap = 0;
+    uint64_t* keys = nullptr;    // 2 x u64 per raw hit (hi, lo), unsorted
+    uint64_t* tmp_hi = nullptr;  // sort buffers
+    uint64_t* tmp_lo = nullptr;
+    mp_hit* out = nullptr;
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    unsigned long long* counters = nullptr;  // [0] hits, [1] candidates
+    SeqSpan* spans = nullptr;
+    uint64_t spans_cap = 0;
+    uint64_t n_hits = 0;
+    uint64_t n_windows = 0, n_candidates = 0;
+    float scan_ms = 0.f;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+// ---------------------------------------------------------------- device helpers
+// 32 bases (64 bits) of the 2-bit plane starting at global base j, base j on top.
+__device__ __forceinline__ uint64_t ext2(const uint64_t* __restrict__ p, uint64_t j) {
+    const uint64_t w = j >> 5;
+    const uint32_t s = (uint32_t)(j & 31) * 2;
+    const uint64_t a = p[w];
+    const uint64_t b = p[w + 1];
+    return s ? (a << s) | (b >> (64 - s)) : a;
+}
+
+// 64 bits of a 1-bit plane starting at global base j, base j on top.
+__device__ __forceinline__ uint64_t ext1(const uint64_t* __restrict__ p, uint64_t j) {
+    const uint64_t w = j >> 6;
+    const uint32_t s = (uint32_t)(j & 63);
+    const uint64_t a = p[w];
+    const uint64_t b = p[w + 1];
+    return s ? (a << s) | (b >> (64 - s)) : a;
+}
+
+// Spaced mask (bit 62-2i) for primer-chunk positions i < b, 0 <= b <= 32.
+__device__ __forceinline__ uint64_t sp_lt(int b) {
+    return b <= 0 ? 0ull : (b >= 32 ? kEven : (kEven & (~0ull << (64 - 2 * b))));
+}
+
+__host__ __device__ __forceinline__ uint32_t iupac_mask(uint8_t c) {
+    // A=1 C=2 G=4 T=U=8 (engine.py:138-172 expansion sets, as bit masks)
+    switch (c) {
+        case 'A': return 1; case 'C': return 2; case 'G': return 4;
+        case 'T': case 'U': return 8;
+        case 'R': return 5; case 'Y': return 10; case 'M': return 3; case 'K': return 12;
+        case 'S': return 6; case 'W': return 9; case 'B': return 14; case 'D': return 13;
+        case 'H': return 11; case 'V': return 7; case 'N': return 15;
+        default: return 0;
+    }
+}
+
+// engine.py:613-631: one genome character against one primer character.
+__host__ __device__ __forceinline__ bool char_match(uint8_t g, uint8_t c, int iupac) {
+    if (iupac) {
+        const uint32_t mg = iupac_mask(g), mc = iupac_mask(c);
+        if (mg && mc) return (mg & mc) != 0;
+    }
+    return g == c;
+}
+
+__host__ __device__ __forceinline__ uint32_t table_slot(uint32_t key, uint32_t log2cap) {
+    return (uint32_t)(((uint64_t)key * 0x9E3779B97F4A7C15ull) >> (64 - log2cap));
+}
+
+__host__ __device__ __forceinline__ uint32_t filter_index(uint32_t key, uint32_t log2bits) {
+    return (uint32_t)(((uint64_t)key * 0xD6E8FEB86659FD93ull) >> (64 - log2bits));
+}
+
+__host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {
+    return d == 0 ? 0u : (d < 0 ? (uint32_t)(-2 * d - 1) : (uint32_t)(2 * d));
+}
+
+__host__ __device__ __forceinline__ int32_t try_offset(uint32_t r) {
+    return r == 0 ? 0 : ((r & 1) ? -(int32_t)((r + 1) >> 1) : (int32_t)(r >> 1));
+}
+
+inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
+
+// internal entry points shared across TUs
+int sort_hits(Search* s, uint64_t n, hipStream_t st);
+int sort_runs(Genome* g, hipStream_t st);
+
+}  // namespace mp

@@ -1,0 +1,86 @@
+// Device sorts (rocPRIM radix sort; kept in its own translation unit because of
+// its compile time).
+//
+// sort_hits puts the raw hits of a run into the reference's output order: the
+// stable sort on pos1 at src/merpcr/core/engine.py:434 applied to discovery
+// order is the lexicographic order (sequence, k, hash_offset, record, try rank)
+// -- SURVEY 8a-8.  Hits carry it as a 128-bit key (hi = global k coordinate,
+// lo = rank(record) << 32 | try rank) and two stable LSD passes order them.
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "mp_internal.h"
+
+namespace mp {
+
+static unsigned bits_for(uint64_t v) {
+    unsigned b = 1;
+    while (b < 64 && (v >> b)) ++b;
+    return b;
+}
+
+static int ensure_tmp(void** p, size_t* have, size_t need) {
+    if (need <= *have) return MP_OK;
+    hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    MP_HIP_CHECK(hipMalloc(p, need));
+    *have = need;
+    return MP_OK;
+}
+
+int sort_hits(Search* s, uint64_t n, hipStream_t st) {
+    if (n < 2) return MP_OK;
+    uint64_t* hi = s->keys;
+    uint64_t* lo = s->keys + s->cap;
+    const unsigned lo_bits = 32 + s->table->rank_bits;
+    const unsigned hi_bits = bits_for(s->genome->total);
+    size_t need1 = 0, need2 = 0;
+    MP_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, need1, lo, s->tmp_lo, hi, s->tmp_hi, (size_t)n,
+                                           0, lo_bits, st));
+    MP_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, need2, s->tmp_hi, hi, s->tmp_lo, lo, (size_t)n,
+                                           0, hi_bits, st));
+    int rc = ensure_tmp(&s->sort_tmp, &s->sort_tmp_bytes, std::max(need1, need2));
+    if (rc) return rc;
+    size_t b1 = s->sort_tmp_bytes, b2 = s->sort_tmp_bytes;
+    // pass 1: by lo (record rank, try rank), carrying hi
+    MP_HIP_CHECK(rocprim::radix_sort_pairs(s->sort_tmp, b1, lo, s->tmp_lo, hi, s->tmp_hi, (size_t)n,
+                                           0, lo_bits, st));
+    // pass 2: stable by hi (global k), carrying lo; result back in (hi, lo)
+    MP_HIP_CHECK(rocprim::radix_sort_pairs(s->sort_tmp, b2, s->tmp_hi, hi, s->tmp_lo, lo, (size_t)n,
+                                           0, hi_bits, st));
+    return MP_OK;
+}
+
+// Exception runs may be appended out of order by separate puts: order them by start.
+int sort_runs(Genome* g, hipStream_t st) {
+    const uint64_t n = g->n_xr;
+    if (n < 2) return MP_OK;
+    uint64_t* ks = nullptr;
+    uint8_t* vs = nullptr;
+    void* tmp = nullptr;
+    size_t tb = 0;
+    int rc = MP_OK;
+    do {
+        if (hipMalloc(&ks, n * 8) != hipSuccess || hipMalloc(&vs, n) != hipSuccess) {
+            rc = fail(MP_E_NOMEM, "sort_runs: allocation failed");
+            break;
+        }
+        const unsigned kb = bits_for(g->total);
+        if (rocprim::radix_sort_pairs(nullptr, tb, g->xr_start, ks, g->xr_char, vs, (size_t)n, 0, kb, st) !=
+                hipSuccess ||
+            hipMalloc(&tmp, tb) != hipSuccess ||
+            rocprim::radix_sort_pairs(tmp, tb, g->xr_start, ks, g->xr_char, vs, (size_t)n, 0, kb, st) !=
+                hipSuccess ||
+            hipMemcpyAsync(g->xr_start, ks, n * 8, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(g->xr_char, vs, n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            rc = fail(MP_E_HIP, "sort_runs: device sort failed");
+        }
+    } while (0);
+    hipFree(ks);
+    hipFree(vs);
+    hipFree(tmp);
+    return rc;
+}
+
+}  // namespace mp

@@ -1,0 +1,236 @@
+// Seed table: host build + upload to HBM.
+//
+// Replaces MerPCR.sts_table / sts_records (src/merpcr/core/engine.py:193-329):
+// the Python host hands over the oriented records in sts_records order with the
+// (hash_offset, key) pair _hash_value computed for primer1 (engine.py:331-355);
+// this file turns them into the device structures the scan kernel probes.
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+
+#include "mp_internal.h"
+
+namespace mp {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg) {
+    set_error(msg);
+    return code;
+}
+
+template <class T>
+static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
+    const size_t nb = std::max<size_t>(n, 1) * sizeof(T);
+    MP_HIP_CHECK(hipMalloc((void**)dst, nb));
+    if (n) MP_HIP_CHECK(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    *bytes += nb;
+    return MP_OK;
+}
+
+static void free_table(Table* t) {
+    if (!t) return;
+    hipFree(t->filt); hipFree(t->slots); hipFree(t->boff); hipFree(t->blist);
+    hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
+    hipFree(t->pchars);
+    delete t;
+}
+
+static inline uint8_t upcase(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
+
+// Accept planes of one primer: for every 32-base chunk, four spaced masks telling
+// which genome base (A, C, G, T) satisfies the compare rule of engine.py:613-631
+// at each primer position; positions past the primer end accept everything.
+static void build_planes(const uint8_t* p, uint32_t L, int iupac, std::vector<uint64_t>& out) {
+    const uint32_t chunks = (L + 31) / 32;
+    for (uint32_t c = 0; c < chunks; ++c) {
+        uint64_t acc[4] = {0, 0, 0, 0};
+        for (uint32_t i = 0; i < 32; ++i) {
+            const uint32_t pos = c * 32 + i;
+            const int bit = 62 - 2 * (int)i;
+            if (pos >= L) {
+                for (int b = 0; b < 4; ++b) acc[b] |= 1ull << bit;
+                continue;
+            }
+            const uint8_t ch = upcase(p[pos]);
+            for (int b = 0; b < 4; ++b) {
+                if (char_match((uint8_t)"ACGT"[b], ch, iupac)) acc[b] |= 1ull << bit;
+            }
+        }
+        for (int b = 0; b < 4; ++b) out.push_back(acc[b]);
+    }
+}
+
+}  // namespace mp
+
+using namespace mp;
+
+MP_EXPORT int32_t mp_abi_version(void) { return MP_ABI_VERSION; }
+
+MP_EXPORT const char* mp_last_error(void) { return g_last_error.c_str(); }
+
+MP_EXPORT int mp_device_count(int32_t* n) {
+    if (!n) return fail(MP_E_ARG, "mp_device_count: null pointer");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = (e == hipSuccess) ? c : 0;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_rec,
+                              const uint32_t* key, const uint32_t* hash_off,
+                              const uint64_t* pcr_size, const uint8_t* primer1,
+                              const uint64_t* p1_off, const uint8_t* primer2,
+                              const uint64_t* p2_off, void** table_out) {
+    if (!prm || !table_out) return fail(MP_E_ARG, "mp_table_create: null pointer");
+    *table_out = nullptr;
+    const mp_params& p = *prm;
+    if (p.wordsize < 3 || p.wordsize > 16) return fail(MP_E_ARG, "Word size must be between 3 and 16");
+    if (p.mismatches < 0 || p.mismatches > 10)
+        return fail(MP_E_ARG, "Number of mismatches must be between 0 and 10");
+    if (p.margin < 0 || p.margin > 10000) return fail(MP_E_ARG, "Margin must be between 0 and 10000");
+    if (p.three_prime_match < 0) return fail(MP_E_ARG, "Three prime match must be at least 0");
+    if (p.iupac_mode != 0 && p.iupac_mode != 1) return fail(MP_E_ARG, "iupac_mode must be 0 or 1");
+    if (n_rec && (!key || !hash_off || !pcr_size || !primer1 || !p1_off || !primer2 || !p2_off))
+        return fail(MP_E_ARG, "mp_table_create: null record array");
+
+    Table* t = new Table();
+    t->prm = p;
+    t->device = device;
+    t->n_rec = n_rec;
+    int rc = MP_OK;
+    do {
+        if (hipSetDevice(device) != hipSuccess) { rc = fail(MP_E_HIP, "hipSetDevice failed"); break; }
+        const uint32_t W = (uint32_t)p.wordsize;
+        const uint64_t key_limit = (W == 16) ? (1ull << 32) : (1ull << (2 * W));
+
+        // ---- buckets in first-appearance order, records in insertion order
+        std::unordered_map<uint32_t, uint32_t> bucket_of;
+        bucket_of.reserve(n_rec * 2 + 16);
+        std::vector<uint32_t> bkey, bcount, rec_bucket(n_rec);
+        for (uint32_t r = 0; r < n_rec; ++r) {
+            if ((uint64_t)key[r] >= key_limit) { rc = fail(MP_E_ARG, "record key exceeds 4^W"); break; }
+            auto it = bucket_of.find(key[r]);
+            uint32_t b;
+            if (it == bucket_of.end()) {
+                b = (uint32_t)bkey.size();
+                bucket_of.emplace(key[r], b);
+                bkey.push_back(key[r]);
+                bcount.push_back(0);
+            } else {
+                b = it->second;
+            }
+            rec_bucket[r] = b;
+            bcount[b]++;
+        }
+        if (rc) break;
+        const uint32_t nb = (uint32_t)bkey.size();
+        t->n_keys = nb;
+        std::vector<uint32_t> boff(nb + 1, 0);
+        for (uint32_t b = 0; b < nb; ++b) {
+            boff[b + 1] = boff[b] + bcount[b];
+            t->max_bucket = std::max<uint64_t>(t->max_bucket, bcount[b]);
+        }
+        std::vector<uint32_t> fillp(boff.begin(), boff.end() - 1), blist(n_rec);
+        for (uint32_t r = 0; r < n_rec; ++r) blist[fillp[rec_bucket[r]]++] = r;
+
+        // ---- open-addressed key -> bucket slots (load <= 0.5)
+        uint32_t lg = 6;
+        while ((1ull << lg) < 2ull * nb) ++lg;
+        t->slot_log2 = lg;
+        std::vector<uint64_t> slots(1ull << lg, kEmptySlot);
+        for (uint32_t b = 0; b < nb; ++b) {
+            uint32_t s = table_slot(bkey[b], lg);
+            while (slots[s] != kEmptySlot) s = (s + 1) & ((1u << lg) - 1);
+            slots[s] = ((uint64_t)bkey[b] << 32) | b;
+        }
+
+        // ---- presence filter: direct bitmap for small W, hashed filter above
+        t->filt_direct = (W <= (uint32_t)kDirectFilterMaxW);
+        t->filt_log2 = t->filt_direct ? 2 * W : (uint32_t)kHashedFilterLog2;
+        std::vector<uint32_t> filt(std::max<uint64_t>((1ull << t->filt_log2) / 32, 1), 0);
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t idx = t->filt_direct ? bkey[b] : filter_index(bkey[b], t->filt_log2);
+            filt[idx >> 5] |= 1u << (idx & 31);
+        }
+
+        // ---- records, primer planes and bytes
+        std::vector<DevRec> recs(n_rec);
+        std::vector<uint64_t> planes;
+        std::vector<uint8_t> pchars;
+        for (uint32_t r = 0; r < n_rec; ++r) {
+            const uint64_t a1 = p1_off[r], b1 = p1_off[r + 1];
+            const uint64_t a2 = p2_off[r], b2 = p2_off[r + 1];
+            if (b1 < a1 || b2 < a2 || b1 - a1 > 65535 || b2 - a2 > 65535) {
+                rc = fail(MP_E_ARG, "primer length out of range (max 65535)");
+                break;
+            }
+            DevRec& d = recs[r];
+            d.l1 = (uint32_t)(b1 - a1);
+            d.l2 = (uint32_t)(b2 - a2);
+            d.hash_off = hash_off[r];
+            if ((uint64_t)d.hash_off + W > d.l1) { rc = fail(MP_E_ARG, "hash offset outside primer1"); break; }
+            d.size = (uint32_t)std::min<uint64_t>(pcr_size[r], 0xFFFFFFFFull);
+            if ((uint64_t)d.l1 + d.l2 > pcr_size[r]) {
+                rc = fail(MP_E_ARG, "pcr size below primer length sum");
+                break;
+            }
+            t->max_hash_off = std::max(t->max_hash_off, d.hash_off);
+            d.p1_pl = (uint32_t)(planes.size() / 4);
+            build_planes(primer1 + a1, d.l1, p.iupac_mode, planes);
+            d.p2_pl = (uint32_t)(planes.size() / 4);
+            build_planes(primer2 + a2, d.l2, p.iupac_mode, planes);
+            d.p1_ch = (uint32_t)pchars.size();
+            for (uint64_t i = a1; i < b1; ++i) pchars.push_back(upcase(primer1[i]));
+            d.p2_ch = (uint32_t)pchars.size();
+            for (uint64_t i = a2; i < b2; ++i) pchars.push_back(upcase(primer2[i]));
+            if (planes.size() / 4 > 0xFFFFFFF0ull || pchars.size() > 0xFFFFFFF0ull) {
+                rc = fail(MP_E_ARG, "primer set too large");
+                break;
+            }
+        }
+        if (rc) break;
+        // Ties at equal amplicon start are ordered by (hash_offset, record index):
+        // rank[] encodes that order in 32 bits for the device sort.
+        std::vector<uint32_t> order(n_rec), rank(n_rec);
+        for (uint32_t r = 0; r < n_rec; ++r) order[r] = r;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t a, uint32_t b) { return recs[a].hash_off < recs[b].hash_off; });
+        for (uint32_t i = 0; i < n_rec; ++i) rank[order[i]] = i;
+        t->rank_bits = 1;
+        while ((1ull << t->rank_bits) < (uint64_t)n_rec) ++t->rank_bits;
+
+        uint64_t bytes = 0;
+        if ((rc = upload(&t->filt, filt.data(), filt.size(), &bytes))) break;
+        if ((rc = upload(&t->slots, slots.data(), slots.size(), &bytes))) break;
+        if ((rc = upload(&t->boff, boff.data(), boff.size(), &bytes))) break;
+        if ((rc = upload(&t->blist, blist.data(), blist.size(), &bytes))) break;
+        if ((rc = upload(&t->recs, recs.data(), recs.size(), &bytes))) break;
+        if ((rc = upload(&t->rank, rank.data(), rank.size(), &bytes))) break;
+        if ((rc = upload(&t->inv_rank, order.data(), order.size(), &bytes))) break;
+        planes.push_back(0); planes.push_back(0); planes.push_back(0); planes.push_back(0);
+        if ((rc = upload(&t->planes, planes.data(), planes.size(), &bytes))) break;
+        pchars.push_back(0);
+        if ((rc = upload(&t->pchars, pchars.data(), pchars.size(), &bytes))) break;
+        t->dev_bytes = bytes;
+    } while (0);
+    if (rc) {
+        free_table(t);
+        return rc;
+    }
+    *table_out = t;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_table_stats(void* table, uint64_t* n_keys, uint64_t* max_bucket, uint64_t* dev_bytes) {
+    Table* t = (Table*)table;
+    if (!t) return fail(MP_E_ARG, "mp_table_stats: null table");
+    if (n_keys) *n_keys = t->n_keys;
+    if (max_bucket) *max_bucket = t->max_bucket;
+    if (dev_bytes) *dev_bytes = t->dev_bytes;
+    return MP_OK;
+}
+
+MP_EXPORT void mp_table_destroy(void* table) { free_table((Table*)table); }

@@ -1,0 +1,59 @@
+"""FASTA loading with the reference's exact character filter.
+
+The filter defines the coordinate system of every hit: io/fasta.py:60 of the
+reference keeps a character c iff ``c.upper() in "ACGTBDHKMNRSVWXY"``.  Over all
+of Unicode that is the 32 ASCII letters below plus U+017F (long s, upper 'S');
+U is dropped.  Lines are stripped, blank lines skipped, '>' starts a record,
+sequence lines before the first header are discarded (fasta.py:42-66).
+"""
+
+import logging
+import os
+import re
+import time
+from typing import List
+
+from ..core.models import FASTARecord
+
+logger = logging.getLogger(__name__)
+
+KEEP_CHARS = "ABCDGHKMNRSTVWXYabcdghkmnrstvwxyſ"
+_DROP = re.compile("[^" + re.escape(KEEP_CHARS) + "]+")
+
+
+def filter_line(line: str) -> str:
+    """Keep only the characters the reference's FASTA filter keeps."""
+    if line.isascii() and not _DROP.search(line):
+        return line
+    return _DROP.sub("", line)
+
+
+class FASTALoader:
+    """Loads FASTA files into FASTARecord lists (reference: io/fasta.py:15-71)."""
+
+    @staticmethod
+    def load_file(filename: str) -> List[FASTARecord]:
+        start = time.time()
+        if os.path.getsize(filename) == 0:
+            logger.error(f"FASTA file '{filename}' is empty")
+            return []
+        logger.info(f"Reading FASTA file: {filename}")
+        records: List[FASTARecord] = []
+        head = None
+        parts: List[str] = []
+        with open(filename, "r") as fh:
+            for raw in fh:
+                line = raw.strip()
+                if not line:
+                    continue
+                if line[0] == ">":
+                    if head is not None:
+                        records.append(FASTARecord(defline=head, sequence="".join(parts)))
+                    head = line
+                    parts = []
+                elif head is not None:
+                    parts.append(filter_line(line))
+        if head is not None:
+            records.append(FASTARecord(defline=head, sequence="".join(parts)))
+        logger.info(f"Loaded {len(records)} sequences in {time.time() - start:.2f} seconds")
+        return records

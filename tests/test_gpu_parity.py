@@ -1,0 +1,180 @@
+"""GPU parity: the HIP search path against the reference's golden outputs and the oracle.
+
+Every case runs MerPCR.search / find_hits, i.e. the C-ABI library on the GPU,
+and compares its output lines byte for byte with what the reference printed
+(tests/golden/*.json.gz, produced by tests/golden/make_golden.py) or with the
+CPU oracle (oracle/) on seeded synthetic inputs.
+"""
+
+import io
+import os
+import random
+import tempfile
+
+import numpy as np
+import pytest
+
+from merpcr_amd import FASTARecord, MerPCR
+from oracle import epcr_oracle as O
+from tests.golden_io import data_path, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(params):
+    return MerPCR(**params)
+
+
+def _load_sts(eng, text, td):
+    p = os.path.join(td, "x.sts")
+    with open(p, "w") as fh:
+        fh.write(text)
+    return eng.load_sts_file(p)
+
+
+def _records(case, eng, td):
+    if "fasta_text" in case:
+        p = os.path.join(td, "x.fa")
+        with open(p, "w", newline="") as fh:
+            fh.write(case["fasta_text"])
+        return eng.load_fasta_file(p)
+    return [FASTARecord(defline=d, sequence=s) for d, s in case["records"]]
+
+
+def _device_lines(eng, recs):
+    hits = eng.find_hits(recs)
+    return eng.format_hits(recs, hits)
+
+
+def test_library_loaded_and_device_visible():
+    from merpcr_amd import _native
+    assert _native.device_count() >= 1
+
+
+def test_bundled_kat():
+    g = load_golden("bundled.json.gz")
+    for case in g["cases"]:
+        eng = _engine(case["params"])
+        assert eng.load_sts_file(data_path("test.sts"))
+        recs = eng.load_fasta_file(data_path("test.fa"))
+        assert _device_lines(eng, recs) == case["output"].splitlines(), case["params"]
+
+
+def test_bundled_search_to_file():
+    eng = MerPCR(wordsize=11, mismatches=0, margin=50, threads=1)
+    assert eng.load_sts_file(data_path("test.sts"))
+    recs = eng.load_fasta_file(data_path("test.fa"))
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "o.txt")
+        n = eng.search(recs, out)
+        text = open(out).read()
+    assert n == 1 == eng.total_hits
+    assert text == "L78833\t75823..76023\tAFM248yg9\t(D17S932)  Chr.17, 63.7 cM\t(-)\n"
+
+
+def test_dense_repeat_order():
+    case = load_golden("repeat.json.gz")
+    eng = _engine(case["params"])
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, case["sts_text"], td)
+        recs = _records(case, eng, td)
+    lines = _device_lines(eng, recs)
+    assert len(lines) == 15936
+    assert lines == case["output"].splitlines()
+
+
+@pytest.mark.parametrize("name", ["random_cases.json.gz", "special_cases.json.gz"])
+def test_golden_corpus(name):
+    cases = load_golden(name)["cases"]
+    bad = []
+    for i, case in enumerate(cases):
+        eng = _engine(case["params"])
+        with tempfile.TemporaryDirectory() as td:
+            ok = _load_sts(eng, case["sts_text"], td)
+            assert ok == case["load_ok"], i
+            if not ok:
+                continue
+            recs = _records(case, eng, td)
+        lines = _device_lines(eng, recs)
+        if lines != case["output"].splitlines():
+            bad.append((i, case["params"], lines[:5], case["output"].splitlines()[:5]))
+    assert not bad, bad[:3]
+
+
+def _synthetic(seed, n_sts, glen, W, N, I, M=50, iupac_primers=False, nrun=False):
+    rng = random.Random(seed)
+    sts = []
+    seq = [rng.choice("ACGT") for _ in range(glen)]
+    if nrun:
+        for _ in range(glen // 5000):
+            a = rng.randrange(glen)
+            seq[a:a + rng.randint(10, 400)] = ["N"] * min(400, glen - a)
+            del seq[glen:]
+    for s in range(n_sts):
+        p1 = [rng.choice("ACGT") for _ in range(rng.randint(18, 25))]
+        p2 = [rng.choice("ACGT") for _ in range(rng.randint(18, 25))]
+        if iupac_primers:
+            for p in (p1, p2):
+                for _ in range(2):
+                    p[rng.randrange(len(p) - 12)] = rng.choice("RYSWKMN")
+        p1, p2 = "".join(p1), "".join(p2)
+        size = rng.randint(100, 400)
+        sts.append(f"S{s}\t{p1}\t{p2}\t{size}\talias{s}")
+        if rng.random() < 0.8:
+            amp = p2 + "".join(rng.choice("ACGT") for _ in range(size - len(p1) - len(p2) + rng.randint(-M, M)))
+            amp += O.revcomp(p1)
+            if N and rng.random() < 0.5:
+                amp = list(amp)
+                amp[rng.randrange(3, 10)] = rng.choice("ACGT")
+                amp = "".join(amp)
+            a = rng.randrange(max(1, glen - len(amp)))
+            seq[a:a + len(amp)] = list(amp.lower() if rng.random() < 0.3 else amp)
+            del seq[glen:]
+    return "\n".join(sts) + "\n", "".join(seq)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(seed=1, n_sts=300, glen=300_000, W=11, N=0, I=0),
+    dict(seed=2, n_sts=300, glen=300_000, W=11, N=1, I=0),
+    dict(seed=3, n_sts=200, glen=200_000, W=8, N=2, I=1, iupac_primers=True),
+    dict(seed=4, n_sts=200, glen=200_000, W=12, N=1, I=0, nrun=True),
+    dict(seed=5, n_sts=100, glen=150_000, W=16, N=3, I=1, nrun=True),
+])
+def test_synthetic_vs_oracle(cfg):
+    sts_text, seq = _synthetic(cfg["seed"], cfg["n_sts"], cfg["glen"], cfg["W"], cfg["N"], cfg["I"],
+                               iupac_primers=cfg.get("iupac_primers", False), nrun=cfg.get("nrun", False))
+    prm = dict(wordsize=cfg["W"], mismatches=cfg["N"], iupac_mode=cfg["I"], margin=50)
+    eng = MerPCR(**prm)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    recs = [FASTARecord(defline=">chrS", sequence=seq)]
+    got = _device_lines(eng, recs)
+    table = O.load_sts_lines(sts_text.splitlines(True), cfg["W"], 240)
+    exp = O.search_lines([("chrS", seq)], table, O.params(**prm))
+    assert len(exp) > 0
+    assert got == exp
+
+
+def test_sharded_ranges_concatenate_to_whole():
+    """Owned (seq, k) ranges partition the hit list exactly (multi-GPU invariant)."""
+    from merpcr_amd import _native
+    sts_text, seq = _synthetic(9, 200, 120_000, 10, 1, 0)
+    eng = MerPCR(wordsize=10, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    seqs = [seq[:50_000], seq[50_000:50_500], "", seq[50_500:]]
+    data = eng.encode_sequences(seqs)
+    genome = _native.Genome(0, [len(d) for d in data])
+    for i, d in enumerate(data):
+        if len(d):
+            genome.put(i, d)
+    genome.seal()
+    s = _native.Search(eng.device_table(), genome)
+    whole = s.fetch(s.run())
+    cuts = [(0, 0), (0, 17_001), (1, 100), (3, 0), (3, 33_333), (4, 0)]
+    parts = []
+    for (a, ka), (b, kb) in zip(cuts[:-1], cuts[1:]):
+        parts.append(s.fetch(s.run((a, b, ka, kb))))
+    cat = np.concatenate(parts)
+    assert len(whole) > 0
+    assert np.array_equal(cat, whole)
