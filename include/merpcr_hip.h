@@ -113,6 +113,9 @@ int mp_search_create(void* table, void* genome, void** search_out);
 int mp_search_run(void* search, const mp_range* range, void* stream, uint64_t* n_hits);
 /* Copy the sorted hits of the last run to host memory (cap entries). */
 int mp_search_fetch(void* search, mp_hit* out, uint64_t cap, void* stream);
+/* Copy the sorted hits of the last run into DEVICE memory on the search's GPU
+ * (e.g. a communication buffer for the multi-GPU gather). */
+int mp_search_fetch_device(void* search, mp_hit* dev_out, uint64_t cap, void* stream);
 /* Device pointer to the sorted hits of the last run (n_hits entries of mp_hit). */
 int mp_search_device_hits(void* search, const mp_hit** dev_hits);
 /* Duration of the last run's scan kernel (HIP events on the run's stream), the

@@ -28,7 +28,7 @@ EXPORTS = (
     "mp_table_create", "mp_table_stats", "mp_table_destroy",
     "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
     "mp_genome_stats", "mp_genome_destroy",
-    "mp_search_create", "mp_search_run", "mp_search_fetch", "mp_search_device_hits",
+    "mp_search_create", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
     "mp_search_last_stats", "mp_search_destroy",
 )
 
@@ -76,14 +76,11 @@ def _sig(lib):
     lib.mp_search_create.argtypes = [P, P, POINTER(c_void_p)]
     lib.mp_search_run.argtypes = [P, POINTER(MPRange), P, u64p]
     lib.mp_search_fetch.argtypes = [P, P, c_uint64, P]
+    lib.mp_search_fetch_device.argtypes = [P, P, c_uint64, P]
     lib.mp_search_device_hits.argtypes = [P, POINTER(c_void_p)]
     lib.mp_search_last_stats.argtypes = [P, POINTER(c_float), u64p, u64p]
     lib.mp_search_destroy.argtypes = [P]
     lib.mp_search_destroy.restype = None
-    for name in EXPORTS:
-        f = getattr(lib, name)
-        if f.restype is ctypes.c_int and name not in ("mp_abi_version",):
-            f.restype = c_int
 
 
 def lib():
@@ -211,6 +208,10 @@ class Search:
         out = np.empty(n, dtype=HIT_DTYPE)
         check(lib().mp_search_fetch(self._h, ptr(out), n, c_void_p(stream or 0)))
         return out
+
+    def fetch_device(self, dev_ptr: int, cap: int, stream=None):
+        """Copy the last run's hits into device memory at dev_ptr (cap entries)."""
+        check(lib().mp_search_fetch_device(self._h, c_void_p(dev_ptr), cap, c_void_p(stream or 0)))
 
     def device_hits(self) -> int:
         p = c_void_p()

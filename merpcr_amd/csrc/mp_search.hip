@@ -461,6 +461,17 @@ MP_EXPORT int mp_search_fetch(void* search, mp_hit* out, uint64_t cap, void* str
     return MP_OK;
 }
 
+MP_EXPORT int mp_search_fetch_device(void* search, mp_hit* dev_out, uint64_t cap, void* stream) {
+    Search* s = (Search*)search;
+    if (!s || (s->n_hits && !dev_out)) return fail(MP_E_ARG, "mp_search_fetch_device: null pointer");
+    if (cap < s->n_hits) return fail(MP_E_CAP, "mp_search_fetch_device: output buffer too small");
+    if (!s->n_hits) return MP_OK;
+    MP_HIP_CHECK(hipSetDevice(s->genome->device));
+    MP_HIP_CHECK(hipMemcpyAsync(dev_out, s->out, s->n_hits * sizeof(mp_hit), hipMemcpyDeviceToDevice,
+                                (hipStream_t)stream));
+    return MP_OK;
+}
+
 MP_EXPORT int mp_search_device_hits(void* search, const mp_hit** dev_hits) {
     Search* s = (Search*)search;
     if (!s || !dev_hits) return fail(MP_E_ARG, "mp_search_device_hits: null pointer");

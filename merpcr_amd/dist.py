@@ -1,0 +1,97 @@
+"""Multi-GPU search: owned-k sharding and the hit gather.
+
+The reference's only parallelism is a ProcessPoolExecutor over overlapping
+chunks of one record (src/merpcr/core/engine.py:386-422), whose results come
+back by pickling.  Here one process drives one GPU (torch.distributed, backend
+"nccl" = RCCL over xGMI on MI355X, "gloo" on CPU for tests):
+
+* ``shard_ranges`` splits the genome's (sequence, amplicon start k) space into
+  contiguous owned ranges of equal base count.  Every rank can hold the whole
+  genome (it is tiny next to 288 GB of HBM); each scans only the windows its
+  owned k need, and all boundary tests use the true record length, so the
+  union of the ranks' hits is exactly the single-GPU hit list.
+* Owned ranges are ordered and hit order never crosses a range boundary, so the
+  rank-ordered concatenation of per-rank sorted lists is the global order.
+  ``gather_hits`` is a gatherv: an all_gather of per-rank counts, then one
+  point-to-point transfer per rank into rank 0's buffer.  There is no other
+  data-path collective.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+HIT_BYTES = 24
+
+
+def shard_ranges(lengths: Sequence[int], world: int) -> List[Tuple[int, int, int, int]]:
+    """Owned ranges (seq_begin, seq_end, k_begin, k_end) for each rank."""
+    lens = np.asarray(lengths, dtype=np.int64)
+    cum = np.concatenate([[0], np.cumsum(lens)])
+    total = int(cum[-1])
+    n_seq = len(lens)
+
+    def locate(g: int):
+        if g >= total:
+            return n_seq, 0
+        s = int(np.searchsorted(cum, g, side="right") - 1)
+        return s, g - int(cum[s])
+
+    out = []
+    for r in range(world):
+        a = total * r // world
+        b = total * (r + 1) // world
+        sa, ka = locate(a)
+        sb, kb = locate(b)
+        out.append((sa, sb, ka, kb))
+    return out
+
+
+def gather_hits(local, n_local: int, group=None, dst: int = 0) -> Optional[object]:
+    """Gather per-rank hit byte buffers (torch uint8 tensors) to rank ``dst``.
+
+    ``local`` holds at least n_local * 24 bytes.  Returns the concatenated
+    tensor on rank ``dst`` (rank order), None elsewhere.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = local.device
+    cnt = torch.tensor([n_local], dtype=torch.int64, device=dev)
+    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    if rank == dst:
+        total = sum(counts)
+        out = torch.empty(max(total, 1) * HIT_BYTES, dtype=torch.uint8, device=dev)
+        ops = []
+        off = 0
+        for r, c in enumerate(counts):
+            if c == 0:
+                off += c
+                continue
+            view = out[off * HIT_BYTES:(off + c) * HIT_BYTES]
+            if r == rank:
+                view.copy_(local[:c * HIT_BYTES])
+            else:
+                ops.append(dist.P2POp(dist.irecv, view, r, group=group))
+            off += c
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        return out[:total * HIT_BYTES]
+    if n_local:
+        op = dist.P2POp(dist.isend, local[:n_local * HIT_BYTES].contiguous(), dst, group=group)
+        for w in dist.batch_isend_irecv([op]):
+            w.wait()
+    return None
+
+
+def as_hits(buf) -> np.ndarray:
+    """uint8 tensor / array of packed mp_hit records -> structured numpy array."""
+    from ._native import HIT_DTYPE
+    arr = buf.cpu().numpy() if hasattr(buf, "cpu") else np.asarray(buf)
+    return np.frombuffer(arr.tobytes(), dtype=HIT_DTYPE)
