@@ -47,8 +47,8 @@ def cpu_baseline(eng, names, lens, buf, offs, cfg, hits_dev, budget_s: float, th
     sts_lines = open(eng._sts_path).read().splitlines(True)
     table = O.load_sts_lines(sts_lines, cfg["W"], 240)
     prm = O.params(wordsize=cfg["W"], mismatches=cfg["N"], margin=cfg["M"], iupac_mode=cfg["I"])
-    # calibrate on 4 Mbp of record 0
-    probe = buf[int(offs[0]):int(offs[0]) + 4_000_000].cpu().numpy()
+    # calibrate on 64 Mbp of record 0
+    probe = buf[int(offs[0]):int(offs[0]) + min(64_000_000, lens[0])].cpu().numpy()
     t = time.time()
     C.search(table, [probe], prm, threads)
     rate = len(probe) / max(time.time() - t, 1e-6)

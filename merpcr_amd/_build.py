@@ -25,7 +25,7 @@ def hipcc() -> str:
 
 
 def _flags():
-    return ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+    return ["--offload-arch=" + ARCH, "-O3", "-std=c++20", "-fPIC", "-fvisibility=hidden",
             "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include")]
 
 
@@ -36,18 +36,20 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_native(force: bool = False, verbose: bool = False) -> str:
+def build_native(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB) -> str:
+    """Compile the sources and link `lib`; `defines` (timing-only variants) get their own objects."""
     os.makedirs(LIBDIR, exist_ok=True)
     cc = hipcc()
+    tag = "".join("_" + d.replace("=", "") for d in defines)
     hdrs = [os.path.normpath(os.path.join(CSRC, h)) for h in HEADERS]
     objs = []
     jobs = []
     for src in SOURCES:
         sp = os.path.join(CSRC, src)
-        op = os.path.join(LIBDIR, src.replace(".hip", ".o"))
+        op = os.path.join(LIBDIR, src.replace(".hip", tag + ".o"))
         objs.append(op)
         if force or _stale(op, [sp] + hdrs):
-            jobs.append([cc] + _flags() + ["-c", sp, "-o", op])
+            jobs.append([cc] + _flags() + ["-D" + d for d in defines] + ["-c", sp, "-o", op])
     if jobs:
         with concurrent.futures.ThreadPoolExecutor(max_workers=min(4, len(jobs))) as ex:
             for cmd, res in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):
@@ -56,14 +58,14 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
                     print(res.stdout + res.stderr)
                 if res.returncode:
                     raise RuntimeError(f"hipcc failed for {cmd[-3]}")
-    if force or jobs or _stale(LIB, objs):
-        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+    if force or jobs or _stale(lib, objs):
+        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode:
             print(" ".join(cmd))
             print(res.stdout + res.stderr)
             raise RuntimeError("hipcc link failed")
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

@@ -29,7 +29,7 @@ EXPORTS = (
     "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
     "mp_genome_stats", "mp_genome_destroy",
     "mp_search_create", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
-    "mp_search_last_stats", "mp_search_destroy",
+    "mp_search_last_stats", "mp_search_survivors", "mp_search_destroy",
 )
 
 
@@ -79,6 +79,7 @@ def _sig(lib):
     lib.mp_search_fetch_device.argtypes = [P, P, c_uint64, P]
     lib.mp_search_device_hits.argtypes = [P, POINTER(c_void_p)]
     lib.mp_search_last_stats.argtypes = [P, POINTER(c_float), u64p, u64p]
+    lib.mp_search_survivors.argtypes = [P, u64p]
     lib.mp_search_destroy.argtypes = [P]
     lib.mp_search_destroy.restype = None
 
@@ -221,7 +222,9 @@ class Search:
     def last_stats(self):
         ms, nw, nc = c_float(), c_uint64(), c_uint64()
         check(lib().mp_search_last_stats(self._h, ctypes.byref(ms), ctypes.byref(nw), ctypes.byref(nc)))
-        return {"scan_ms": ms.value, "windows": nw.value, "candidates": nc.value}
+        sv = c_uint64()
+        check(lib().mp_search_survivors(self._h, ctypes.byref(sv)))
+        return {"scan_ms": ms.value, "windows": nw.value, "candidates": nc.value, "survivors": sv.value}
 
     def close(self):
         if self._h:

@@ -35,7 +35,8 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ s
                                                    uint64_t* __restrict__ xr_start,
                                                    uint8_t* __restrict__ xr_char,
                                                    unsigned long long* __restrict__ xr_count,
-                                                   uint64_t xr_cap, uint64_t xr_base) {
+                                                   uint64_t xr_cap, uint64_t xr_base,
+                                                   unsigned long long* __restrict__ u_count) {
     const uint64_t grp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t i0 = grp * 64;
     const bool active = i0 < nbytes;
@@ -81,6 +82,8 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ s
             prev_exc = !pad && (c & 4u);
         }
         heads = __popcll(headmask);
+        const uint32_t nu = (uint32_t)__popcll(exc & ~inv & (cnt == 64 ? ~0ull : ~(~0ull >> cnt)));
+        if (nu) atomicAdd(u_count, (unsigned long long)nu);
         const uint64_t gw = (gstart + i0) >> 5;
         g2[gw] = w0;
         g2[gw + 1] = w1;
@@ -117,8 +120,24 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ s
     }
 }
 
+// dir[b] = index of the last exception run starting at or before b << kDirShift.
+__global__ void run_dir_kernel(const uint64_t* __restrict__ xr_start, uint64_t n_xr, uint32_t* __restrict__ dir,
+                               uint64_t n_dir) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n_dir) return;
+    const uint64_t j = b << kDirShift;
+    uint64_t lo = 0, hi = n_xr;
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (xr_start[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    dir[b] = (uint32_t)lo;
+}
+
 static void free_genome(Genome* g) {
     if (!g) return;
+    hipFree(g->xr_dir); hipFree(g->d_ucount);
     hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv); hipFree(g->d_base); hipFree(g->d_len);
     hipFree(g->xr_start); hipFree(g->xr_char); hipFree(g->d_counter); hipFree(g->staging);
     delete g;
@@ -160,7 +179,7 @@ static int put_device_bytes(Genome* g, uint32_t seq, uint64_t offset, const uint
         MP_HIP_CHECK(hipMemsetAsync(g->d_counter, 0, sizeof(unsigned long long), st));
         hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, st, dsrc, nbytes,
                            g->base[seq] + offset, g->g2, g->gexc, g->ginv, g->xr_start, g->xr_char,
-                           g->d_counter, g->xr_cap, g->n_xr);
+                           g->d_counter, g->xr_cap, g->n_xr, g->d_ucount);
         MP_HIP_CHECK(hipGetLastError());
         unsigned long long cnt = 0;
         MP_HIP_CHECK(hipMemcpyAsync(&cnt, g->d_counter, sizeof(cnt), hipMemcpyDeviceToHost, st));
@@ -205,12 +224,13 @@ MP_EXPORT int mp_genome_create(int32_t device, uint32_t n_seq, const uint64_t* s
             hipMalloc(&g->ginv, w1 * 8) != hipSuccess ||
             hipMalloc(&g->d_base, std::max<uint64_t>(n_seq, 1) * 8) != hipSuccess ||
             hipMalloc(&g->d_len, std::max<uint64_t>(n_seq, 1) * 8) != hipSuccess ||
-            hipMalloc(&g->d_counter, 64) != hipSuccess) {
+            hipMalloc(&g->d_counter, 64) != hipSuccess || hipMalloc(&g->d_ucount, 64) != hipSuccess) {
             rc = fail(MP_E_NOMEM, "mp_genome_create: device allocation failed");
             break;
         }
         g->dev_bytes = w2 * 8 + 2 * w1 * 8;
-        if (hipMemset(g->g2, 0, w2 * 8) != hipSuccess || hipMemset(g->gexc, 0xFF, w1 * 8) != hipSuccess ||
+        if (hipMemset(g->d_ucount, 0, 64) != hipSuccess || hipMemset(g->g2, 0, w2 * 8) != hipSuccess ||
+            hipMemset(g->gexc, 0xFF, w1 * 8) != hipSuccess ||
             hipMemset(g->ginv, 0xFF, w1 * 8) != hipSuccess) {
             rc = fail(MP_E_HIP, "mp_genome_create: memset failed");
             break;
@@ -263,9 +283,21 @@ MP_EXPORT int mp_genome_seal(void* genome, void* stream) {
     Genome* g = (Genome*)genome;
     if (!g) return fail(MP_E_ARG, "mp_genome_seal: null genome");
     MP_HIP_CHECK(hipSetDevice(g->device));
-    int rc = sort_runs(g, (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    int rc = sort_runs(g, st);
     if (rc) return rc;
-    MP_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    if (g->n_xr >> 32) return fail(MP_E_ARG, "more than 2^32 exception runs");
+    hipFree(g->xr_dir);
+    g->xr_dir = nullptr;
+    g->n_dir = (g->total >> kDirShift) + 2;
+    MP_HIP_CHECK(hipMalloc(&g->xr_dir, g->n_dir * sizeof(uint32_t)));
+    hipLaunchKernelGGL(run_dir_kernel, dim3((uint32_t)((g->n_dir + 255) / 256)), dim3(256), 0, st, g->xr_start,
+                       g->n_xr, g->xr_dir, g->n_dir);
+    MP_HIP_CHECK(hipGetLastError());
+    unsigned long long nu = 0;
+    MP_HIP_CHECK(hipMemcpyAsync(&nu, g->d_ucount, sizeof(nu), hipMemcpyDeviceToHost, st));
+    MP_HIP_CHECK(hipStreamSynchronize(st));
+    g->has_u = nu != 0;
     g->sealed = true;
     return MP_OK;
 }

@@ -12,11 +12,20 @@
 //   Sequences are laid end to end, each padded to a multiple of 64 bases; the
 //   padding is marked ginv = gexc = 1.  A "global" coordinate is the index in
 //   that padded space.
-//   table   filt : seed-presence bitmap (direct 4^W bits for W <= 13, else a
-//                  hashed 2^27-bit filter), slots: open-addressed key -> bucket,
-//                  boff/blist: bucket CSR of record indices (insertion order),
-//                  recs: one 32-B DevRec per oriented STS record, primer accept
-//                  planes (4 x u64 per 32 primer bases) and raw primer bytes.
+//   table   lfilt: 64 KiB seed prefilter, staged in LDS by every workgroup (exact
+//                  4^W bitmap for W <= 9, hashed above)
+//           W <= 13: rk: {presence bits, prefix popcount} per 32 keys of the exact
+//                  4^W bitmap; the rank of a present key indexes dents, one 32-B
+//                  bucket-head Entry per distinct key
+//           W >= 14: filt: hashed 2^27-bit presence filter, slots: open-addressed
+//                  key -> 64-B Slot holding the bucket-head Entry
+//           Entry: record id, seed offset and a primer-1 fingerprint (2-bit code +
+//                  plain/never masks of its first 32 bases) that rejects almost
+//                  every random seed hit; ents: all Entries in bucket order
+//                  (records of one key in insertion order), read for bucket tails
+//           recs : one 32-B DevRec per record (sts_records order), primer accept
+//                  planes (4 x u64 per 32 primer bases) and raw primer bytes, read
+//                  only for fingerprint survivors.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -44,13 +53,17 @@ int fail(int code, const std::string& msg);
 
 // ---------------------------------------------------------------- constants
 constexpr uint64_t kEven = 0x5555555555555555ull;  // the low bit of every 2-bit slot
-constexpr uint64_t kEmptySlot = ~0ull;
 constexpr int kHashedFilterLog2 = 27;               // 16 MiB hashed filter for W >= 14
 constexpr int kDirectFilterMaxW = 13;               // 4^13 bits = 8 MiB direct bitmap
-constexpr int kBlock = 256;                         // threads per scan workgroup
+constexpr int kBlock = 1024;                        // threads per scan workgroup (one per CU)
 constexpr int kWaves = kBlock / 64;
-constexpr int kStepsPerWave = 16;                   // 64-position steps per wave per tile
-constexpr uint32_t kTile = kWaves * 64 * kStepsPerWave;  // window positions per workgroup
+constexpr int kLanePos = 32;                        // consecutive window positions per lane
+constexpr uint32_t kSuper = 64 * kLanePos;          // positions per wave super-step
+constexpr int kBlocksPerCU = 1;                     // persistent grid: resident workgroups per CU
+constexpr int kDirShift = 12;                       // exception-run directory granularity
+constexpr int kLdsFilterLog2 = 19;                  // 64 KiB seed prefilter staged in LDS
+constexpr uint32_t kLdsFilterWords = (1u << kLdsFilterLog2) / 32;
+constexpr int kSub = 8;                             // filter probes in flight per lane
 
 struct DevRec {            // one oriented STS record, 32 bytes
     uint32_t hash_off;     // offset of the seed W-mer inside primer1
@@ -61,11 +74,32 @@ struct DevRec {            // one oriented STS record, 32 bytes
 };
 static_assert(sizeof(DevRec) == 32, "DevRec layout");
 
+struct Entry {             // one oriented record, 32 bytes
+    uint64_t code;         // 2-bit code of primer-1 bases [0, 32) (big-endian slots)
+    uint64_t pmask;        // even bits: base is a single A/C/G/T for the compare rule
+                           // (plain); odd bits: no A/C/G/T matches it (never)
+    uint32_t rec;          // index in sts_records
+    uint16_t hash_off;     // seed offset inside primer 1
+    uint16_t l1;           // primer-1 length
+    uint32_t xstart;       // bucket head only: ents index of the bucket's 2nd record
+    uint32_t count;        // bucket head only: records with this key
+};
+static_assert(sizeof(Entry) == 32, "Entry layout");
+
+struct Slot {              // open-addressed seed-table slot (W >= 14), 64 bytes
+    uint32_t key;
+    uint32_t used;         // 0 = empty slot
+    uint32_t pad0, pad1;
+    Entry e0;              // the bucket head
+    uint64_t pad2, pad3;
+};
+static_assert(sizeof(Slot) == 64, "Slot layout");
+
 struct SeqSpan {           // per-sequence work description for one search run
-    uint64_t tile0;        // first workgroup index of this sequence
+    uint64_t super0;       // first global super-step of this sequence (sentinel: total)
     uint32_t seq;          // sequence index in the genome handle
     uint32_t p_lo, p_hi;   // window positions [p_lo, p_hi) scanned
-    uint32_t pad;
+    uint32_t p_al;         // p_lo rounded down to a multiple of kLanePos (super-step origin)
 };
 
 // ---------------------------------------------------------------- handles
@@ -77,11 +111,14 @@ struct Table {
     uint32_t max_hash_off = 0;
     int filt_direct = 1;
     uint32_t filt_log2 = 0;   // log2(filter bits)
+    int lds_exact = 0;        // LDS prefilter is the exact 4^W bitmap (W <= 9)
+    uint32_t* lfilt = nullptr;  // kLdsFilterWords words
     uint32_t slot_log2 = 0;
-    uint32_t* filt = nullptr;
-    uint64_t* slots = nullptr;
-    uint32_t* boff = nullptr;
-    uint32_t* blist = nullptr;
+    uint32_t* filt = nullptr;     // W >= 14: hashed presence filter
+    uint2* rk = nullptr;          // W <= 13: rank bitmap
+    Entry* dents = nullptr;       // W <= 13: bucket heads by key rank
+    Slot* slots = nullptr;        // W >= 14
+    Entry* ents = nullptr;
     DevRec* recs = nullptr;
     uint32_t* rank = nullptr;      // rec -> position in (hash_off, rec) order
     uint32_t* inv_rank = nullptr;  // position -> rec
@@ -103,6 +140,10 @@ struct Genome {
     uint64_t* xr_start = nullptr;
     uint8_t* xr_char = nullptr;
     uint64_t xr_cap = 0, n_xr = 0;
+    uint32_t* xr_dir = nullptr;               // last run starting at or before b * 4096
+    uint64_t n_dir = 0;
+    unsigned long long* d_ucount = nullptr;   // U bases seen by the packer
+    bool has_u = false;
     unsigned long long* d_counter = nullptr;  // run-count scratch
     uint8_t* staging = nullptr;
     uint64_t staging_cap = 0;
@@ -123,8 +164,9 @@ struct Search {
     unsigned long long* counters = nullptr;  // [0] hits, [1] candidates
     SeqSpan* spans = nullptr;
     uint64_t spans_cap = 0;
+    int n_cu = 0;
     uint64_t n_hits = 0;
-    uint64_t n_windows = 0, n_candidates = 0;
+    uint64_t n_windows = 0, n_candidates = 0, n_survivors = 0;
     float scan_ms = 0.f;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -180,6 +222,19 @@ __host__ __device__ __forceinline__ uint32_t table_slot(uint32_t key, uint32_t l
 
 __host__ __device__ __forceinline__ uint32_t filter_index(uint32_t key, uint32_t log2bits) {
     return (uint32_t)(((uint64_t)key * 0xD6E8FEB86659FD93ull) >> (64 - log2bits));
+}
+
+// LDS prefilter index of a seed key (exact for W <= 9, multiplicative hash above);
+// with kLdsHashes == 2 a second index is set too (two-probe Bloom filter).
+#ifndef MP_LDS_HASHES
+#define MP_LDS_HASHES 1
+#endif
+constexpr int kLdsHashes = MP_LDS_HASHES;
+__host__ __device__ __forceinline__ uint32_t lds_index(uint32_t key, int exact) {
+    return exact ? key : (uint32_t)(key * 0x9E3779B1u) >> (32 - kLdsFilterLog2);
+}
+__host__ __device__ __forceinline__ uint32_t lds_index2(uint32_t key) {
+    return (uint32_t)((key ^ 0x5bd1e995u) * 0x85EBCA77u) >> (32 - kLdsFilterLog2);
 }
 
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {

@@ -4,23 +4,37 @@
 // _match_sts (engine.py:507-597) and _compare_seqs (engine.py:599-642), all in
 // src/merpcr/core/engine.py of the reference.
 //
-// Kernel structure (one 256-thread workgroup = one tile of kTile window
-// positions of one sequence; each wave owns 1024 consecutive positions):
-//   1. seed stage: 64 consecutive window positions per wave step, one per lane.
-//      Each lane pulls its W-mer from the 2-bit plane and its ambiguity bits from
-//      ginv (L1-broadcast loads), tests the presence filter and, on a hit, probes
-//      the open-addressed table for its bucket.
-//   2. compaction: lanes holding a bucket append (pos, bucket) to a per-wave LDS
-//      queue with a ballot + popcount prefix, so verification runs with all 64
-//      lanes busy whatever the seed density.
-//   3. drain (queue >= 64 entries): a wave prefix over bucket sizes expands the
-//      queue into (pos, record) candidates, 64 per pass; each lane verifies
-//      primer 1 with a bit-sliced 2-bit compare (32 bases per step, exception
-//      positions resolved through the run index), then pair-checks primer 2 over
-//      the amplicon +- margin window and emits 128-bit order keys.
+// Kernel structure: a persistent grid of one 1024-thread workgroup per CU.  Each
+// workgroup first stages the 64 KiB seed prefilter in LDS; then every wave walks
+// "super-steps" of 2048 consecutive window positions of one sequence (32 per lane):
+//   1. seed stage: the lane's two 2-bit words and one ambiguity word cover its 32
+//      windows (coalesced loads, prefetched one super-step ahead).  Every W-mer comes
+//      from registers (alignbit), the "all A/C/G/T/U" test of engine.py:464-503 is one
+//      smear of the ambiguity word, the LDS prefilter is probed by ds_read and, where
+//      it passes and is not exact, the global presence bitmap (8 probes in flight).
+//   2. compaction: seed hits (about 4.6% of windows at W=11 / 100k STS) become u16
+//      offsets in a per-wave LDS queue (popcount + wave prefix).
+//   3. drain: one lane per queued seed.  Its W-mer and the genome window of the
+//      candidate primer come from the wave's registers by cross-lane shuffles.  The
+//      bucket head (exact rank bitmap for W <= 13, open-addressed slot above) holds a
+//      primer-1 fingerprint; a 2-bit XOR/popcount lower bound on the mismatches
+//      rejects almost every random seed from that one 32-B entry.  Buckets with more
+//      records are expanded 64 candidates per pass.
+//   4. survivors (at most 64 per pass) are verified and pair-checked by the whole
+//      wave (primer_ok: bit-sliced accept planes, exception bases resolved through the
+//      run index; lanes split the amplicon-end offsets) and emit 128-bit order keys.
 #include <algorithm>
+#include <utility>
 
 #include "mp_internal.h"
+
+// Timing-only ablation builds (scripts/ablate.py); 0 in the product library.
+//   1: no drain (seed stage only)   2: no global filter probe (hash-based stand-in)
+//   3: neither                      4: drain stops after the bucket lookup
+//   5: fingerprint only (survivors are counted, not pair-checked)
+#ifndef MP_ABLATE
+#define MP_ABLATE 0
+#endif
 
 namespace mp {
 
@@ -30,23 +44,26 @@ struct ScanArgs {
     const uint64_t* ginv;
     const uint64_t* xr_start;
     const uint8_t* xr_char;
+    const uint32_t* xr_dir;
     uint64_t n_xr;
     const uint64_t* seq_base;
     const uint64_t* seq_len;
     const SeqSpan* spans;
     uint32_t n_spans;
-    const uint32_t* filt;
+    const uint32_t* filt;   // W >= 14: hashed presence filter
     uint32_t filt_log2;
-    int filt_direct;
-    const uint64_t* slots;
+    const uint2* rk;        // W <= 13: rank bitmap
+    const Entry* dents;     // W <= 13: bucket heads by rank
+    const uint32_t* lfilt;
+    const Slot* slots;
     uint32_t slot_log2;
-    const uint32_t* boff;
-    const uint32_t* blist;
+    const Entry* ents;
     const DevRec* recs;
     const uint32_t* rank;
     const uint64_t* planes;
     const uint8_t* pchars;
     int W, M, N, X, I;
+    int has_u;              // genome holds U: exception bits come from gexc, not ginv
     uint64_t g_lo, g_hi;
     uint64_t* hit_hi;
     uint64_t* hit_lo;
@@ -54,8 +71,12 @@ struct ScanArgs {
     uint64_t cap;
 };
 
+// Character of exception base j: the run index entry with the largest start <= j,
+// searched between the directory bounds of j's 4096-base block.
 __device__ __forceinline__ uint8_t exc_char(const ScanArgs& a, uint64_t j) {
-    uint64_t lo = 0, hi = a.n_xr;  // last run with start <= j
+    const uint64_t b = j >> kDirShift;
+    uint64_t lo = a.xr_dir[b];
+    uint64_t hi = min<uint64_t>((uint64_t)a.xr_dir[b + 1] + 1, a.n_xr);
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
         if (a.xr_start[mid] <= j) lo = mid;
@@ -103,6 +124,42 @@ __device__ bool primer_ok(const ScanArgs& a, uint64_t gpos, uint32_t L, uint32_t
     return true;
 }
 
+// 32-bit per-base mask (bit 31-i) -> spaced form (bit 62-2i).
+__device__ __forceinline__ uint64_t spread32(uint32_t v) {
+    uint64_t x = v;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & kEven;
+    return x;
+}
+
+// Lower bound on primer-1 mismatches from the fingerprint, over the first min(l1, 32)
+// bases of the genome window G (exception bits ex, bit 31-i): plain primer positions
+// whose genome base differs, plus "never" positions.  A genome exception base is
+// counted only where it certainly mismatches: at a plain position in literal mode
+// (I=0: an exception character never equals A/C/G/T); with I=1 it may match and is
+// skipped.  Every counted position is a real mismatch of engine.py:599-642, so a
+// rejection here is exact.
+__device__ __forceinline__ bool fp_reject(const ScanArgs& a, uint64_t G, uint32_t ex, uint32_t l1, uint64_t code,
+                                          uint64_t pmask) {
+    const int len = (int)min(l1, 32u);
+    const uint64_t inside = sp_lt(len);
+    const uint64_t x = G ^ code;
+    const uint64_t plain = pmask & kEven;
+    uint64_t d = (((x | (x >> 1)) & plain) | ((pmask >> 1) & kEven)) & inside;
+    if (ex) {
+        const uint64_t es = spread32(ex) & inside;
+        d &= ~es;
+        if (!a.I) d |= es & plain;
+    }
+    const int64_t a0 = (int64_t)l1 - a.X;  // '+' strand: positions >= l1 - X are protected
+    const uint64_t prot = inside & ~sp_lt((int)max<int64_t>(min<int64_t>(a0, 32), 0));
+    if (d & prot) return true;
+    return __popcll(d) > a.N;
+}
+
 __device__ __forceinline__ void emit(const ScanArgs& a, uint64_t gk, uint32_t rank, uint32_t tr) {
     const unsigned long long idx = atomicAdd(&a.counters[0], 1ull);
     if (idx < a.cap) {
@@ -111,16 +168,14 @@ __device__ __forceinline__ void emit(const ScanArgs& a, uint64_t gk, uint32_t ra
     }
 }
 
-// _match_sts (engine.py:507-597) for record `rec` seeded at window position pos.
-__device__ void process_candidate(const ScanArgs& a, uint64_t sbase, uint32_t n, uint32_t pos, uint32_t rec,
-                                  uint32_t& ncand) {
+// _match_sts (engine.py:507-597) for one fingerprint survivor (record `rec`, amplicon
+// start k), executed by the whole wave: every lane re-checks primer 1 (same addresses,
+// broadcast loads) and the lanes split the amplicon-end offsets d in [-lo, hi] (the
+// reference's try order is restored by the device sort through try_rank(d)).
+__device__ void pair_check_wave(const ScanArgs& a, uint64_t sbase, uint32_t n, uint32_t k, uint32_t rec,
+                                int lane) {
     const DevRec r = a.recs[rec];
-    if (pos < r.hash_off) return;
-    const uint32_t k = pos - r.hash_off;
-    if ((uint64_t)k + r.l1 > n) return;
     const uint64_t gk = sbase + k;
-    if (gk < a.g_lo || gk >= a.g_hi) return;
-    ++ncand;
     if (!primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true)) return;
     const uint32_t avail = n - k - r.l1;
     if (avail < r.l2) return;
@@ -135,27 +190,11 @@ __device__ void process_candidate(const ScanArgs& a, uint64_t sbase, uint32_t n,
     }
     const int lo = (int)max<int64_t>(0, min<int64_t>(a.M, (int64_t)e - r.l1 - r.l2));
     const uint32_t rk = a.rank[rec];
-    for (int d = -lo; d <= hi; ++d) {
+    for (int d = -lo + lane; d <= hi; d += 64) {
         const int64_t p2 = (int64_t)k + e - r.l2 + d;
         if (d <= 0 && (int64_t)k + r.l1 > p2) continue;
         if (p2 + r.l2 > (int64_t)n) continue;
         if (primer_ok(a, sbase + (uint64_t)p2, r.l2, r.p2_pl, r.p2_ch, false)) emit(a, gk, rk, try_rank(d));
-    }
-}
-
-__device__ __forceinline__ bool lookup(const ScanArgs& a, uint32_t h, uint32_t& bs, uint32_t& bc) {
-    const uint32_t mask = (1u << a.slot_log2) - 1;
-    uint32_t s = table_slot(h, a.slot_log2);
-    for (;;) {
-        const uint64_t v = a.slots[s];
-        if (v == kEmptySlot) return false;
-        if ((uint32_t)(v >> 32) == h) {
-            const uint32_t b = (uint32_t)v;
-            bs = a.boff[b];
-            bc = a.boff[b + 1] - bs;
-            return true;
-        }
-        s = (s + 1) & mask;
     }
 }
 
@@ -168,93 +207,345 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct WaveLds {           // per-wave LDS scratch of the drain
+    uint32_t sv_k[64];     // survivors of one pass (at most one per lane)
+    uint32_t sv_r[64];
+    uint32_t x_pos[64];    // bucket tails of one pass
+    uint32_t x_start[64];
+    uint32_t x_pre[64];
+};
+
+// The current super-step as the wave holds it: lane L owns bases [base + 32L,
+// base + 32L + 64) as two 2-bit words and one ambiguity word.
+struct SuperRegs {
+    uint64_t w0, w1, iv;
+    uint32_t base;
+};
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// 32 bases (2-bit, base p on top) and their exception bits (bit 31-i) starting at
+// sequence position p, with p - base in [0, kSuper): from the owning lane's registers.
+// All lanes must call (shuffles); `p` of inactive lanes may be anything in range.
+__device__ __forceinline__ void window_from_regs(const ScanArgs& a, const SuperRegs& R, uint64_t sbase,
+                                                 uint32_t p, bool in_regs, uint64_t& G, uint32_t& ex) {
+    const uint32_t off = in_regs ? p - R.base : 0u;
+    const int src = (int)(off >> 5);
+    const uint32_t r = off & 31u;
+    const uint64_t x0 = shfl64(R.w0, src), x1 = shfl64(R.w1, src), v = shfl64(R.iv, src);
+    if (in_regs) {
+        G = r ? (x0 << (2 * r)) | (x1 >> (64 - 2 * r)) : x0;
+        ex = (uint32_t)((v << r) >> 32);
+    } else {
+        G = ext2(a.g2, sbase + p);
+        ex = (uint32_t)(ext1(a.ginv, sbase + p) >> 32);
+    }
+    if (a.has_u) ex = (uint32_t)(ext1(a.gexc, sbase + p) >> 32);
+}
+
+// One (seed position, record) candidate: the bounds of engine.py:486-489, the
+// owned-range test and the fingerprint filter.  True = survivor (k returned).
+// All lanes must call (shuffles); `act` marks lanes that hold a candidate.
+__device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
+                                          bool act, uint32_t pos, const Entry& e, uint32_t& ncand, uint32_t& k_out,
+                                          uint64_t Gpos, uint32_t expos, bool reuse) {
+    const uint32_t k = pos - e.hash_off;
+    act = act && pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
+    act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
+    uint64_t G = Gpos;
+    uint32_t ex = expos;
+    if (!reuse || !__all(!act || e.hash_off == 0)) {  // some seed is not at the primer start
+        const bool in_regs = k >= R.base && k - R.base < kSuper;
+        window_from_regs(a, R, sbase, act ? k : R.base, !act || in_regs, G, ex);
+    }
+    if (!act) return false;
+    ++ncand;
+    if (fp_reject(a, G, ex, e.l1, e.code, e.pmask)) return false;
+    k_out = k;
+    return true;
+}
+
+// Compact this pass's survivors (one per lane at most) and pair-check each with the
+// whole wave.
+__device__ __forceinline__ void flush_survivors(const ScanArgs& a, uint64_t sbase, uint32_t n, bool surv,
+                                                uint32_t k, uint32_t rec, int lane, WaveLds& L) {
+    const uint64_t m = __ballot(surv);
+    if (!m) return;
+    if (surv) {
+        const uint32_t i = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        L.sv_k[i] = k;
+        L.sv_r[i] = rec;
+    }
+    if (lane == 0) atomicAdd(&a.counters[2], (unsigned long long)__popcll(m));
+    wave_sync();
+#if MP_ABLATE != 5
+    const uint32_t ns = (uint32_t)__popcll(m);
+    for (uint32_t i = 0; i < ns; ++i) pair_check_wave(a, sbase, n, L.sv_k[i], L.sv_r[i], lane);
+#endif
+    wave_sync();
+}
+
+// Bucket head of seed key h (W <= 13: rank of h in the exact bitmap; above: slot).
+template <int kMode>
+__device__ __forceinline__ bool bucket_head(const ScanArgs& a, uint32_t h, Entry& e0) {
+    if constexpr (kMode != 2) {
+        const uint2 rw = a.rk[h >> 5];
+        const uint32_t bit = h & 31u;
+        if (!((rw.x >> bit) & 1u)) return false;
+        e0 = a.dents[rw.y + (uint32_t)__popc(rw.x & ((1u << bit) - 1u))];
+        return true;
+    } else {
+        const uint32_t mask = (1u << a.slot_log2) - 1;
+        uint32_t s = table_slot(h, a.slot_log2);
+        for (;;) {
+            const uint4 head = *reinterpret_cast<const uint4*>(&a.slots[s]);  // key, used
+            if (head.y == 0) return false;  // hashed-filter false positive
+            if (head.x == h) break;
+            s = (s + 1) & mask;
+        }
+        e0 = a.slots[s].e0;
+        return true;
+    }
+}
+
+// Drain a wave's seed queue: one lane per queued seed looks up its bucket head and
+// tests it; bucket tails are expanded 64 candidates at a time.  Every pass yields at
+// most 64 survivors.
+template <int kMode>
+__device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
+                                            const uint16_t* q, uint32_t qn, int lane, uint32_t& ncand,
+                                            WaveLds& L) {
+    const uint32_t shw = 64u - 2u * (uint32_t)a.W;
+    for (uint32_t b = 0; b < qn; b += 64) {
+        const uint32_t e = b + (uint32_t)lane;
+        const bool live = e < qn;
+        const uint32_t pos = R.base + (live ? q[e] : 0u);
+        uint64_t Gp;
+        uint32_t exp_;
+        window_from_regs(a, R, sbase, pos, true, Gp, exp_);
+        const uint32_t h = (uint32_t)(Gp >> shw);
+        Entry e0{};
+        const bool have = live && bucket_head<kMode>(a, h, e0);
+#if MP_ABLATE == 4
+        ncand += have && e0.rec == 0xFFFFFFFFu;
+        continue;
+#endif
+        uint32_t sk = 0;
+        const bool surv = candidate(a, R, sbase, n, have, pos, e0, ncand, sk, Gp, exp_, true);
+        flush_survivors(a, sbase, n, surv, sk, e0.rec, lane, L);
+        // bucket tails
+        const uint32_t xc = have ? e0.count - 1u : 0u;
+        const uint32_t incl = wave_incl_scan(xc, lane);
+        const uint32_t total = __shfl(incl, 63, 64);
+        if (total) {
+            L.x_pos[lane] = pos;
+            L.x_start[lane] = e0.xstart;
+            L.x_pre[lane] = incl - xc;
+            wave_sync();
+            for (uint32_t c0 = 0; c0 < total; c0 += 64) {
+                const uint32_t c = c0 + (uint32_t)lane;
+                const bool act = c < total;
+                uint32_t lo = 0;
+                if (act) {
+                    uint32_t hi = 64;  // last lane with x_pre <= c
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (L.x_pre[mid] <= c) lo = mid;
+                        else hi = mid;
+                    }
+                }
+                Entry ej{};
+                if (act) ej = a.ents[L.x_start[lo] + (c - L.x_pre[lo])];
+                const bool s2 = candidate(a, R, sbase, n, act, L.x_pos[lo], ej, ncand, sk, 0, 0, false);
+                flush_survivors(a, sbase, n, s2, sk, ej.rec, lane, L);
+            }
+            wave_sync();
+        }
+    }
+}
+
+// Bit 31-i set iff window i (bases [i, i+W) of the lane's 64-base ambiguity window,
+// bit 63-j = base j is not A/C/G/T/U) is clean: every bad base is smeared over the W
+// windows that contain it (OR of bad << t, t < W, by binary decomposition of W).
+__device__ __forceinline__ uint32_t window_ok_mask(uint64_t bad, uint32_t W) {
+    uint64_t acc = 0, pw = bad;
+    uint32_t done = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+        if (W & (1u << b)) {
+            acc |= pw << done;
+            done += 1u << b;
+        }
+        pw |= pw << (1u << b);
+    }
+    return ~(uint32_t)(acc >> 32);
+}
+
+// Bits 31-i for i in [lo, hi), 0 <= lo, hi <= 32.
+__device__ __forceinline__ uint32_t bit_range(int lo, int hi) {
+    const uint32_t a = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu >> lo));
+    const uint32_t b = hi <= 0 ? 0xFFFFFFFFu : (hi >= 32 ? 0u : (0xFFFFFFFFu >> hi));
+    return a & ~b;
+}
+
+// W-mer at window i of a lane: top 2W bits of the 32-bit big-endian funnel at bit 2i of
+// (d0, d1, d2), the lane's 48 bases; i is a compile-time constant after unrolling.
+template <int I>
+__device__ __forceinline__ uint32_t kmer_top(uint32_t d0, uint32_t d1, uint32_t d2) {
+    constexpr int q = (2 * I) >> 5;
+    constexpr int r = (2 * I) & 31;
+    const uint32_t hi = q == 0 ? d0 : d1;
+    const uint32_t lo = q == 0 ? d1 : d2;
+    if constexpr (r == 0) return hi;
+    else return __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+}
+
+// Seed filter for 8 consecutive windows of a lane.  Level 1: the LDS prefilter
+// (random ds_read_b32).  Level 2 (unless the LDS filter is the exact 4^W bitmap): the
+// global presence bitmap, probed only by lanes whose level-1 bit is set -- the others
+// load word 0, so their requests coalesce into one line.  All 8 loads of a level are
+// issued before any result is used.
+template <int SUB, int kMode>
+__device__ __forceinline__ uint32_t probe8(const ScanArgs& a, const uint32_t* __restrict__ lds, uint32_t d0,
+                                           uint32_t d1, uint32_t d2, uint32_t shw) {
+    // kMode 0: LDS exact; 1: LDS hashed + exact rank bitmap; 2: LDS hashed + hashed filter
+    uint32_t h[kSub], lw[kSub];
+    [&]<int... T>(std::integer_sequence<int, T...>) {
+        ((h[T] = kmer_top<SUB * kSub + T>(d0, d1, d2) >> shw), ...);
+    }(std::make_integer_sequence<int, kSub>{});
+#pragma unroll
+    for (int t = 0; t < kSub; ++t) {
+        const uint32_t li = lds_index(h[t], kMode == 0);
+        lw[t] = (lds[li >> 5] >> (li & 31)) & 1u;
+        if constexpr (kLdsHashes == 2 && kMode != 0) {
+            const uint32_t l2 = lds_index2(h[t]);
+            lw[t] &= (lds[l2 >> 5] >> (l2 & 31)) & 1u;
+        }
+    }
+    uint32_t hits = 0;
+    if constexpr (kMode == 0) {
+#pragma unroll
+        for (int t = 0; t < kSub; ++t) hits |= lw[t] << (31 - (SUB * kSub + t));
+    } else {
+        uint32_t gw[kSub], gb[kSub];
+#pragma unroll
+        for (int t = 0; t < kSub; ++t) {
+            const uint32_t fi = kMode == 1 ? h[t] : filter_index(h[t], a.filt_log2);
+            gb[t] = fi & 31;
+#if MP_ABLATE == 2 || MP_ABLATE == 3
+            gw[t] = (h[t] * 2654435761u) >> 27 == 0 ? 0xFFFFFFFFu : 0u;
+#else
+            if constexpr (kMode == 1) gw[t] = a.rk[lw[t] ? (fi >> 5) : 0u].x;
+            else gw[t] = a.filt[lw[t] ? (fi >> 5) : 0u];
+#endif
+        }
+#pragma unroll
+        for (int t = 0; t < kSub; ++t) hits |= (lw[t] & (gw[t] >> gb[t])) << (31 - (SUB * kSub + t));
+    }
+    return hits;
+}
+
+// Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
+// ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
+// The next super-step's plane words are loaded before the current one is processed.
+template <int kMode>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
-    __shared__ uint32_t q_pos[kWaves][128];
-    __shared__ uint32_t q_bs[kWaves][128];
-    __shared__ uint32_t q_bc[kWaves][128];
-    __shared__ uint32_t q_pre[kWaves][128];
-    __shared__ uint32_t s_span;
+    __shared__ uint32_t s_lf[kLdsFilterWords];
+    __shared__ uint16_t q_off[kWaves][kSuper];
+    __shared__ WaveLds s_wl[kWaves];
+
+    // stage the seed prefilter in LDS (once per persistent workgroup)
+    for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)
+        reinterpret_cast<uint4*>(s_lf)[i] = reinterpret_cast<const uint4*>(a.lfilt)[i];
+    __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) {
-        uint32_t lo = 0, hi = a.n_spans;  // last span with tile0 <= blockIdx.x
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.spans[mid].tile0 <= blockIdx.x) lo = mid;
-            else hi = mid;
-        }
-        s_span = lo;
-    }
-    __syncthreads();
-    const SeqSpan sp = a.spans[s_span];
-    const uint64_t sbase = a.seq_base[sp.seq];
-    const uint32_t n = (uint32_t)a.seq_len[sp.seq];
-    const uint32_t tile_begin = sp.p_lo + (uint32_t)(blockIdx.x - sp.tile0) * kTile;
-    const uint32_t wb = tile_begin + (uint32_t)w * (64 * kStepsPerWave);
-    const uint32_t we = min(wb + 64 * kStepsPerWave, sp.p_hi);
-    const int W = a.W;
-    uint32_t* qp = q_pos[w];
-    uint32_t* qs = q_bs[w];
-    uint32_t* qc = q_bc[w];
-    uint32_t* qr = q_pre[w];
-    uint32_t qn = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+    const uint64_t n_supers = a.spans[a.n_spans].super0;
+    const uint32_t W = (uint32_t)a.W;
+    const uint32_t shw = 32u - 2u * W;
+    uint16_t* q = q_off[w];
     uint32_t ncand = 0;
 
-    auto drain = [&]() {
-        const uint32_t c0 = lane < (int)qn ? qc[lane] : 0u;
-        const uint32_t c1 = lane + 64 < (int)qn ? qc[lane + 64] : 0u;
-        const uint32_t s0 = wave_incl_scan(c0, lane);
-        const uint32_t t0 = __shfl(s0, 63, 64);
-        const uint32_t s1 = wave_incl_scan(c1, lane) + t0;
-        const uint32_t total = __shfl(s1, 63, 64);
-        if (lane < (int)qn) qr[lane] = s0 - c0;
-        if (lane + 64 < (int)qn) qr[lane + 64] = s1 - c1;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (uint32_t b = 0; b < total; b += 64) {
-            const uint32_t c = b + (uint32_t)lane;
-            if (c < total) {
-                uint32_t lo = 0, hi = qn;
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (qr[mid] <= c) lo = mid;
-                    else hi = mid;
-                }
-                const uint32_t rec = a.blist[qs[lo] + (c - qr[lo])];
-                process_candidate(a, sbase, n, qp[lo], rec, ncand);
-            }
+    uint64_t ss = (uint64_t)blockIdx.x * kWaves + (uint64_t)w;
+    uint32_t sid = 0;
+    auto locate = [&](uint64_t x) {  // span holding super-step x (wave-uniform)
+        if (x >= a.spans[sid].super0 && x < a.spans[sid + 1].super0) return;
+        uint32_t lo = 0, hi = a.n_spans;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.spans[mid].super0 <= x) lo = mid;
+            else hi = mid;
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        qn = 0;
+        sid = lo;
     };
-
-    for (uint32_t p0 = wb; p0 < we; p0 += 64) {
-        const uint32_t pos = p0 + (uint32_t)lane;
-        uint32_t bs = 0, bc = 0;
-        if (pos < we) {
-            const uint64_t j = sbase + pos;
-            if ((ext1(a.ginv, j) >> (64 - W)) == 0) {
-                const uint32_t h = (uint32_t)(ext2(a.g2, j) >> (64 - 2 * W));
-                const uint32_t fi = a.filt_direct ? h : filter_index(h, a.filt_log2);
-                if ((a.filt[fi >> 5] >> (fi & 31)) & 1u) lookup(a, h, bs, bc);
-            }
-        }
-        const bool have = bc > 0;
-        const uint64_t m = __ballot(have);
-        if (have) {
-            const uint32_t slot = qn + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            qp[slot] = pos;
-            qs[slot] = bs;
-            qc[slot] = bc;
-        }
-        qn += (uint32_t)__popcll(m);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (qn >= 64) drain();
+    auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& iv) {
+        const SeqSpan sp = a.spans[sid];
+        const uint64_t j = a.seq_base[sp.seq] + sp.p_al + (x - sp.super0) * kSuper + (uint64_t)lane * kLanePos;
+        w0 = a.g2[j >> 5];
+        w1 = a.g2[(j >> 5) + 1];
+        const uint64_t v0 = a.ginv[j >> 6];
+        const uint64_t v1 = a.ginv[(j >> 6) + 1];
+        iv = (j & 32) ? ((v0 << 32) | (v1 >> 32)) : v0;
+    };
+    uint64_t nw0 = 0, nw1 = 0, niv = 0;
+    if (ss < n_supers) {
+        locate(ss);
+        words(ss, nw0, nw1, niv);
     }
-    if (qn) drain();
+    while (ss < n_supers) {
+        const SeqSpan sp = a.spans[sid];
+        const uint64_t sbase = a.seq_base[sp.seq];
+        const uint32_t n = (uint32_t)a.seq_len[sp.seq];
+        SuperRegs R;
+        R.w0 = nw0;
+        R.w1 = nw1;
+        R.iv = niv;
+        R.base = sp.p_al + (uint32_t)(ss - sp.super0) * kSuper;
+        const uint32_t pb = R.base + (uint32_t)lane * kLanePos;
+        const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
+        const uint32_t okm = window_ok_mask(R.iv, W) &
+                             bit_range((int)sp.p_lo - (int)pb, (int)min<int64_t>((int64_t)sp.p_hi - pb, 32));
+        // prefetch the next super-step's words
+        const uint64_t nx = ss + stride;
+        if (nx < n_supers) {
+            locate(nx);
+            words(nx, nw0, nw1, niv);
+        }
+        uint32_t hits = probe8<0, kMode>(a, s_lf, d0, d1, d2, shw);
+        hits |= probe8<1, kMode>(a, s_lf, d0, d1, d2, shw);
+        hits |= probe8<2, kMode>(a, s_lf, d0, d1, d2, shw);
+        hits |= probe8<3, kMode>(a, s_lf, d0, d1, d2, shw);
+        hits &= okm;
+        // compact this super-step's seed hits into the wave queue (u16 offsets)
+        const uint32_t c = (uint32_t)__popc(hits);
+        const uint32_t incl = wave_incl_scan(c, lane);
+        const uint32_t total = __shfl(incl, 63, 64);
+        uint32_t o = incl - c;
+        while (hits) {
+            const int i = __clz(hits);
+            hits &= ~(0x80000000u >> i);
+            q[o++] = (uint16_t)(lane * kLanePos + i);
+        }
+        wave_sync();
+#if MP_ABLATE == 1 || MP_ABLATE == 3
+        ncand += total;
+#else
+        if (total) drain_seeds<kMode>(a, R, sbase, n, q, total, lane, ncand, s_wl[w]);
+#endif
+        ss = nx;
+    }
     // candidate statistics, one atomic per wave
     uint32_t tot = ncand;
 #pragma unroll
@@ -329,6 +620,9 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
     do {
         if (hipSetDevice(g->device) != hipSuccess) { rc = fail(MP_E_HIP, "hipSetDevice failed"); break; }
         if (hipMalloc(&s->counters, 64) != hipSuccess) { rc = fail(MP_E_NOMEM, "counter allocation failed"); break; }
+        if (hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess ||
+            s->n_cu <= 0)
+            s->n_cu = 256;
         if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) {
             rc = fail(MP_E_HIP, "event creation failed");
             break;
@@ -377,13 +671,13 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         const uint64_t phi = std::min<uint64_t>(khi + t->max_hash_off, n - W + 1);
         if (plo >= phi) continue;
         SeqSpan sp;
-        sp.tile0 = tiles;
+        sp.super0 = tiles;
         sp.seq = q;
         sp.p_lo = (uint32_t)plo;
         sp.p_hi = (uint32_t)phi;
-        sp.pad = 0;
+        sp.p_al = (uint32_t)(plo & ~(uint64_t)(kLanePos - 1));
         spans.push_back(sp);
-        tiles += (phi - plo + kTile - 1) / kTile;
+        tiles += (phi - sp.p_al + kSuper - 1) / kSuper;
         windows += phi - plo;
     }
     s->n_windows = windows;
@@ -392,6 +686,12 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     s->scan_ms = 0.f;
     if (n_hits) *n_hits = 0;
     if (!tiles) return MP_OK;
+    const uint32_t n_real_spans = (uint32_t)spans.size();
+    {
+        SeqSpan sentinel{};
+        sentinel.super0 = tiles;
+        spans.push_back(sentinel);
+    }
     if (spans.size() > s->spans_cap) {
         hipFree(s->spans);
         s->spans = nullptr;
@@ -403,29 +703,34 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
 
     ScanArgs a;
     a.g2 = g->g2; a.gexc = g->gexc; a.ginv = g->ginv;
-    a.xr_start = g->xr_start; a.xr_char = g->xr_char; a.n_xr = g->n_xr;
+    a.xr_start = g->xr_start; a.xr_char = g->xr_char; a.xr_dir = g->xr_dir; a.n_xr = g->n_xr;
+    a.has_u = g->has_u ? 1 : 0;
     a.seq_base = g->d_base; a.seq_len = g->d_len;
-    a.spans = s->spans; a.n_spans = (uint32_t)spans.size();
-    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.filt_direct = t->filt_direct;
+    a.spans = s->spans; a.n_spans = n_real_spans;
+    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
-    a.boff = t->boff; a.blist = t->blist; a.recs = t->recs; a.rank = t->rank;
+    a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
     a.planes = t->planes; a.pchars = t->pchars;
     a.W = t->prm.wordsize; a.M = t->prm.margin; a.N = t->prm.mismatches;
     a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
     a.g_lo = g_lo; a.g_hi = g_hi;
 
-    unsigned long long cnt[2] = {0, 0};
+    unsigned long long cnt[4] = {0, 0, 0, 0};
     for (int attempt = 0; attempt < 2; ++attempt) {
         a.hit_hi = s->keys;
         a.hit_lo = s->keys + s->cap;
         a.counters = s->counters;
         a.cap = s->cap;
-        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 16, st));
+        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 32, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-        hipLaunchKernelGGL(scan_kernel, dim3((uint32_t)tiles), dim3(kBlock), 0, st, a);
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
+                                                           (uint64_t)s->n_cu * kBlocksPerCU);
+        if (t->lds_exact) hipLaunchKernelGGL(scan_kernel<0>, dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct) hipLaunchKernelGGL(scan_kernel<1>, dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL(scan_kernel<2>, dim3(grid), dim3(kBlock), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
         MP_HIP_CHECK(hipEventRecord(s->ev1, st));
-        MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 16, hipMemcpyDeviceToHost, st));
+        MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 32, hipMemcpyDeviceToHost, st));
         MP_HIP_CHECK(hipStreamSynchronize(st));
         if (cnt[0] <= s->cap) break;
         int rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
@@ -434,6 +739,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     if (cnt[0] > s->cap) return fail(MP_E_STATE, "mp_search_run: hit buffer overflow after growth");
     MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->ev1));
     s->n_candidates = cnt[1];
+    s->n_survivors = cnt[2];
     const uint64_t nh = cnt[0];
     int rc = sort_hits(s, nh, st);
     if (rc) return rc;
@@ -485,6 +791,13 @@ MP_EXPORT int mp_search_last_stats(void* search, float* scan_ms, uint64_t* n_win
     if (scan_ms) *scan_ms = s->scan_ms;
     if (n_windows) *n_windows = s->n_windows;
     if (n_candidates) *n_candidates = s->n_candidates;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_search_survivors(void* search, uint64_t* n_survivors) {
+    Search* s = (Search*)search;
+    if (!s || !n_survivors) return fail(MP_E_ARG, "mp_search_survivors: null pointer");
+    *n_survivors = s->n_survivors;
     return MP_OK;
 }
 

@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->slots); hipFree(t->boff); hipFree(t->blist);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -136,16 +136,6 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         std::vector<uint32_t> fillp(boff.begin(), boff.end() - 1), blist(n_rec);
         for (uint32_t r = 0; r < n_rec; ++r) blist[fillp[rec_bucket[r]]++] = r;
 
-        // ---- open-addressed key -> bucket slots (load <= 0.5)
-        uint32_t lg = 6;
-        while ((1ull << lg) < 2ull * nb) ++lg;
-        t->slot_log2 = lg;
-        std::vector<uint64_t> slots(1ull << lg, kEmptySlot);
-        for (uint32_t b = 0; b < nb; ++b) {
-            uint32_t s = table_slot(bkey[b], lg);
-            while (slots[s] != kEmptySlot) s = (s + 1) & ((1u << lg) - 1);
-            slots[s] = ((uint64_t)bkey[b] << 32) | b;
-        }
 
         // ---- presence filter: direct bitmap for small W, hashed filter above
         t->filt_direct = (W <= (uint32_t)kDirectFilterMaxW);
@@ -154,6 +144,16 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         for (uint32_t b = 0; b < nb; ++b) {
             const uint32_t idx = t->filt_direct ? bkey[b] : filter_index(bkey[b], t->filt_log2);
             filt[idx >> 5] |= 1u << (idx & 31);
+        }
+        t->lds_exact = (2 * W <= (uint32_t)kLdsFilterLog2);
+        std::vector<uint32_t> lfilt(kLdsFilterWords, 0);
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t idx = lds_index(bkey[b], t->lds_exact);
+            lfilt[idx >> 5] |= 1u << (idx & 31);
+            if (kLdsHashes == 2 && !t->lds_exact) {
+                const uint32_t i2 = lds_index2(bkey[b]);
+                lfilt[i2 >> 5] |= 1u << (i2 & 31);
+            }
         }
 
         // ---- records, primer planes and bytes
@@ -192,6 +192,67 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             }
         }
         if (rc) break;
+        // ---- bucket-ordered entries with primer-1 fingerprints
+        std::vector<Entry> ents(n_rec);
+        for (uint32_t i = 0; i < n_rec; ++i) {
+            const uint32_t r = blist[i];
+            Entry& e = ents[i];
+            std::memset(&e, 0, sizeof(e));
+            e.rec = r;
+            e.hash_off = (uint16_t)recs[r].hash_off;
+            e.l1 = (uint16_t)recs[r].l1;
+            const uint64_t* pl = &planes[(size_t)recs[r].p1_pl * 4];
+            const uint32_t lim = std::min<uint32_t>(recs[r].l1, 32);
+            for (uint32_t q = 0; q < lim; ++q) {
+                const int bit = 62 - 2 * (int)q;
+                int nacc = 0, base = 0;
+                for (int b = 0; b < 4; ++b)
+                    if ((pl[b] >> bit) & 1) { ++nacc; base = b; }
+                if (nacc == 1) {
+                    e.code |= (uint64_t)base << bit;
+                    e.pmask |= 1ull << bit;
+                } else if (nacc == 0) {
+                    e.pmask |= 1ull << (bit + 1);
+                }
+            }
+        }
+        for (uint32_t b = 0; b < nb; ++b) {  // bucket heads carry the bucket's size
+            ents[boff[b]].count = bcount[b];
+            ents[boff[b]].xstart = boff[b] + 1;
+        }
+        std::vector<uint2> rk;
+        std::vector<Entry> dents;
+        std::vector<Slot> slots;
+        if (t->filt_direct) {
+            // rank bitmap over the exact 4^W presence bitmap; heads in key order
+            rk.resize(filt.size());
+            uint32_t acc = 0;
+            for (size_t w = 0; w < filt.size(); ++w) {
+                rk[w].x = filt[w];
+                rk[w].y = acc;
+                acc += (uint32_t)__builtin_popcount(filt[w]);
+            }
+            dents.resize(std::max<uint32_t>(nb, 1));
+            for (uint32_t b = 0; b < nb; ++b) {
+                const uint32_t k = bkey[b];
+                const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
+                dents[rank] = ents[boff[b]];
+            }
+            filt.assign(1, 0);
+        } else {
+            uint32_t lg = 6;
+            while ((1ull << lg) < 2ull * nb) ++lg;
+            t->slot_log2 = lg;
+            slots.resize(1ull << lg);
+            std::memset(slots.data(), 0, slots.size() * sizeof(Slot));
+            for (uint32_t b = 0; b < nb; ++b) {
+                uint32_t s = table_slot(bkey[b], lg);
+                while (slots[s].used) s = (s + 1) & ((1u << lg) - 1);
+                slots[s].key = bkey[b];
+                slots[s].used = 1;
+                slots[s].e0 = ents[boff[b]];
+            }
+        }
         // Ties at equal amplicon start are ordered by (hash_offset, record index):
         // rank[] encodes that order in 32 bits for the device sort.
         std::vector<uint32_t> order(n_rec), rank(n_rec);
@@ -204,9 +265,11 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
 
         uint64_t bytes = 0;
         if ((rc = upload(&t->filt, filt.data(), filt.size(), &bytes))) break;
+        if ((rc = upload(&t->lfilt, lfilt.data(), lfilt.size(), &bytes))) break;
         if ((rc = upload(&t->slots, slots.data(), slots.size(), &bytes))) break;
-        if ((rc = upload(&t->boff, boff.data(), boff.size(), &bytes))) break;
-        if ((rc = upload(&t->blist, blist.data(), blist.size(), &bytes))) break;
+        if ((rc = upload(&t->rk, rk.data(), rk.size(), &bytes))) break;
+        if ((rc = upload(&t->dents, dents.data(), dents.size(), &bytes))) break;
+        if ((rc = upload(&t->ents, ents.data(), ents.size(), &bytes))) break;
         if ((rc = upload(&t->recs, recs.data(), recs.size(), &bytes))) break;
         if ((rc = upload(&t->rank, rank.data(), rank.size(), &bytes))) break;
         if ((rc = upload(&t->inv_rank, order.data(), order.size(), &bytes))) break;

@@ -1,0 +1,78 @@
+"""Time ablation variants of the scan kernel on the same resident c3 data (timing only).
+
+Builds libmerpcr_hip_ablateN.so with -DMP_ABLATE=N next to the product library,
+generates the workload once, and for each variant packs the genome, runs the
+search `--steps` times and prints the mean scan-kernel time.  Hit counts of the
+variants are meaningless except for variant 0 (the product kernel).
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,4,5")
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--build-only", action="store_true")
+    args = ap.parse_args()
+    from merpcr_amd import _build
+    variants = [int(v) for v in args.variants.split(",")]
+    libs = {}
+    for v in variants:
+        # 0 = product; 1-5 = MP_ABLATE=v; 12 = product with the 2-probe LDS prefilter
+        defs = () if v == 0 else (("MP_LDS_HASHES=2",) if v == 12 else (f"MP_ABLATE={v}",))
+        path = _build.LIB if v == 0 else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{v}.so")
+        libs[v] = _build.build_native(defines=defs, lib=path)
+    if args.build_only:
+        return
+    import ctypes
+    import torch
+    from merpcr_amd import MerPCR, _native, synth
+    cfg = dict(synth.CONFIGS[args.config])
+    total = int(cfg["total"] * args.scale) // 64 * 64
+    n_sts = max(1, int(cfg["n_sts"] * args.scale))
+    sts = synth.make_sts(n_sts, W=cfg["W"], iupac=cfg["iupac"])
+    dev = torch.device("cuda", 0)
+    names, lens, buf, offs, planted = synth.build_genome_torch(
+        total, cfg["records"], sts, seed=1, N=cfg["N"], M=cfg["M"], W=cfg["W"], nrun=cfg["nrun"], device=dev)
+    torch.cuda.synchronize()
+    with tempfile.NamedTemporaryFile("w", suffix=".sts", delete=False) as fh:
+        fh.write(sts.text())
+    out = {}
+    for v in variants:
+        lib = ctypes.CDLL(libs[v])
+        _native._sig(lib)
+        _native._lib = lib
+        eng = MerPCR(wordsize=cfg["W"], margin=cfg["M"], mismatches=cfg["N"], iupac_mode=cfg["I"])
+        assert eng.load_sts_file(fh.name)
+        table = eng.device_table()
+        genome = _native.Genome(0, lens)
+        for r, n in enumerate(lens):
+            genome.put_device(r, buf.data_ptr() + int(offs[r]), n)
+        genome.seal()
+        s = _native.Search(table, genome)
+        s.run()
+        ms = []
+        for _ in range(args.steps):
+            n = s.run()
+            ms.append(s.last_stats()["scan_ms"])
+        st = s.last_stats()
+        out[v] = {"scan_ms": round(sum(ms) / len(ms), 3), "hits": n, "candidates": st["candidates"],
+                  "survivors": st["survivors"]}
+        print(f"variant {v}: {out[v]}", flush=True)
+        s.close(); genome.close(); table.close()
+        eng._dev_table = None
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
