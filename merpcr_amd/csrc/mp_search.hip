@@ -143,11 +143,14 @@ __device__ __forceinline__ uint64_t spread32(uint32_t v) {
 // skipped.  Every counted position is a real mismatch of engine.py:599-642, so a
 // rejection here is exact.
 __device__ __forceinline__ bool fp_reject(const ScanArgs& a, uint64_t G, uint32_t ex, uint32_t l1, uint64_t code,
-                                          uint64_t pmask) {
+                                          uint64_t pmask, bool& exact) {
     const int len = (int)min(l1, 32u);
     const uint64_t inside = sp_lt(len);
     const uint64_t x = G ^ code;
     const uint64_t plain = pmask & kEven;
+    // the bound is the exact mismatch count when every position was decidable: primer
+    // within 32 bases, each base plain or never, no genome exception base
+    exact = l1 <= 32u && ex == 0 && (inside & ~((pmask | (pmask >> 1)) & kEven)) == 0;
     uint64_t d = (((x | (x >> 1)) & plain) | ((pmask >> 1) & kEven)) & inside;
     if (ex) {
         const uint64_t es = spread32(ex) & inside;
@@ -169,14 +172,15 @@ __device__ __forceinline__ void emit(const ScanArgs& a, uint64_t gk, uint32_t ra
 }
 
 // _match_sts (engine.py:507-597) for one fingerprint survivor (record `rec`, amplicon
-// start k), executed by the whole wave: every lane re-checks primer 1 (same addresses,
-// broadcast loads) and the lanes split the amplicon-end offsets d in [-lo, hi] (the
-// reference's try order is restored by the device sort through try_rank(d)).
+// start k), executed by the whole wave: unless the fingerprint test was already exact,
+// every lane re-checks primer 1 (same addresses, broadcast loads); the lanes split the
+// amplicon-end offsets d in [-lo, hi] (the reference's try order is restored by the
+// device sort through try_rank(d)).
 __device__ void pair_check_wave(const ScanArgs& a, uint64_t sbase, uint32_t n, uint32_t k, uint32_t rec,
-                                int lane) {
+                                bool p1_exact, int lane) {
     const DevRec r = a.recs[rec];
     const uint64_t gk = sbase + k;
-    if (!primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true)) return;
+    if (!p1_exact && !primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true)) return;
     const uint32_t avail = n - k - r.l1;
     if (avail < r.l2) return;
     uint32_t e;
@@ -214,6 +218,8 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 struct WaveLds {           // per-wave LDS scratch of the drain
+    uint32_t h_mask[64];   // seed hits of the super-step, per lane (bit 31-i = window i)
+    uint32_t h_pre[64];    // exclusive prefix of the per-lane hit counts
     uint32_t sv_k[64];     // survivors of one pass (at most one per lane)
     uint32_t sv_r[64];
     uint32_t x_pos[64];    // bucket tails of one pass
@@ -258,7 +264,7 @@ __device__ __forceinline__ void window_from_regs(const ScanArgs& a, const SuperR
 // All lanes must call (shuffles); `act` marks lanes that hold a candidate.
 __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
                                           bool act, uint32_t pos, const Entry& e, uint32_t& ncand, uint32_t& k_out,
-                                          uint64_t Gpos, uint32_t expos, bool reuse) {
+                                          uint64_t Gpos, uint32_t expos, bool reuse, bool& exact) {
     const uint32_t k = pos - e.hash_off;
     act = act && pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
     act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
@@ -270,7 +276,7 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
     }
     if (!act) return false;
     ++ncand;
-    if (fp_reject(a, G, ex, e.l1, e.code, e.pmask)) return false;
+    if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) return false;
     k_out = k;
     return true;
 }
@@ -278,19 +284,22 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
 // Compact this pass's survivors (one per lane at most) and pair-check each with the
 // whole wave.
 __device__ __forceinline__ void flush_survivors(const ScanArgs& a, uint64_t sbase, uint32_t n, bool surv,
-                                                uint32_t k, uint32_t rec, int lane, WaveLds& L) {
+                                                uint32_t k, uint32_t rec, bool exact, int lane, WaveLds& L) {
     const uint64_t m = __ballot(surv);
     if (!m) return;
     if (surv) {
         const uint32_t i = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         L.sv_k[i] = k;
-        L.sv_r[i] = rec;
+        L.sv_r[i] = rec | (exact ? 0x80000000u : 0u);  // record ids are < 2^31
     }
     if (lane == 0) atomicAdd(&a.counters[2], (unsigned long long)__popcll(m));
     wave_sync();
 #if MP_ABLATE != 5
     const uint32_t ns = (uint32_t)__popcll(m);
-    for (uint32_t i = 0; i < ns; ++i) pair_check_wave(a, sbase, n, L.sv_k[i], L.sv_r[i], lane);
+    for (uint32_t i = 0; i < ns; ++i) {
+        const uint32_t rv = L.sv_r[i];
+        pair_check_wave(a, sbase, n, L.sv_k[i], rv & 0x7FFFFFFFu, (rv >> 31) != 0, lane);
+    }
 #endif
     wave_sync();
 }
@@ -321,56 +330,93 @@ __device__ __forceinline__ bool bucket_head(const ScanArgs& a, uint32_t h, Entry
 // Drain a wave's seed queue: one lane per queued seed looks up its bucket head and
 // tests it; bucket tails are expanded 64 candidates at a time.  Every pass yields at
 // most 64 survivors.
+// e-th seed of the super-step: lane by prefix search, window by n-th set bit.
+__device__ __forceinline__ uint32_t seed_offset(const WaveLds& L, uint32_t e) {
+    uint32_t lo = 0, hi = 64;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.h_pre[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    uint32_t m = L.h_mask[lo];
+    for (uint32_t r = e - L.h_pre[lo]; r; --r) m &= ~(0x80000000u >> __clz(m));
+    return lo * kLanePos + (uint32_t)__clz(m);
+}
+
+// Candidate test of one bucket head per lane, survivors, then the bucket tails.
+template <int kMode>
+__device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRegs& R, uint64_t sbase,
+                                                uint32_t n, bool have, uint32_t pos, const Entry& e0, uint64_t Gp,
+                                                uint32_t exp_, int lane, uint32_t& ncand, WaveLds& L) {
+    uint32_t sk = 0;
+    bool ex0 = false;
+    const bool surv = candidate(a, R, sbase, n, have, pos, e0, ncand, sk, Gp, exp_, true, ex0);
+    flush_survivors(a, sbase, n, surv, sk, e0.rec, ex0, lane, L);
+    const uint32_t xc = have ? e0.count - 1u : 0u;
+    const uint32_t incl = wave_incl_scan(xc, lane);
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (total) {
+        L.x_pos[lane] = pos;
+        L.x_start[lane] = e0.xstart;
+        L.x_pre[lane] = incl - xc;
+        wave_sync();
+        for (uint32_t c0 = 0; c0 < total; c0 += 64) {
+            const uint32_t c = c0 + (uint32_t)lane;
+            const bool act = c < total;
+            uint32_t lo = 0;
+            if (act) {
+                uint32_t hi = 64;  // last lane with x_pre <= c
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (L.x_pre[mid] <= c) lo = mid;
+                    else hi = mid;
+                }
+            }
+            Entry ej{};
+            if (act) ej = a.ents[L.x_start[lo] + (c - L.x_pre[lo])];
+            bool ex2 = false;
+            const bool s2 = candidate(a, R, sbase, n, act, L.x_pos[lo], ej, ncand, sk, 0, 0, false, ex2);
+            flush_survivors(a, sbase, n, s2, sk, ej.rec, ex2, lane, L);
+        }
+        wave_sync();
+    }
+}
+
+// Drain a super-step's seeds, two per lane per pass (128 per pass): both lanes'
+// lookup chains (rank word -> bucket head) are in flight together.
 template <int kMode>
 __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
-                                            const uint16_t* q, uint32_t qn, int lane, uint32_t& ncand,
-                                            WaveLds& L) {
+                                            uint32_t qn, int lane, uint32_t& ncand, WaveLds& L) {
     const uint32_t shw = 64u - 2u * (uint32_t)a.W;
-    for (uint32_t b = 0; b < qn; b += 64) {
-        const uint32_t e = b + (uint32_t)lane;
-        const bool live = e < qn;
-        const uint32_t pos = R.base + (live ? q[e] : 0u);
-        uint64_t Gp;
-        uint32_t exp_;
-        window_from_regs(a, R, sbase, pos, true, Gp, exp_);
-        const uint32_t h = (uint32_t)(Gp >> shw);
-        Entry e0{};
-        const bool have = live && bucket_head<kMode>(a, h, e0);
+    for (uint32_t b = 0; b < qn; b += 128) {
+        const uint32_t ea = b + (uint32_t)lane, eb = ea + 64;
+        const bool la = ea < qn, lb = eb < qn;
+        const uint32_t pa = R.base + (la ? seed_offset(L, ea) : 0u);
+        const uint32_t pb = R.base + (lb ? seed_offset(L, eb) : 0u);
+        uint64_t Ga, Gb;
+        uint32_t xa, xb;
+        window_from_regs(a, R, sbase, pa, true, Ga, xa);
+        window_from_regs(a, R, sbase, pb, true, Gb, xb);
+        const uint32_t ha = (uint32_t)(Ga >> shw), hb = (uint32_t)(Gb >> shw);
+        Entry e0a{}, e0b{};
+        bool hva, hvb;
+        if constexpr (kMode != 2) {
+            const uint2 ra = la ? a.rk[ha >> 5] : make_uint2(0, 0);
+            const uint2 rb = lb ? a.rk[hb >> 5] : make_uint2(0, 0);
+            hva = (ra.x >> (ha & 31u)) & 1u;
+            hvb = (rb.x >> (hb & 31u)) & 1u;
+            if (hva) e0a = a.dents[ra.y + (uint32_t)__popc(ra.x & ((1u << (ha & 31u)) - 1u))];
+            if (hvb) e0b = a.dents[rb.y + (uint32_t)__popc(rb.x & ((1u << (hb & 31u)) - 1u))];
+        } else {
+            hva = la && bucket_head<kMode>(a, ha, e0a);
+            hvb = lb && bucket_head<kMode>(a, hb, e0b);
+        }
 #if MP_ABLATE == 4
-        ncand += have && e0.rec == 0xFFFFFFFFu;
+        ncand += (hva && e0a.rec == 0xFFFFFFFFu) + (hvb && e0b.rec == 0xFFFFFFFFu);
         continue;
 #endif
-        uint32_t sk = 0;
-        const bool surv = candidate(a, R, sbase, n, have, pos, e0, ncand, sk, Gp, exp_, true);
-        flush_survivors(a, sbase, n, surv, sk, e0.rec, lane, L);
-        // bucket tails
-        const uint32_t xc = have ? e0.count - 1u : 0u;
-        const uint32_t incl = wave_incl_scan(xc, lane);
-        const uint32_t total = __shfl(incl, 63, 64);
-        if (total) {
-            L.x_pos[lane] = pos;
-            L.x_start[lane] = e0.xstart;
-            L.x_pre[lane] = incl - xc;
-            wave_sync();
-            for (uint32_t c0 = 0; c0 < total; c0 += 64) {
-                const uint32_t c = c0 + (uint32_t)lane;
-                const bool act = c < total;
-                uint32_t lo = 0;
-                if (act) {
-                    uint32_t hi = 64;  // last lane with x_pre <= c
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (L.x_pre[mid] <= c) lo = mid;
-                        else hi = mid;
-                    }
-                }
-                Entry ej{};
-                if (act) ej = a.ents[L.x_start[lo] + (c - L.x_pre[lo])];
-                const bool s2 = candidate(a, R, sbase, n, act, L.x_pos[lo], ej, ncand, sk, 0, 0, false);
-                flush_survivors(a, sbase, n, s2, sk, ej.rec, lane, L);
-            }
-            wave_sync();
-        }
+        heads_and_tails<kMode>(a, R, sbase, n, hva, pa, e0a, Ga, xa, lane, ncand, L);
+        if (b + 64 < qn) heads_and_tails<kMode>(a, R, sbase, n, hvb, pb, e0b, Gb, xb, lane, ncand, L);
     }
 }
 
@@ -410,49 +456,67 @@ __device__ __forceinline__ uint32_t kmer_top(uint32_t d0, uint32_t d1, uint32_t 
     else return __builtin_amdgcn_alignbit(hi, lo, 32 - r);
 }
 
-// Seed filter for 8 consecutive windows of a lane.  Level 1: the LDS prefilter
-// (random ds_read_b32).  Level 2 (unless the LDS filter is the exact 4^W bitmap): the
-// global presence bitmap, probed only by lanes whose level-1 bit is set -- the others
-// load word 0, so their requests coalesce into one line.  All 8 loads of a level are
-// issued before any result is used.
-template <int SUB, int kMode>
-__device__ __forceinline__ uint32_t probe8(const ScanArgs& a, const uint32_t* __restrict__ lds, uint32_t d0,
-                                           uint32_t d1, uint32_t d2, uint32_t shw) {
+// Seed filter for the lane's 32 windows.  Level 1: the LDS prefilter (32 random
+// ds_read_b32).  Level 2 (unless the LDS filter is the exact 4^W bitmap): the global
+// presence bitmap, probed only for windows whose level-1 bit is set -- other lanes'
+// requests go to word 0 and coalesce into one line.  All 32 level-2 loads are issued
+// before the first result is consumed (one L2 round trip per super-step); the
+// returned `issue_next` hook runs between issue and consumption so that younger loads
+// (the next super-step's prefetch) do not gate the probe results.
+template <int kMode, class F>
+__device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* __restrict__ lds, uint32_t d0,
+                                            uint32_t d1, uint32_t d2, uint32_t shw, uint32_t okm, F&& issue_next) {
     // kMode 0: LDS exact; 1: LDS hashed + exact rank bitmap; 2: LDS hashed + hashed filter
-    uint32_t h[kSub], lw[kSub];
+    uint32_t lmask = 0;
     [&]<int... T>(std::integer_sequence<int, T...>) {
-        ((h[T] = kmer_top<SUB * kSub + T>(d0, d1, d2) >> shw), ...);
-    }(std::make_integer_sequence<int, kSub>{});
-#pragma unroll
-    for (int t = 0; t < kSub; ++t) {
-        const uint32_t li = lds_index(h[t], kMode == 0);
-        lw[t] = (lds[li >> 5] >> (li & 31)) & 1u;
-        if constexpr (kLdsHashes == 2 && kMode != 0) {
-            const uint32_t l2 = lds_index2(h[t]);
-            lw[t] &= (lds[l2 >> 5] >> (l2 & 31)) & 1u;
-        }
-    }
-    uint32_t hits = 0;
+        ((
+            [&] {
+                const uint32_t h = kmer_top<T>(d0, d1, d2) >> shw;
+                const uint32_t li = lds_index(h, kMode == 0);
+                uint32_t bit = (lds[li >> 5] >> (li & 31)) & 1u;
+                if constexpr (kLdsHashes == 2 && kMode != 0) {
+                    const uint32_t l2 = lds_index2(h);
+                    bit &= (lds[l2 >> 5] >> (l2 & 31)) & 1u;
+                }
+                lmask |= bit << (31 - T);
+            }()),
+         ...);
+    }(std::make_integer_sequence<int, 32>{});
+    lmask &= okm;
     if constexpr (kMode == 0) {
-#pragma unroll
-        for (int t = 0; t < kSub; ++t) hits |= lw[t] << (31 - (SUB * kSub + t));
+        issue_next();
+        return lmask;
     } else {
-        uint32_t gw[kSub], gb[kSub];
-#pragma unroll
-        for (int t = 0; t < kSub; ++t) {
-            const uint32_t fi = kMode == 1 ? h[t] : filter_index(h[t], a.filt_log2);
-            gb[t] = fi & 31;
+        uint32_t gw[32];
+        [&]<int... T>(std::integer_sequence<int, T...>) {
+            ((
+                [&] {
+                    const uint32_t h = kmer_top<T>(d0, d1, d2) >> shw;
+                    const uint32_t fi = kMode == 1 ? h : filter_index(h, a.filt_log2);
+                    const bool on = (lmask >> (31 - T)) & 1u;
 #if MP_ABLATE == 2 || MP_ABLATE == 3
-            gw[t] = (h[t] * 2654435761u) >> 27 == 0 ? 0xFFFFFFFFu : 0u;
+                    gw[T] = (h * 2654435761u) >> 27 == 0 ? 0xFFFFFFFFu : 0u;
+                    (void)on; (void)fi;
 #else
-            if constexpr (kMode == 1) gw[t] = a.rk[lw[t] ? (fi >> 5) : 0u].x;
-            else gw[t] = a.filt[lw[t] ? (fi >> 5) : 0u];
+                    if constexpr (kMode == 1) gw[T] = a.rk[on ? (fi >> 5) : 0u].x;
+                    else gw[T] = a.filt[on ? (fi >> 5) : 0u];
 #endif
-        }
-#pragma unroll
-        for (int t = 0; t < kSub; ++t) hits |= (lw[t] & (gw[t] >> gb[t])) << (31 - (SUB * kSub + t));
+                }()),
+             ...);
+        }(std::make_integer_sequence<int, 32>{});
+        issue_next();
+        uint32_t hits = 0;
+        [&]<int... T>(std::integer_sequence<int, T...>) {
+            ((
+                [&] {
+                    const uint32_t h = kmer_top<T>(d0, d1, d2) >> shw;
+                    const uint32_t fi = kMode == 1 ? h : filter_index(h, a.filt_log2);
+                    hits |= ((gw[T] >> (fi & 31)) & 1u) << (31 - T);
+                }()),
+             ...);
+        }(std::make_integer_sequence<int, 32>{});
+        return hits & lmask;
     }
-    return hits;
 }
 
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
@@ -461,7 +525,6 @@ __device__ __forceinline__ uint32_t probe8(const ScanArgs& a, const uint32_t* __
 template <int kMode>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
-    __shared__ uint16_t q_off[kWaves][kSuper];
     __shared__ WaveLds s_wl[kWaves];
 
     // stage the seed prefilter in LDS (once per persistent workgroup)
@@ -475,29 +538,37 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     const uint64_t n_supers = a.spans[a.n_spans].super0;
     const uint32_t W = (uint32_t)a.W;
     const uint32_t shw = 32u - 2u * W;
-    uint16_t* q = q_off[w];
+    WaveLds& L = s_wl[w];
     uint32_t ncand = 0;
 
     uint64_t ss = (uint64_t)blockIdx.x * kWaves + (uint64_t)w;
-    uint32_t sid = 0;
-    auto locate = [&](uint64_t x) {  // span holding super-step x (wave-uniform)
-        if (x >= a.spans[sid].super0 && x < a.spans[sid + 1].super0) return;
+    // span of the super-step being prefetched, cached in registers (wave-uniform): the
+    // common path of the prefetch issues only the four plane loads, no waits
+    SeqSpan pf{};
+    pf.super0 = 1;
+    uint64_t pf_end = 0, pf_sbase = 0;
+    uint32_t pf_n = 0;
+    auto locate = [&](uint64_t x) {
+        if (x >= pf.super0 && x < pf_end) return;
         uint32_t lo = 0, hi = a.n_spans;
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (a.spans[mid].super0 <= x) lo = mid;
             else hi = mid;
         }
-        sid = lo;
+        pf = a.spans[lo];
+        pf_end = a.spans[lo + 1].super0;
+        pf_sbase = a.seq_base[pf.seq];
+        pf_n = (uint32_t)a.seq_len[pf.seq];
     };
     auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& iv) {
-        const SeqSpan sp = a.spans[sid];
-        const uint64_t j = a.seq_base[sp.seq] + sp.p_al + (x - sp.super0) * kSuper + (uint64_t)lane * kLanePos;
+        const uint64_t j = pf_sbase + pf.p_al + (x - pf.super0) * kSuper + (uint64_t)lane * kLanePos;
         w0 = a.g2[j >> 5];
         w1 = a.g2[(j >> 5) + 1];
         const uint64_t v0 = a.ginv[j >> 6];
         const uint64_t v1 = a.ginv[(j >> 6) + 1];
-        iv = (j & 32) ? ((v0 << 32) | (v1 >> 32)) : v0;
+        const uint32_t sh = (uint32_t)(j & 32);  // branch-free: both loads always issue
+        iv = (v0 << sh) | ((v1 >> (63 - sh)) >> 1);
     };
     uint64_t nw0 = 0, nw1 = 0, niv = 0;
     if (ss < n_supers) {
@@ -505,9 +576,9 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         words(ss, nw0, nw1, niv);
     }
     while (ss < n_supers) {
-        const SeqSpan sp = a.spans[sid];
-        const uint64_t sbase = a.seq_base[sp.seq];
-        const uint32_t n = (uint32_t)a.seq_len[sp.seq];
+        const SeqSpan sp = pf;
+        const uint64_t sbase = pf_sbase;
+        const uint32_t n = pf_n;
         SuperRegs R;
         R.w0 = nw0;
         R.w1 = nw1;
@@ -517,32 +588,28 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
         const uint32_t okm = window_ok_mask(R.iv, W) &
                              bit_range((int)sp.p_lo - (int)pb, (int)min<int64_t>((int64_t)sp.p_hi - pb, 32));
-        // prefetch the next super-step's words
         const uint64_t nx = ss + stride;
-        if (nx < n_supers) {
-            locate(nx);
-            words(nx, nw0, nw1, niv);
-        }
-        uint32_t hits = probe8<0, kMode>(a, s_lf, d0, d1, d2, shw);
-        hits |= probe8<1, kMode>(a, s_lf, d0, d1, d2, shw);
-        hits |= probe8<2, kMode>(a, s_lf, d0, d1, d2, shw);
-        hits |= probe8<3, kMode>(a, s_lf, d0, d1, d2, shw);
-        hits &= okm;
-        // compact this super-step's seed hits into the wave queue (u16 offsets)
+        uint32_t hits = probe32<kMode>(a, s_lf, d0, d1, d2, shw, okm, [&] {
+            // prefetch the next super-step's words (issued after this step's probes)
+            if (nx < n_supers) {
+                locate(nx);
+                words(nx, nw0, nw1, niv);
+            }
+        });
+        // publish this super-step's seed hits: per-lane masks + prefix of their counts
         const uint32_t c = (uint32_t)__popc(hits);
         const uint32_t incl = wave_incl_scan(c, lane);
         const uint32_t total = __shfl(incl, 63, 64);
-        uint32_t o = incl - c;
-        while (hits) {
-            const int i = __clz(hits);
-            hits &= ~(0x80000000u >> i);
-            q[o++] = (uint16_t)(lane * kLanePos + i);
-        }
-        wave_sync();
 #if MP_ABLATE == 1 || MP_ABLATE == 3
         ncand += total;
 #else
-        if (total) drain_seeds<kMode>(a, R, sbase, n, q, total, lane, ncand, s_wl[w]);
+        if (total) {
+            L.h_mask[lane] = hits;
+            L.h_pre[lane] = incl - c;
+            wave_sync();
+            drain_seeds<kMode>(a, R, sbase, n, total, lane, ncand, L);
+            wave_sync();
+        }
 #endif
         ss = nx;
     }

@@ -93,6 +93,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
     if (p.margin < 0 || p.margin > 10000) return fail(MP_E_ARG, "Margin must be between 0 and 10000");
     if (p.three_prime_match < 0) return fail(MP_E_ARG, "Three prime match must be at least 0");
     if (p.iupac_mode != 0 && p.iupac_mode != 1) return fail(MP_E_ARG, "iupac_mode must be 0 or 1");
+    if (n_rec >= 0x80000000u) return fail(MP_E_ARG, "too many records (max 2^31 - 1)");
     if (n_rec && (!key || !hash_off || !pcr_size || !primer1 || !p1_off || !primer2 || !p2_off))
         return fail(MP_E_ARG, "mp_table_create: null record array");
 
