@@ -37,6 +37,25 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(workload: str):
+    """HBM bytes per scan launch from the newest committed PMC pass of this workload
+    (profiles/<tag>_pmc.json next to the bench line it was collected with), else None."""
+    import glob
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")):
+        tag = os.path.basename(f)[:-len("_pmc.json")]
+        bj = os.path.join(ROOT, "profiles", f"{tag}_bench.json")
+        try:
+            if json.load(open(bj))["config"]["workload"] != workload:
+                continue
+            d = json.load(open(f))
+        except (OSError, ValueError, KeyError):
+            continue
+        if "hbm_traffic_bytes_per_launch" in d and (best is None or os.path.getmtime(f) > best[0]):
+            best = (os.path.getmtime(f), d["hbm_traffic_bytes_per_launch"], tag)
+    return (best[1], best[2]) if best else (None, None)
+
+
 def cpu_baseline(eng, names, lens, buf, offs, cfg, hits_dev, budget_s: float, threads: int):
     """Time the C oracle (scalar restatement, `threads` pthreads over k ranges) on whole
     leading records of the same genome, and check its hits against the GPU's."""
@@ -179,6 +198,9 @@ def main():
     kern_s = float(np.mean(scan_ms)) / 1e3
     alg_bytes = BYTES_PER_BASE * st["windows"] + BYTES_PER_HIT * nhits  # rank 0's scan launch
     achieved = alg_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
+    workload = (f"{args.config}: {n_sts} STS vs {bases / 1e9:.3f} Gbp ({len(lens)} records), "
+                f"W={cfg['W']} N={cfg['N']} M={cfg['M']} I={cfg['I']}")
+    traffic, traffic_src = pmc_traffic(workload) if world == 1 else (None, None)
     out = {
         "metric": METRIC,
         "value": round(bases / t_step / 1e9, 4),
@@ -192,8 +214,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded generator, merpcr_amd/synth.py; genome generated in HBM)",
-        "config": {"workload": f"{args.config}: {n_sts} STS vs {bases / 1e9:.3f} Gbp ({len(lens)} records), "
-                               f"W={cfg['W']} N={cfg['N']} M={cfg['M']} I={cfg['I']}",
+        "config": {"workload": workload,
                    "sts": n_sts, "records": len(lens), "bases": int(bases), "W": cfg["W"], "N": cfg["N"],
                    "M": cfg["M"], "I": cfg["I"], "parallelism": f"owned-k shards x{world}"},
         "hits": int(tot_hits),
@@ -202,7 +223,10 @@ def main():
         "kernel_gbps_bases": round(st["windows"] / kern_s / 1e9, 3) if kern_s > 0 else None,
         "candidates": st["candidates"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": int(traffic) if traffic else None,
+                     "traffic_source": f"profiles/{traffic_src}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, "
+                                       "gfx950-corrected; includes Infinity-Cache hits)" if traffic else None,
                      "kernel": "mp::scan_kernel", "alg_bytes_per_launch": int(alg_bytes)},
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,46 @@
+"""Copy a round's rocprofv3 summaries from gpurun_out/ into profiles/ and derive traffic.
+
+usage: python scripts/collect_profile.py <tag>   (reads gpurun_out/prof_<tag>)
+Writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_bench.json (the bench line printed
+under the trace pass) and profiles/<tag>_pmc.json (per-dispatch counter means for the scan
+kernel plus HBM traffic per launch, gfx950-corrected as MI355X_MICROARCH.md prescribes:
+FETCH_SIZE is in KiB and reports half of a wide streaming read, so read bytes = 2 x
+FETCH_SIZE x 1024; WRITE_SIZE x 1024 for writes).
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag = sys.argv[1]
+src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+dst = os.path.join(ROOT, "profiles")
+os.makedirs(dst, exist_ok=True)
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+bench = [l for l in open(os.path.join(src, "trace.log")) if l.startswith("{")]
+if bench:
+    open(os.path.join(dst, f"{tag}_bench.json"), "w").write(bench[-1])
+pmc = {}
+for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv"))):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        if "scan_kernel" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, v in agg.items():
+        pmc[k] = sum(v) / len(v)
+trace_ns = None
+for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
+    if "scan_kernel" in r["Name"]:
+        trace_ns = float(r["AverageNs"])
+out = {"kernel": "mp::scan_kernel", "avg_duration_ns_trace": trace_ns, "counters_mean_per_dispatch": pmc}
+if "FETCH_SIZE" in pmc:
+    rd = 2 * pmc["FETCH_SIZE"] * 1024
+    wr = pmc.get("WRITE_SIZE", 0.0) * 1024
+    out["hbm_traffic_bytes_per_launch"] = rd + wr
+    out["traffic_note"] = "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB; L3 hits are counted"
+json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))

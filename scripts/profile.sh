@@ -1,21 +1,23 @@
 #!/bin/bash
-# Kernel trace + PMC passes of bench.py on the GPU box (each counter set in its own run).
-# usage: bash scripts/profile.sh <tag> [bench args...]
+# rocprofv3 evidence for one round: kernel-trace stats of the bench command itself,
+# then one PMC pass per counter set (never combined with tracing domains).
+# usage: bash scripts/profile.sh <tag> [extra bench args...]
 set -o pipefail
 TAG=${1:-r01}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--no-cpu-baseline --steps 5 --warmup 1 $*"
-run() {  # name, rocprof args...
-  local name=$1; shift
-  timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- python3 "$R/bench.py" $ARGS \
+run() {  # name, bench-args, rocprof args...
+  local name=$1; local bargs=$2; shift 2
+  timeout -k 10 400 rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- python3 "$R/bench.py" $bargs \
       > "$OUT/$name.log" 2>&1 || { echo "pass $name failed rc=$?"; tail -5 "$OUT/$name.log"; exit 1; }
   echo "pass $name ok"
 }
-run trace --kernel-trace --stats
-run fetch --pmc FETCH_SIZE --kernel-include-regex scan_kernel
-run write --pmc WRITE_SIZE --kernel-include-regex scan_kernel
-run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY --kernel-include-regex scan_kernel
-run tcc --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex scan_kernel
+run trace "$*" --kernel-trace --stats
+Q="--no-cpu-baseline --steps 5 --warmup 1 $*"
+run fetch "$Q" --pmc FETCH_SIZE --kernel-include-regex scan_kernel
+run write "$Q" --pmc WRITE_SIZE --kernel-include-regex scan_kernel
+run sq "$Q" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY --kernel-include-regex scan_kernel
+run tcc "$Q" --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex scan_kernel
+run lds "$Q" --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --kernel-include-regex scan_kernel
