@@ -170,10 +170,13 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scan_ms, nhits = [], 0
+    scan_ms, pair_ms, order_ms, nhits = [], [], [], 0
     for _ in range(args.steps):
         nhits = step()
-        scan_ms.append(search.last_stats()["scan_ms"])
+        ls = search.last_stats()
+        scan_ms.append(ls["scan_ms"])
+        pair_ms.append(ls["pair_ms"])
+        order_ms.append(ls["order_ms"])
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -220,6 +223,9 @@ def main():
         "hits": int(tot_hits),
         "hits_per_s": round(tot_hits / t_step, 1),
         "scan_kernel_ms": round(kern_s * 1e3, 3),
+        "pair_kernel_ms": round(float(np.mean(pair_ms)), 3),
+        "order_ms": round(float(np.mean(order_ms)), 3),
+        "survivors": st["survivors"],
         "kernel_gbps_bases": round(st["windows"] / kern_s / 1e9, 3) if kern_s > 0 else None,
         "candidates": st["candidates"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

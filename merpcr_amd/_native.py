@@ -29,7 +29,7 @@ EXPORTS = (
     "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
     "mp_genome_stats", "mp_genome_destroy",
     "mp_search_create", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
-    "mp_search_last_stats", "mp_search_survivors", "mp_search_destroy",
+    "mp_search_last_stats", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
 )
 
 
@@ -80,6 +80,7 @@ def _sig(lib):
     lib.mp_search_device_hits.argtypes = [P, POINTER(c_void_p)]
     lib.mp_search_last_stats.argtypes = [P, POINTER(c_float), u64p, u64p]
     lib.mp_search_survivors.argtypes = [P, u64p]
+    lib.mp_search_timing.argtypes = [P, POINTER(c_float), POINTER(c_float), POINTER(c_float)]
     lib.mp_search_destroy.argtypes = [P]
     lib.mp_search_destroy.restype = None
 
@@ -224,7 +225,10 @@ class Search:
         check(lib().mp_search_last_stats(self._h, ctypes.byref(ms), ctypes.byref(nw), ctypes.byref(nc)))
         sv = c_uint64()
         check(lib().mp_search_survivors(self._h, ctypes.byref(sv)))
-        return {"scan_ms": ms.value, "windows": nw.value, "candidates": nc.value, "survivors": sv.value}
+        t1, t2, t3 = c_float(), c_float(), c_float()
+        check(lib().mp_search_timing(self._h, ctypes.byref(t1), ctypes.byref(t2), ctypes.byref(t3)))
+        return {"scan_ms": ms.value, "windows": nw.value, "candidates": nc.value, "survivors": sv.value,
+                "pair_ms": t2.value, "order_ms": t3.value}
 
     def close(self):
         if self._h:

@@ -161,14 +161,16 @@ struct Search {
     mp_hit* out = nullptr;
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
-    unsigned long long* counters = nullptr;  // [0] hits, [1] candidates
+    unsigned long long* counters = nullptr;  // [0] hits, [1] candidates, [2] survivors
+    uint4* surv = nullptr;                   // fingerprint survivors {gk lo, gk hi, rec|exact, seq}
+    uint64_t surv_cap = 0;
     SeqSpan* spans = nullptr;
     uint64_t spans_cap = 0;
     int n_cu = 0;
     uint64_t n_hits = 0;
     uint64_t n_windows = 0, n_candidates = 0, n_survivors = 0;
-    float scan_ms = 0.f;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float scan_ms = 0.f, pair_ms = 0.f, order_ms = 0.f;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
 };
 
 // ---------------------------------------------------------------- device helpers

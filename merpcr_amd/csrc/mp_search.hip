@@ -32,6 +32,7 @@
 //   1: no drain (seed stage only)   2: no global filter probe (hash-based stand-in)
 //   3: neither                      4: drain stops after the bucket lookup
 //   5: fingerprint only (survivors are counted, not pair-checked)
+//   6: pair kernel stops after loading the record   7: pair kernel skips the primer-2 compares
 #ifndef MP_ABLATE
 #define MP_ABLATE 0
 #endif
@@ -69,7 +70,15 @@ struct ScanArgs {
     uint64_t* hit_lo;
     unsigned long long* counters;
     uint64_t cap;
+    uint4* surv;
+    uint64_t surv_cap;
 };
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Character of exception base j: the run index entry with the largest start <= j,
 // searched between the directory bounds of j's 4096-base block.
@@ -163,12 +172,31 @@ __device__ __forceinline__ bool fp_reject(const ScanArgs& a, uint64_t G, uint32_
     return __popcll(d) > a.N;
 }
 
-__device__ __forceinline__ void emit(const ScanArgs& a, uint64_t gk, uint32_t rank, uint32_t tr) {
-    const unsigned long long idx = atomicAdd(&a.counters[0], 1ull);
-    if (idx < a.cap) {
-        a.hit_hi[idx] = gk;
-        a.hit_lo[idx] = ((uint64_t)rank << 32) | tr;
+// Per-wave hit staging (pair kernel): hits collect in LDS and leave in batches of up
+// to 127 with one atomic reservation -- a returning atomic on one global counter
+// sustains only ~88 per microsecond (MI355X_MICROARCH.md, dequeue), far below the hit rate.
+struct HitStage {
+    uint64_t hi[128];
+    uint64_t lo[128];
+    uint32_t n;
+};
+
+__device__ __forceinline__ void stage_flush(const ScanArgs& a, HitStage& S, int lane) {
+    const uint32_t cnt = S.n;
+    if (!cnt) return;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&a.counters[0], (unsigned long long)cnt);
+    base = (unsigned long long)__shfl((long long)base, 0, 64);
+    for (uint32_t i = (uint32_t)lane; i < cnt; i += 64) {
+        const unsigned long long idx = base + i;
+        if (idx < a.cap) {
+            a.hit_hi[idx] = S.hi[i];
+            a.hit_lo[idx] = S.lo[i];
+        }
     }
+    wave_sync_lds();
+    if (lane == 0) S.n = 0;
+    wave_sync_lds();
 }
 
 // _match_sts (engine.py:507-597) for one fingerprint survivor (record `rec`, amplicon
@@ -177,9 +205,12 @@ __device__ __forceinline__ void emit(const ScanArgs& a, uint64_t gk, uint32_t ra
 // amplicon-end offsets d in [-lo, hi] (the reference's try order is restored by the
 // device sort through try_rank(d)).
 __device__ void pair_check_wave(const ScanArgs& a, uint64_t sbase, uint32_t n, uint32_t k, uint32_t rec,
-                                bool p1_exact, int lane) {
+                                bool p1_exact, int lane, HitStage& S) {
     const DevRec r = a.recs[rec];
     const uint64_t gk = sbase + k;
+#if MP_ABLATE == 6
+    if (r.l1 != 0xFFFFFFFFu) return;
+#endif
     if (!p1_exact && !primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true)) return;
     const uint32_t avail = n - k - r.l1;
     if (avail < r.l2) return;
@@ -194,11 +225,32 @@ __device__ void pair_check_wave(const ScanArgs& a, uint64_t sbase, uint32_t n, u
     }
     const int lo = (int)max<int64_t>(0, min<int64_t>(a.M, (int64_t)e - r.l1 - r.l2));
     const uint32_t rk = a.rank[rec];
-    for (int d = -lo + lane; d <= hi; d += 64) {
-        const int64_t p2 = (int64_t)k + e - r.l2 + d;
-        if (d <= 0 && (int64_t)k + r.l1 > p2) continue;
-        if (p2 + r.l2 > (int64_t)n) continue;
-        if (primer_ok(a, sbase + (uint64_t)p2, r.l2, r.p2_pl, r.p2_ch, false)) emit(a, gk, rk, try_rank(d));
+    const int ntry = lo + hi + 1;
+    for (int b = 0; b < ntry; b += 64) {  // wave-uniform trip count
+        const int d = -lo + b + lane;
+        bool hit = false;
+        if (b + lane < ntry) {
+            const int64_t p2 = (int64_t)k + e - r.l2 + d;
+            const bool inb = !(d <= 0 && (int64_t)k + r.l1 > p2) && p2 + r.l2 <= (int64_t)n;
+#if MP_ABLATE == 7
+            hit = inb && p2 == -12345;
+#else
+            hit = inb && primer_ok(a, sbase + (uint64_t)p2, r.l2, r.p2_pl, r.p2_ch, false);
+#endif
+        }
+        const uint64_t m = __ballot(hit);
+        if (m) {
+            const uint32_t at = S.n;
+            if (hit) {
+                const uint32_t i = at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                S.hi[i] = gk;
+                S.lo[i] = ((uint64_t)rk << 32) | try_rank(d);
+            }
+            wave_sync_lds();
+            if (lane == 0) S.n = at + (uint32_t)__popcll(m);
+            wave_sync_lds();
+            if (S.n >= 64) stage_flush(a, S, lane);
+        }
     }
 }
 
@@ -211,17 +263,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+__device__ __forceinline__ void wave_sync() { wave_sync_lds(); }
 
 struct WaveLds {           // per-wave LDS scratch of the drain
     uint32_t h_mask[64];   // seed hits of the super-step, per lane (bit 31-i = window i)
     uint32_t h_pre[64];    // exclusive prefix of the per-lane hit counts
-    uint32_t sv_k[64];     // survivors of one pass (at most one per lane)
-    uint32_t sv_r[64];
     uint32_t x_pos[64];    // bucket tails of one pass
     uint32_t x_start[64];
     uint32_t x_pre[64];
@@ -232,6 +278,7 @@ struct WaveLds {           // per-wave LDS scratch of the drain
 struct SuperRegs {
     uint64_t w0, w1, iv;
     uint32_t base;
+    uint32_t seq;
 };
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
@@ -281,27 +328,47 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
     return true;
 }
 
-// Compact this pass's survivors (one per lane at most) and pair-check each with the
-// whole wave.
-__device__ __forceinline__ void flush_survivors(const ScanArgs& a, uint64_t sbase, uint32_t n, bool surv,
-                                                uint32_t k, uint32_t rec, bool exact, int lane, WaveLds& L) {
+// Survivor output of a wave: slots are reserved from the global list 64 at a time (one
+// atomic per chunk); unused tail slots of a wave's last chunk are marked empty.
+struct SurvChunk {
+    uint64_t base;   // first slot of the current chunk
+    uint32_t used;   // slots of it already written (64 = none left)
+    uint32_t total;  // survivors of this wave (statistics)
+};
+
+__device__ __forceinline__ void flush_survivors(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, bool surv,
+                                                uint32_t k, uint32_t rec, bool exact, int lane, SurvChunk& C) {
     const uint64_t m = __ballot(surv);
     if (!m) return;
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    C.total += cnt;
+    const uint32_t avail = 64u - C.used;
+    uint64_t nbase = C.base;
+    if (cnt > avail) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(&a.counters[2], 64ull);
+        nbase = shfl64((uint64_t)b, 0);
+    }
     if (surv) {
-        const uint32_t i = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        L.sv_k[i] = k;
-        L.sv_r[i] = rec | (exact ? 0x80000000u : 0u);  // record ids are < 2^31
+        const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        const uint64_t idx = r < avail ? C.base + C.used + r : nbase + (r - avail);
+        if (idx < a.surv_cap) {
+            const uint64_t gk = sbase + k;
+            a.surv[idx] = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec | (exact ? 0x80000000u : 0u), R.seq);
+        }
     }
-    if (lane == 0) atomicAdd(&a.counters[2], (unsigned long long)__popcll(m));
-    wave_sync();
-#if MP_ABLATE != 5
-    const uint32_t ns = (uint32_t)__popcll(m);
-    for (uint32_t i = 0; i < ns; ++i) {
-        const uint32_t rv = L.sv_r[i];
-        pair_check_wave(a, sbase, n, L.sv_k[i], rv & 0x7FFFFFFFu, (rv >> 31) != 0, lane);
+    if (cnt > avail) {
+        C.base = nbase;
+        C.used = cnt - avail;
+    } else {
+        C.used += cnt;
     }
-#endif
-    wave_sync();
+}
+
+__device__ __forceinline__ void close_survivors(const ScanArgs& a, int lane, const SurvChunk& C) {
+    const uint32_t i = C.used + (uint32_t)lane;
+    if (C.used < 64u && i < 64u && C.base + i < a.surv_cap)
+        a.surv[C.base + i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // empty slot
 }
 
 // Bucket head of seed key h (W <= 13: rank of h in the exact bitmap; above: slot).
@@ -347,11 +414,12 @@ __device__ __forceinline__ uint32_t seed_offset(const WaveLds& L, uint32_t e) {
 template <int kMode>
 __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRegs& R, uint64_t sbase,
                                                 uint32_t n, bool have, uint32_t pos, const Entry& e0, uint64_t Gp,
-                                                uint32_t exp_, int lane, uint32_t& ncand, WaveLds& L) {
+                                                uint32_t exp_, int lane, uint32_t& ncand, WaveLds& L,
+                                                SurvChunk& C) {
     uint32_t sk = 0;
     bool ex0 = false;
     const bool surv = candidate(a, R, sbase, n, have, pos, e0, ncand, sk, Gp, exp_, true, ex0);
-    flush_survivors(a, sbase, n, surv, sk, e0.rec, ex0, lane, L);
+    flush_survivors(a, R, sbase, surv, sk, e0.rec, ex0, lane, C);
     const uint32_t xc = have ? e0.count - 1u : 0u;
     const uint32_t incl = wave_incl_scan(xc, lane);
     const uint32_t total = __shfl(incl, 63, 64);
@@ -376,7 +444,7 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
             if (act) ej = a.ents[L.x_start[lo] + (c - L.x_pre[lo])];
             bool ex2 = false;
             const bool s2 = candidate(a, R, sbase, n, act, L.x_pos[lo], ej, ncand, sk, 0, 0, false, ex2);
-            flush_survivors(a, sbase, n, s2, sk, ej.rec, ex2, lane, L);
+            flush_survivors(a, R, sbase, s2, sk, ej.rec, ex2, lane, C);
         }
         wave_sync();
     }
@@ -386,7 +454,8 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
 // lookup chains (rank word -> bucket head) are in flight together.
 template <int kMode>
 __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
-                                            uint32_t qn, int lane, uint32_t& ncand, WaveLds& L) {
+                                            uint32_t qn, int lane, uint32_t& ncand, WaveLds& L,
+                                            SurvChunk& C) {
     const uint32_t shw = 64u - 2u * (uint32_t)a.W;
     for (uint32_t b = 0; b < qn; b += 128) {
         const uint32_t ea = b + (uint32_t)lane, eb = ea + 64;
@@ -415,8 +484,8 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
         ncand += (hva && e0a.rec == 0xFFFFFFFFu) + (hvb && e0b.rec == 0xFFFFFFFFu);
         continue;
 #endif
-        heads_and_tails<kMode>(a, R, sbase, n, hva, pa, e0a, Ga, xa, lane, ncand, L);
-        if (b + 64 < qn) heads_and_tails<kMode>(a, R, sbase, n, hvb, pb, e0b, Gb, xb, lane, ncand, L);
+        heads_and_tails<kMode>(a, R, sbase, n, hva, pa, e0a, Ga, xa, lane, ncand, L, C);
+        if (b + 64 < qn) heads_and_tails<kMode>(a, R, sbase, n, hvb, pb, e0b, Gb, xb, lane, ncand, L, C);
     }
 }
 
@@ -540,6 +609,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     const uint32_t shw = 32u - 2u * W;
     WaveLds& L = s_wl[w];
     uint32_t ncand = 0;
+    SurvChunk C{0, 64u, 0u};
 
     uint64_t ss = (uint64_t)blockIdx.x * kWaves + (uint64_t)w;
     // span of the super-step being prefetched, cached in registers (wave-uniform): the
@@ -584,6 +654,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         R.w1 = nw1;
         R.iv = niv;
         R.base = sp.p_al + (uint32_t)(ss - sp.super0) * kSuper;
+        R.seq = sp.seq;
         const uint32_t pb = R.base + (uint32_t)lane * kLanePos;
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
         const uint32_t okm = window_ok_mask(R.iv, W) &
@@ -607,17 +678,41 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             L.h_mask[lane] = hits;
             L.h_pre[lane] = incl - c;
             wave_sync();
-            drain_seeds<kMode>(a, R, sbase, n, total, lane, ncand, L);
+            drain_seeds<kMode>(a, R, sbase, n, total, lane, ncand, L, C);
             wave_sync();
         }
 #endif
         ss = nx;
     }
+    close_survivors(a, lane, C);
     // candidate statistics, one atomic per wave
     uint32_t tot = ncand;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
     if (lane == 0 && tot) atomicAdd(&a.counters[1], (unsigned long long)tot);
+    if (lane == 0 && C.total) atomicAdd(&a.counters[3], (unsigned long long)C.total);
+}
+
+// One wave per fingerprint survivor: exact primer-1 compare unless the fingerprint was
+// already exact, then the amplicon pair-check with lanes over the offsets.
+// Persistent: each wave strides over the survivor list (empty slots skipped) and stages
+// its hits in LDS.
+__global__ __launch_bounds__(256) void pair_kernel(ScanArgs a, uint64_t n_surv) {
+    __shared__ HitStage s_st[4];
+    const int lane = threadIdx.x & 63;
+    HitStage& S = s_st[threadIdx.x >> 6];
+    if (lane == 0) S.n = 0;
+    wave_sync_lds();
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n_surv; i += stride) {
+        const uint4 v = a.surv[i];
+        if (v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu) continue;  // wave-uniform
+        const uint64_t gk = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        const uint64_t sbase = a.seq_base[v.w];
+        const uint32_t n = (uint32_t)a.seq_len[v.w];
+        pair_check_wave(a, sbase, n, (uint32_t)(gk - sbase), v.z & 0x7FFFFFFFu, (v.z >> 31) != 0, lane, S);
+    }
+    stage_flush(a, S, lane);
 }
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
@@ -652,8 +747,11 @@ static void free_search(Search* s) {
     if (!s) return;
     hipFree(s->keys); hipFree(s->tmp_hi); hipFree(s->tmp_lo); hipFree(s->out); hipFree(s->sort_tmp);
     hipFree(s->counters); hipFree(s->spans);
+    hipFree(s->surv);
     if (s->ev0) hipEventDestroy(s->ev0);
     if (s->ev1) hipEventDestroy(s->ev1);
+    if (s->ev2) hipEventDestroy(s->ev2);
+    if (s->ev3) hipEventDestroy(s->ev3);
     delete s;
 }
 
@@ -667,6 +765,15 @@ static int alloc_hits(Search* s, uint64_t cap) {
     MP_HIP_CHECK(hipMalloc(&s->tmp_lo, cap * 8));
     MP_HIP_CHECK(hipMalloc(&s->out, cap * sizeof(mp_hit)));
     s->cap = cap;
+    return MP_OK;
+}
+
+static int alloc_surv(Search* s, uint64_t cap) {
+    hipFree(s->surv);
+    s->surv = nullptr;
+    s->surv_cap = 0;
+    MP_HIP_CHECK(hipMalloc(&s->surv, cap * sizeof(uint4)));
+    s->surv_cap = cap;
     return MP_OK;
 }
 
@@ -690,11 +797,13 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
         if (hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess ||
             s->n_cu <= 0)
             s->n_cu = 256;
-        if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) {
+        if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
+            hipEventCreate(&s->ev2) != hipSuccess || hipEventCreate(&s->ev3) != hipSuccess) {
             rc = fail(MP_E_HIP, "event creation failed");
             break;
         }
         rc = alloc_hits(s, 1 << 16);
+        if (!rc) rc = alloc_surv(s, 1 << 20);
     } while (0);
     if (rc) {
         free_search(s);
@@ -783,15 +892,18 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.g_lo = g_lo; a.g_hi = g_hi;
 
     unsigned long long cnt[4] = {0, 0, 0, 0};
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
+                                                       (uint64_t)s->n_cu * kBlocksPerCU);
+    // scan: seeds -> fingerprint survivors (grow the survivor list and rerun on overflow)
     for (int attempt = 0; attempt < 2; ++attempt) {
         a.hit_hi = s->keys;
         a.hit_lo = s->keys + s->cap;
         a.counters = s->counters;
         a.cap = s->cap;
+        a.surv = s->surv;
+        a.surv_cap = s->surv_cap;
         MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 32, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
-                                                           (uint64_t)s->n_cu * kBlocksPerCU);
         if (t->lds_exact) hipLaunchKernelGGL(scan_kernel<0>, dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct) hipLaunchKernelGGL(scan_kernel<1>, dim3(grid), dim3(kBlock), 0, st, a);
         else hipLaunchKernelGGL(scan_kernel<2>, dim3(grid), dim3(kBlock), 0, st, a);
@@ -799,14 +911,35 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         MP_HIP_CHECK(hipEventRecord(s->ev1, st));
         MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 32, hipMemcpyDeviceToHost, st));
         MP_HIP_CHECK(hipStreamSynchronize(st));
+        if (cnt[2] <= s->surv_cap) break;
+        int rc = alloc_surv(s, cnt[2] + cnt[2] / 4 + 1024);
+        if (rc) return rc;
+    }
+    if (cnt[2] > s->surv_cap) return fail(MP_E_STATE, "mp_search_run: survivor list overflow after growth");
+    MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->ev1));
+    s->n_candidates = cnt[1];
+    s->n_survivors = cnt[3];
+    // pair-check: survivors -> hits (grow the hit buffer and rerun this stage on overflow)
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        a.hit_hi = s->keys;
+        a.hit_lo = s->keys + s->cap;
+        a.cap = s->cap;
+        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 8, st));
+        MP_HIP_CHECK(hipEventRecord(s->ev1, st));
+        if (cnt[2]) {
+            const uint32_t pgrid = (uint32_t)std::min<uint64_t>((cnt[2] + 3) / 4, (uint64_t)s->n_cu * 8);
+            hipLaunchKernelGGL(pair_kernel, dim3(pgrid), dim3(256), 0, st, a, (uint64_t)cnt[2]);
+            MP_HIP_CHECK(hipGetLastError());
+        }
+        MP_HIP_CHECK(hipEventRecord(s->ev2, st));
+        MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 8, hipMemcpyDeviceToHost, st));
+        MP_HIP_CHECK(hipStreamSynchronize(st));
         if (cnt[0] <= s->cap) break;
         int rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
         if (rc) return rc;
     }
     if (cnt[0] > s->cap) return fail(MP_E_STATE, "mp_search_run: hit buffer overflow after growth");
-    MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->ev1));
-    s->n_candidates = cnt[1];
-    s->n_survivors = cnt[2];
+    MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     const uint64_t nh = cnt[0];
     int rc = sort_hits(s, nh, st);
     if (rc) return rc;
@@ -816,7 +949,9 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
                            g->d_base, g->d_len, g->n_seq, t->inv_rank, t->recs, s->out);
         MP_HIP_CHECK(hipGetLastError());
     }
+    MP_HIP_CHECK(hipEventRecord(s->ev3, st));
     MP_HIP_CHECK(hipStreamSynchronize(st));
+    MP_HIP_CHECK(hipEventElapsedTime(&s->order_ms, s->ev2, s->ev3));
     s->n_hits = nh;
     if (n_hits) *n_hits = nh;
     return MP_OK;
@@ -865,6 +1000,15 @@ MP_EXPORT int mp_search_survivors(void* search, uint64_t* n_survivors) {
     Search* s = (Search*)search;
     if (!s || !n_survivors) return fail(MP_E_ARG, "mp_search_survivors: null pointer");
     *n_survivors = s->n_survivors;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_search_timing(void* search, float* scan_ms, float* pair_ms, float* order_ms) {
+    Search* s = (Search*)search;
+    if (!s) return fail(MP_E_ARG, "mp_search_timing: null search");
+    if (scan_ms) *scan_ms = s->scan_ms;
+    if (pair_ms) *pair_ms = s->pair_ms;
+    if (order_ms) *order_ms = s->order_ms;
     return MP_OK;
 }
 
