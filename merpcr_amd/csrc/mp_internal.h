@@ -117,6 +117,7 @@ struct Table {
     uint32_t* filt = nullptr;     // W >= 14: hashed presence filter
     uint2* rk = nullptr;          // W <= 13: rank bitmap
     Entry* dents = nullptr;       // W <= 13: bucket heads by key rank
+    uint4* dents16 = nullptr;     // W <= 13: compact heads {code lo, code hi, rec, off|l1<<8|flags<<16}
     Slot* slots = nullptr;        // W >= 14
     Entry* ents = nullptr;
     DevRec* recs = nullptr;
@@ -225,6 +226,11 @@ __host__ __device__ __forceinline__ uint32_t table_slot(uint32_t key, uint32_t l
 __host__ __device__ __forceinline__ uint32_t filter_index(uint32_t key, uint32_t log2bits) {
     return (uint32_t)(((uint64_t)key * 0xD6E8FEB86659FD93ull) >> (64 - log2bits));
 }
+
+// Compact bucket head (16 B): usable when the primer-1 fingerprint is "all plain" over
+// l1 <= 32 bases (pmask derivable from l1) and the bucket has no tail; otherwise the
+// flag sends the lookup to the full 32-B Entry.
+constexpr uint32_t kHeadFull = 1u;   // flags: read dents[rank] instead
 
 // LDS prefilter index of a seed key (exact for W <= 9, multiplicative hash above);
 // with kLdsHashes == 2 a second index is set too (two-probe Bloom filter).

@@ -55,6 +55,7 @@ struct ScanArgs {
     uint32_t filt_log2;
     const uint2* rk;        // W <= 13: rank bitmap
     const Entry* dents;     // W <= 13: bucket heads by rank
+    const uint4* dents16;   // W <= 13: compact heads
     const uint32_t* lfilt;
     const Slot* slots;
     uint32_t slot_log2;
@@ -371,6 +372,19 @@ __device__ __forceinline__ void close_survivors(const ScanArgs& a, int lane, con
         a.surv[C.base + i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // empty slot
 }
 
+// Entry of a compact head: all-plain fingerprint over l1 bases, single-record bucket.
+__device__ __forceinline__ Entry compact_head(const uint4 c) {
+    Entry e;
+    e.code = (uint64_t)c.x | ((uint64_t)c.y << 32);
+    e.rec = c.z;
+    e.hash_off = (uint16_t)(c.w & 0xFFu);
+    e.l1 = (uint16_t)((c.w >> 8) & 0xFFu);
+    e.pmask = sp_lt((int)e.l1);
+    e.xstart = 0;
+    e.count = 1;
+    return e;
+}
+
 // Bucket head of seed key h (W <= 13: rank of h in the exact bitmap; above: slot).
 template <int kMode>
 __device__ __forceinline__ bool bucket_head(const ScanArgs& a, uint32_t h, Entry& e0) {
@@ -474,8 +488,18 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
             const uint2 rb = lb ? a.rk[hb >> 5] : make_uint2(0, 0);
             hva = (ra.x >> (ha & 31u)) & 1u;
             hvb = (rb.x >> (hb & 31u)) & 1u;
-            if (hva) e0a = a.dents[ra.y + (uint32_t)__popc(ra.x & ((1u << (ha & 31u)) - 1u))];
-            if (hvb) e0b = a.dents[rb.y + (uint32_t)__popc(rb.x & ((1u << (hb & 31u)) - 1u))];
+            const uint32_t qa = ra.y + (uint32_t)__popc(ra.x & ((1u << (ha & 31u)) - 1u));
+            const uint32_t qb = rb.y + (uint32_t)__popc(rb.x & ((1u << (hb & 31u)) - 1u));
+            const uint4 ca = hva ? a.dents16[qa] : make_uint4(0, 0, 0, 0);
+            const uint4 cb = hvb ? a.dents16[qb] : make_uint4(0, 0, 0, 0);
+            if (hva) {
+                if (ca.w >> 16) e0a = a.dents[qa];  // full entry: IUPAC/long primer or bucket tail
+                else e0a = compact_head(ca);
+            }
+            if (hvb) {
+                if (cb.w >> 16) e0b = a.dents[qb];
+                else e0b = compact_head(cb);
+            }
         } else {
             hva = la && bucket_head<kMode>(a, ha, e0a);
             hvb = lb && bucket_head<kMode>(a, hb, e0b);
@@ -883,7 +907,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.has_u = g->has_u ? 1 : 0;
     a.seq_base = g->d_base; a.seq_len = g->d_len;
     a.spans = s->spans; a.n_spans = n_real_spans;
-    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.lfilt = t->lfilt;
+    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents16 = t->dents16; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
     a.planes = t->planes; a.pchars = t->pchars;
