@@ -31,6 +31,8 @@ extern "C" {
 #define MP_E_NOMEM (-3)   /* device or host allocation failed */
 #define MP_E_STATE (-4)   /* handle used out of order (e.g. search before seal) */
 #define MP_E_CAP (-5)     /* caller's output buffer too small; *n_hits has the need */
+#define MP_E_IO (-6)      /* file cannot be opened or read (OSError) */
+#define MP_E_DECODE (-7)  /* input is not valid UTF-8 (UnicodeDecodeError) */
 
 /* Search parameters: the MerPCR constructor arguments that reach the hot path
  * (engine.py:47-97).  Bounds are the reference's (W 3..16, N 0..10, M 0..10000,
@@ -127,6 +129,21 @@ int mp_search_survivors(void* search, uint64_t* n_survivors);
  * survivor pair-check kernel, ordering (sort + decode). */
 int mp_search_timing(void* search, float* scan_ms, float* pair_ms, float* order_ms);
 void mp_search_destroy(void* search);
+
+/* ---- FASTA input (replaces FASTALoader.load_file, src/merpcr/io/fasta.py:18-71) --
+ * Reads `path` as the reference's text-mode loop does: strict UTF-8, universal
+ * newlines, Python str.strip() whitespace, '>' headers (defline = stripped line),
+ * sequence lines filtered to the characters whose upper case is in
+ * "ACGTBDHKMNRSVWXY" (32 ASCII letters + U+017F as its two UTF-8 bytes), lines
+ * before the first header dropped.  The caller handles the reference's empty-file
+ * case (fasta.py:31-33) before calling.  Records stay owned by the handle. */
+int mp_fasta_load(const char* path, void** fasta_out);
+/* Number of records and total filtered sequence bytes. */
+int mp_fasta_info(void* fasta, uint64_t* n_records, uint64_t* total_bytes);
+/* Borrowed pointers to record i's defline (UTF-8, with '>') and filtered sequence. */
+int mp_fasta_record(void* fasta, uint64_t i, const uint8_t** defline, uint64_t* defline_len,
+                    const uint8_t** seq, uint64_t* seq_len);
+void mp_fasta_destroy(void* fasta);
 
 #ifdef __cplusplus
 }

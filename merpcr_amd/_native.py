@@ -21,6 +21,8 @@ MP_E_HIP = -2
 MP_E_NOMEM = -3
 MP_E_STATE = -4
 MP_E_CAP = -5
+MP_E_IO = -6
+MP_E_DECODE = -7
 
 # every symbol include/merpcr_hip.h declares
 EXPORTS = (
@@ -30,6 +32,7 @@ EXPORTS = (
     "mp_genome_stats", "mp_genome_destroy",
     "mp_search_create", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
     "mp_search_last_stats", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
+    "mp_fasta_load", "mp_fasta_info", "mp_fasta_record", "mp_fasta_destroy",
 )
 
 
@@ -83,6 +86,11 @@ def _sig(lib):
     lib.mp_search_timing.argtypes = [P, POINTER(c_float), POINTER(c_float), POINTER(c_float)]
     lib.mp_search_destroy.argtypes = [P]
     lib.mp_search_destroy.restype = None
+    lib.mp_fasta_load.argtypes = [c_char_p, POINTER(c_void_p)]
+    lib.mp_fasta_info.argtypes = [P, u64p, u64p]
+    lib.mp_fasta_record.argtypes = [P, c_uint64, POINTER(c_void_p), u64p, POINTER(c_void_p), u64p]
+    lib.mp_fasta_destroy.argtypes = [P]
+    lib.mp_fasta_destroy.restype = None
 
 
 def lib():
@@ -106,6 +114,8 @@ def check(rc: int):
         msg = lib().mp_last_error().decode(errors="replace")
         if rc == MP_E_ARG:
             raise ValueError(msg)
+        if rc == MP_E_IO:
+            raise OSError(msg)
         raise NativeError(rc, msg)
 
 
@@ -240,3 +250,30 @@ class Search:
             self.close()
         except Exception:
             pass
+
+
+def fasta_read(path: str):
+    """Read a FASTA file natively (mp_fasta_load); returns [(defline, sequence bytes)].
+
+    Raises UnicodeDecodeError for invalid UTF-8, as the reference's text-mode read does.
+    """
+    h = c_void_p()
+    rc = lib().mp_fasta_load(os.fsencode(path), ctypes.byref(h))
+    if rc == MP_E_DECODE:
+        msg = lib().mp_last_error().decode(errors="replace")
+        pos = int(msg.rsplit(" ", 1)[-1])
+        raise UnicodeDecodeError("utf-8", b"", pos, pos + 1, msg)
+    check(rc)
+    try:
+        n, total = c_uint64(), c_uint64()
+        check(lib().mp_fasta_info(h, ctypes.byref(n), ctypes.byref(total)))
+        out = []
+        dp, dl, sp, sl = c_void_p(), c_uint64(), c_void_p(), c_uint64()
+        for i in range(n.value):
+            check(lib().mp_fasta_record(h, i, ctypes.byref(dp), ctypes.byref(dl), ctypes.byref(sp), ctypes.byref(sl)))
+            d = ctypes.string_at(dp, dl.value).decode("utf-8")
+            seq = ctypes.string_at(sp, sl.value) if sl.value else b""
+            out.append((d, seq))
+        return out
+    finally:
+        lib().mp_fasta_destroy(h)

@@ -5,8 +5,16 @@ reference keeps a character c iff ``c.upper() in "ACGTBDHKMNRSVWXY"``.  Over all
 of Unicode that is the 32 ASCII letters below plus U+017F (long s, upper 'S');
 U is dropped.  Lines are stripped, blank lines skipped, '>' starts a record,
 sequence lines before the first header are discarded (fasta.py:42-66).
+
+``FASTALoader.load_file`` reads through the native reader of libmerpcr_hip.so
+(``mp_fasta_load``, merpcr_amd/csrc/mp_fasta.hip), which restates that loop in C++
+for UTF-8 text (the locale encoding of the reference's ``open(filename, "r")``).
+``load_file_py`` is the same loop in Python; it serves non-UTF-8 locales and the
+parity tests.
 """
 
+import codecs
+import locale
 import logging
 import os
 import re
@@ -21,6 +29,11 @@ KEEP_CHARS = "ABCDGHKMNRSTVWXYabcdghkmnrstvwxyſ"
 _DROP = re.compile("[^" + re.escape(KEEP_CHARS) + "]+")
 
 
+def _utf8_locale() -> bool:
+    """True when open(filename, "r") decodes UTF-8, as the native reader does."""
+    return codecs.lookup(locale.getpreferredencoding(False)).name == "utf-8"
+
+
 def filter_line(line: str) -> str:
     """Keep only the characters the reference's FASTA filter keeps."""
     if line.isascii() and not _DROP.search(line):
@@ -33,6 +46,22 @@ class FASTALoader:
 
     @staticmethod
     def load_file(filename: str) -> List[FASTARecord]:
+        if not _utf8_locale():
+            return FASTALoader.load_file_py(filename)
+        from .. import _native
+        start = time.time()
+        if os.path.getsize(filename) == 0:
+            logger.error(f"FASTA file '{filename}' is empty")
+            return []
+        logger.info(f"Reading FASTA file: {filename}")
+        records = []
+        for defline, seq in _native.fasta_read(filename):
+            records.append(FASTARecord(defline=defline, sequence=seq.decode("utf-8")))
+        logger.info(f"Loaded {len(records)} sequences in {time.time() - start:.2f} seconds")
+        return records
+
+    @staticmethod
+    def load_file_py(filename: str) -> List[FASTARecord]:
         start = time.time()
         if os.path.getsize(filename) == 0:
             logger.error(f"FASTA file '{filename}' is empty")

@@ -1,0 +1,110 @@
+"""Native FASTA reader (mp_fasta_load) vs the reference's text-mode loop.
+
+The expected side is FASTALoader.load_file_py, the Python restatement of
+src/merpcr/io/fasta.py:18-71 (itself pinned to the reference's recorded loader
+outputs by tests/test_host.py::test_fasta_loader_matches_reference).  Inputs are
+byte strings that stress what the C++ reader re-implements: universal newlines
+(also split across read chunks), Python's Unicode whitespace in strip(), the
+U+017F keep character, BOMs, blank and header-less lines, invalid UTF-8.
+"""
+
+import os
+import random
+
+import pytest
+
+from merpcr_amd import _native
+from merpcr_amd.io.fasta import FASTALoader
+
+pytestmark = pytest.mark.skipif(not os.path.exists(_native.LIB_PATH), reason="library not built")
+
+WS = [" ", "\t", "\x0b", "\x0c", "\x1c", "\x1f", "\x85", "\xa0", " ", " ", " ",
+      " ", " ", " ", "　", "﻿", "​"]
+NL = ["\n", "\r\n", "\r"]
+LETTERS = "ACGTNacgtnUuRYKMSWBDHVXZzjſ12-*.É中"
+
+
+def _expected(path):
+    try:
+        return [(r.defline, r.sequence, r.label) for r in FASTALoader.load_file_py(path)]
+    except Exception as e:  # noqa: BLE001 - compare exception types
+        return type(e)
+
+
+def _native_read(path):
+    try:
+        return [(r.defline, r.sequence, r.label) for r in FASTALoader.load_file(path)]
+    except Exception as e:  # noqa: BLE001
+        return type(e)
+
+
+def _random_text(rng):
+    out = []
+    for _ in range(rng.randint(0, 12)):
+        kind = rng.random()
+        pre = "".join(rng.choice(WS) for _ in range(rng.randint(0, 2))) if rng.random() < 0.3 else ""
+        post = "".join(rng.choice(WS) for _ in range(rng.randint(0, 2))) if rng.random() < 0.3 else ""
+        if kind < 0.25:
+            body = ">" + "".join(rng.choice("abc XYZ_|.\t" + "　ſé") for _ in range(rng.randint(1, 12)))
+            body = body if body.strip() != ">" else ">x"
+        elif kind < 0.35:
+            body = ""
+        else:
+            body = "".join(rng.choice(LETTERS + " ") for _ in range(rng.randint(0, 40)))
+        out.append(pre + body + post + rng.choice(NL))
+    if out and rng.random() < 0.5:
+        out[-1] = out[-1].rstrip("\r\n")  # no final newline
+    return "".join(out)
+
+
+@pytest.mark.parametrize("chunk", [None, "4", "7", "64"])
+def test_native_matches_python_loop(tmp_path, monkeypatch, chunk):
+    if chunk:
+        monkeypatch.setenv("MP_FASTA_CHUNK", chunk)
+    rng = random.Random(1234 + (int(chunk) if chunk else 0))
+    p = str(tmp_path / "x.fa")
+    for i in range(300):
+        text = _random_text(rng)
+        if not text:
+            continue
+        with open(p, "wb") as fh:
+            fh.write(text.encode("utf-8"))
+        exp = _expected(p)
+        got = _native_read(p)
+        if isinstance(exp, type) and exp is IndexError:  # '>' alone: FASTARecord label
+            assert got is IndexError
+            continue
+        assert got == exp, (i, text)
+
+
+@pytest.mark.parametrize("blob", [
+    b">a\nAC\xffGT\n", b">a\nACGT\xc5", b">a\nAC\xed\xa0\x80GT\n", b">a\xc0\xaf\nAC\n",
+    b">a\nAC\xf4\x90\x80\x80\n", b">a\nAC\xe0\x80\x80\n",
+])
+def test_invalid_utf8_raises_like_reference(tmp_path, blob):
+    p = str(tmp_path / "bad.fa")
+    with open(p, "wb") as fh:
+        fh.write(blob)
+    with pytest.raises(UnicodeDecodeError):
+        FASTALoader.load_file_py(p)
+    with pytest.raises(UnicodeDecodeError):
+        FASTALoader.load_file(p)
+
+
+def test_crlf_split_across_chunks(tmp_path, monkeypatch):
+    p = str(tmp_path / "crlf.fa")
+    text = ">s1 d\r\nACGT\r\n\r\nGG\r>s2\r\nTT\r\n"
+    with open(p, "wb") as fh:
+        fh.write(text.encode())
+    exp = _expected(p)
+    for c in range(4, len(text) + 2):
+        monkeypatch.setenv("MP_FASTA_CHUNK", str(c))
+        assert _native_read(p) == exp, c
+
+
+def test_missing_and_empty(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        FASTALoader.load_file(str(tmp_path / "nope.fa"))
+    p = tmp_path / "empty.fa"
+    p.write_bytes(b"")
+    assert FASTALoader.load_file(str(p)) == []
