@@ -145,6 +145,18 @@ int mp_fasta_record(void* fasta, uint64_t i, const uint8_t** defline, uint64_t* 
                     const uint8_t** seq, uint64_t* seq_len);
 void mp_fasta_destroy(void* fasta);
 
+/* ---- output (replaces the per-hit print of MerPCR.search, engine.py:436-444) --
+ * Writes one line per hit, in the order given:
+ *     "{label}\t{pos1+1}..{pos2+1}\t{rec_text}\n"
+ * labels: UTF-8 FASTARecord.label of each sequence, CSR offsets label_off[n_seq+1];
+ * rec_text: UTF-8 "{id}\t{alias}\t({direct})" of each record in sts_records order,
+ * CSR offsets rec_off[n_rec+1].  *n_bytes receives the output size; out == NULL is a
+ * size query, cap < size fails with MP_E_CAP. */
+int mp_format_hits(const mp_hit* hits, uint64_t n_hits,
+                   const uint8_t* labels, const uint64_t* label_off, uint32_t n_seq,
+                   const uint8_t* rec_text, const uint64_t* rec_off, uint32_t n_rec,
+                   uint8_t* out, uint64_t cap, uint64_t* n_bytes);
+
 #ifdef __cplusplus
 }
 #endif

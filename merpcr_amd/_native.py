@@ -33,6 +33,7 @@ EXPORTS = (
     "mp_search_create", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
     "mp_search_last_stats", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
     "mp_fasta_load", "mp_fasta_info", "mp_fasta_record", "mp_fasta_destroy",
+    "mp_format_hits",
 )
 
 
@@ -91,6 +92,7 @@ def _sig(lib):
     lib.mp_fasta_record.argtypes = [P, c_uint64, POINTER(c_void_p), u64p, POINTER(c_void_p), u64p]
     lib.mp_fasta_destroy.argtypes = [P]
     lib.mp_fasta_destroy.restype = None
+    lib.mp_format_hits.argtypes = [P, c_uint64, P, P, c_uint32, P, P, c_uint32, P, c_uint64, u64p]
 
 
 def lib():
@@ -277,3 +279,31 @@ def fasta_read(path: str):
         return out
     finally:
         lib().mp_fasta_destroy(h)
+
+
+def _csr(items):
+    """UTF-8 bytes of each string, concatenated, with offsets."""
+    enc = [x.encode("utf-8") for x in items]
+    off = np.zeros(len(enc) + 1, dtype=np.uint64)
+    if enc:
+        np.cumsum([len(b) for b in enc], out=off[1:])
+    return np.frombuffer(b"".join(enc), dtype=np.uint8), off
+
+
+class Formatter:
+    """Output-line formatter over fixed label and record texts (mp_format_hits)."""
+
+    def __init__(self, labels, rec_texts):
+        self.labels, self.label_off = _csr(labels)
+        self.rec, self.rec_off = _csr(rec_texts)
+        self.n_seq, self.n_rec = len(labels), len(rec_texts)
+
+    def __call__(self, hits: np.ndarray) -> bytes:
+        hits = np.ascontiguousarray(hits, dtype=HIT_DTYPE)
+        n = c_uint64()
+        args = (ptr(hits), hits.size, ptr(self.labels), ptr(self.label_off), self.n_seq,
+                ptr(self.rec), ptr(self.rec_off), self.n_rec)
+        check(lib().mp_format_hits(*args, None, 0, ctypes.byref(n)))
+        out = np.empty(n.value, dtype=np.uint8)
+        check(lib().mp_format_hits(*args, ptr(out), out.size, ctypes.byref(n)))
+        return out.tobytes()

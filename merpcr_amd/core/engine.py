@@ -328,20 +328,17 @@ class MerPCR:
             t -= 1
             logger.info(f"Reduced threads to {t} due to sequence size limitations")
 
+    def format_bytes(self, fasta_records: Sequence[FASTARecord], hits: np.ndarray) -> bytes:
+        """The output text of engine.py:437-443 for `hits`, UTF-8, by mp_format_hits."""
+        from .. import _native
+        fmt = _native.Formatter([r.label for r in fasta_records],
+                                [f"{r.id}\t{r.alias}\t({r.direct})" for r in self.sts_records])
+        return fmt(hits)
+
     def format_hits(self, fasta_records: Sequence[FASTARecord], hits: np.ndarray) -> List[str]:
         """Output lines exactly as engine.py:437-443 prints them."""
-        recs = self.sts_records
-        tails = {}
-        labels = [r.label for r in fasta_records]
-        out = []
-        for p1, p2, sq, ri in zip(hits["pos1"].tolist(), hits["pos2"].tolist(),
-                                  hits["seq"].tolist(), hits["rec"].tolist()):
-            tail = tails.get(ri)
-            if tail is None:
-                r = recs[ri]
-                tail = tails[ri] = f"\t{r.id}\t{r.alias}\t({r.direct})"
-            out.append(f"{labels[sq]}\t{p1 + 1}..{p2 + 1}{tail}")
-        return out
+        text = self.format_bytes(fasta_records, hits).decode("utf-8")
+        return text.split("\n")[:-1] if text else []
 
     def hits_as_objects(self, hits: np.ndarray) -> List[STSHit]:
         recs = self.sts_records
@@ -358,10 +355,9 @@ class MerPCR:
             total = 0
             if fasta_records:
                 hits = self.find_hits(fasta_records)
-                lines = self.format_hits(fasta_records, hits)
-                total = len(lines)
-                if lines:
-                    output.write("\n".join(lines) + "\n")
+                total = len(hits)
+                if total:
+                    output.write(self.format_bytes(fasta_records, hits).decode("utf-8"))
         finally:
             if to_file:
                 output.close()
