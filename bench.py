@@ -97,6 +97,40 @@ def cpu_baseline(eng, names, lens, buf, offs, cfg, hits_dev, budget_s: float, th
     }
 
 
+def end_to_end(eng, table, names, lens, buf, offs, device, stream):
+    """One untimed-by-the-metric pass from host bytes to output text (SURVEY 8d t_e2e):
+    H2D + 2-bit pack + exception index (mp_genome_put/seal), search, hit fetch and the
+    native formatter.  Filtered FASTA bytes start in host memory, as after FASTA load."""
+    import torch
+    from merpcr_amd import _native
+    from merpcr_amd.core.models import FASTARecord
+
+    host = buf.cpu().numpy()
+    recs = [FASTARecord(defline=">" + nm, sequence="", label=nm) for nm in names]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g = _native.Genome(device, lens)
+    for r, n in enumerate(lens):
+        g.put(r, host[int(offs[r]):int(offs[r]) + n], stream=stream)
+    g.seal(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    s = _native.Search(table, g)
+    n = s.run(None, stream)
+    hits = s.fetch(n)
+    t2 = time.perf_counter()
+    text = eng.format_bytes(recs, hits)
+    t3 = time.perf_counter()
+    s.close()
+    g.close()
+    bases = float(sum(lens))
+    return {"seconds": round(t3 - t0, 3), "gbp_per_s": round(bases / (t3 - t0) / 1e9, 3),
+            "upload_pack_s": round(t1 - t0, 3), "search_fetch_s": round(t2 - t1, 3),
+            "format_s": round(t3 - t2, 3), "output_bytes": len(text),
+            "note": "filtered sequence bytes in pageable host memory -> output text; PCIe-inclusive, "
+                    "not the metric"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,6 +141,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cores))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-bytes-to-output-text pass")
     args = ap.parse_args()
 
     import torch
@@ -235,6 +270,8 @@ def main():
                                        "gfx950-corrected; includes Infinity-Cache hits)" if traffic else None,
                      "kernel": "mp::scan_kernel", "alg_bytes_per_launch": int(alg_bytes)},
     }
+    if world == 1 and not args.no_e2e:
+        out["e2e"] = end_to_end(eng, table, names, lens, buf, offs, local, stream)
     if world == 1 and not args.no_cpu_baseline:
         hits = search.fetch(nhits)
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
