@@ -145,6 +145,26 @@ int mp_fasta_record(void* fasta, uint64_t i, const uint8_t** defline, uint64_t* 
                     const uint8_t** seq, uint64_t* seq_len);
 void mp_fasta_destroy(void* fasta);
 
+/* ---- STS file (replaces MerPCR.load_sts_file and helpers, engine.py:193-359) --
+ * Parses `path` into the oriented records of the reference's sts_records, in order,
+ * with the same skip/adjust rules.  The caller handles the empty-file case
+ * (engine.py:196-200).  Status after a successful parse: */
+#define MP_STS_OK 0        /* whole file parsed */
+#define MP_STS_BAD_LINE 1  /* stopped at a line with < 4 fields (load returns False);
+                              the records before it are kept, as in the reference */
+#define MP_STS_PYTHON 2    /* a primer/size field needs Python's Unicode upper()/int()
+                              rules (non-ASCII) or a size >= 2^62: parse on the host side */
+int mp_sts_parse(const char* path, int32_t wordsize, int64_t default_pcr_size, void** sts_out);
+/* counts[10]: n_records, bad_line, n_short, n_ambig, n_badsize, max_pcr_size,
+ * primer1 bytes, primer2 bytes, text bytes, n_text (= 2 x kept lines). */
+int mp_sts_info(void* sts, int32_t* status, uint64_t* counts);
+/* ptrs[12] (borrowed, valid until destroy): key u32[n], hash_off u32[n], pcr_size u64[n],
+ * line_no u64[n], direct u8[n] ('+'/'-'), text_idx u32[n] (line index: id = text item
+ * 2i, alias = 2i+1), primer1 u8[], p1_off u64[n+1], primer2 u8[], p2_off u64[n+1],
+ * text u8[] (UTF-8), text_off u64[n_text+1]. */
+int mp_sts_arrays(void* sts, const void** ptrs);
+void mp_sts_destroy(void* sts);
+
 /* ---- output (replaces the per-hit print of MerPCR.search, engine.py:436-444) --
  * Writes one line per hit, in the order given:
  *     "{label}\t{pos1+1}..{pos2+1}\t{rec_text}\n"

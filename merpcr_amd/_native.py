@@ -23,6 +23,7 @@ MP_E_STATE = -4
 MP_E_CAP = -5
 MP_E_IO = -6
 MP_E_DECODE = -7
+MP_STS_OK, MP_STS_BAD_LINE, MP_STS_PYTHON = 0, 1, 2
 
 # every symbol include/merpcr_hip.h declares
 EXPORTS = (
@@ -34,6 +35,7 @@ EXPORTS = (
     "mp_search_last_stats", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
     "mp_fasta_load", "mp_fasta_info", "mp_fasta_record", "mp_fasta_destroy",
     "mp_format_hits",
+    "mp_sts_parse", "mp_sts_info", "mp_sts_arrays", "mp_sts_destroy",
 )
 
 
@@ -92,6 +94,11 @@ def _sig(lib):
     lib.mp_fasta_record.argtypes = [P, c_uint64, POINTER(c_void_p), u64p, POINTER(c_void_p), u64p]
     lib.mp_fasta_destroy.argtypes = [P]
     lib.mp_fasta_destroy.restype = None
+    lib.mp_sts_parse.argtypes = [c_char_p, c_int32, ctypes.c_int64, POINTER(c_void_p)]
+    lib.mp_sts_info.argtypes = [P, POINTER(c_int32), u64p]
+    lib.mp_sts_arrays.argtypes = [P, POINTER(c_void_p)]
+    lib.mp_sts_destroy.argtypes = [P]
+    lib.mp_sts_destroy.restype = None
     lib.mp_format_hits.argtypes = [P, c_uint64, P, P, c_uint32, P, P, c_uint32, P, c_uint64, u64p]
 
 
@@ -254,6 +261,45 @@ class Search:
             pass
 
 
+def _decode_error(rc):
+    if rc == MP_E_DECODE:
+        msg = lib().mp_last_error().decode(errors="replace")
+        pos = int(msg.rsplit(" ", 1)[-1])
+        raise UnicodeDecodeError("utf-8", b"", pos, pos + 1, msg)
+
+
+def sts_parse(path: str, wordsize: int, default_pcr_size: int):
+    """Parse an STS file natively (mp_sts_parse).  Returns a dict of numpy arrays and
+    counters (copies; the native handle is released)."""
+    h = c_void_p()
+    rc = lib().mp_sts_parse(os.fsencode(path), wordsize, default_pcr_size, ctypes.byref(h))
+    _decode_error(rc)
+    check(rc)
+    try:
+        st = c_int32()
+        cnt = (c_uint64 * 10)()
+        check(lib().mp_sts_info(h, ctypes.byref(st), cnt))
+        n, nt = cnt[0], cnt[9]
+        ptrs = (c_void_p * 12)()
+        check(lib().mp_sts_arrays(h, ptrs))
+
+        def arr(i, dtype, count):
+            if not count:
+                return np.zeros(0, dtype=dtype)
+            return np.ctypeslib.as_array(ctypes.cast(ptrs[i], POINTER(np.ctypeslib.as_ctypes_type(dtype))),
+                                         shape=(count,)).copy()
+
+        return {"status": st.value, "n": n, "bad_line": cnt[1], "short": cnt[2], "ambig": cnt[3],
+                "badsize": cnt[4], "max_pcr_size": cnt[5],
+                "key": arr(0, np.uint32, n), "hash_off": arr(1, np.uint32, n), "pcr_size": arr(2, np.uint64, n),
+                "line": arr(3, np.uint64, n), "direct": arr(4, np.uint8, n), "text_idx": arr(5, np.uint32, n),
+                "p1": arr(6, np.uint8, cnt[6]), "p1_off": arr(7, np.uint64, n + 1),
+                "p2": arr(8, np.uint8, cnt[7]), "p2_off": arr(9, np.uint64, n + 1),
+                "text": arr(10, np.uint8, cnt[8]), "text_off": arr(11, np.uint64, nt + 1)}
+    finally:
+        lib().mp_sts_destroy(h)
+
+
 def fasta_read(path: str):
     """Read a FASTA file natively (mp_fasta_load); returns [(defline, sequence bytes)].
 
@@ -261,10 +307,7 @@ def fasta_read(path: str):
     """
     h = c_void_p()
     rc = lib().mp_fasta_load(os.fsencode(path), ctypes.byref(h))
-    if rc == MP_E_DECODE:
-        msg = lib().mp_last_error().decode(errors="replace")
-        pos = int(msg.rsplit(" ", 1)[-1])
-        raise UnicodeDecodeError("utf-8", b"", pos, pos + 1, msg)
+    _decode_error(rc)
     check(rc)
     try:
         n, total = c_uint64(), c_uint64()

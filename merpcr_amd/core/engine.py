@@ -22,7 +22,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from ..io.fasta import FASTALoader
+from ..io.fasta import FASTALoader, _utf8_locale
 from .encode import CharCodes
 from .models import FASTARecord, STSHit, STSRecord, ThreadData
 
@@ -66,7 +66,7 @@ class MerPCR:
                  three_prime_match: int = DEFAULT_THREE_PRIME_MATCH,
                  iupac_mode: int = DEFAULT_IUPAC_MODE, default_pcr_size: int = DEFAULT_PCR_SIZE,
                  threads: int = DEFAULT_THREADS, max_sts_line_length: int = 1022,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, emulate_chunks: bool = False):
         self.wordsize = wordsize
         self.margin = margin
         self.mismatches = mismatches
@@ -76,6 +76,9 @@ class MerPCR:
         self.threads = threads
         self.max_sts_line_length = max_sts_line_length
         self.device = 0 if device is None else int(device)
+        # threads > 1: reproduce the reference's per-chunk output (duplicated overlap
+        # hits, chunk-local record ends) instead of the exact T=1 result
+        self.emulate_chunks = bool(emulate_chunks)
 
         self.sts_records: List[STSRecord] = []
         self.sts_table: Dict[int, List[STSRecord]] = {}
@@ -130,6 +133,56 @@ class MerPCR:
         self._sts_keys = []
         self.max_pcr_size = 0
         self._dev_table = None
+        self._native_arrays = None
+        if _utf8_locale():
+            done = self._load_sts_native(filename, start)
+            if done is not None:
+                return done
+        return self._load_sts_py(filename, start)
+
+    def _load_sts_native(self, filename: str, start: float) -> Optional[bool]:
+        """load_sts_file through mp_sts_parse (merpcr_amd/csrc/mp_sts.hip); None when the
+        file needs Python's Unicode rules (non-ASCII primer/size fields)."""
+        from .. import _native
+        r = _native.sts_parse(filename, self.wordsize, self.default_pcr_size)
+        if r["status"] == _native.MP_STS_PYTHON:
+            return None
+        n = r["n"]
+        p1s = r["p1"].tobytes().decode("ascii")
+        p2s = r["p2"].tobytes().decode("ascii")
+        p1o, p2o = r["p1_off"].tolist(), r["p2_off"].tolist()
+        text, to = r["text"].tobytes(), r["text_off"].tolist()
+        if text.isascii():
+            ts = text.decode("ascii")
+            items = [ts[to[i]:to[i + 1]] for i in range(len(to) - 1)]
+        else:
+            items = [text[to[i]:to[i + 1]].decode("utf-8") for i in range(len(to) - 1)]
+        keys = r["key"].tolist()
+        table = self.sts_table
+        recs = self.sts_records
+        for i, (ti, size, line, hoff, d, key) in enumerate(zip(
+                r["text_idx"].tolist(), r["pcr_size"].tolist(), r["line"].tolist(), r["hash_off"].tolist(),
+                r["direct"].tolist(), keys)):
+            rec = STSRecord(items[2 * ti], p1s[p1o[i]:p1o[i + 1]], p2s[p2o[i]:p2o[i + 1]], size,
+                            items[2 * ti + 1], line, hoff, "+" if d == 43 else "-")
+            recs.append(rec)
+            b = table.get(key)
+            if b is None:
+                table[key] = [rec]
+            else:
+                b.append(rec)
+        self._sts_keys = keys
+        self.max_pcr_size = r["max_pcr_size"]
+        self._native_arrays = (recs, n, (r["key"], r["hash_off"], r["pcr_size"], r["p1"], r["p1_off"],
+                                         r["p2"], r["p2_off"]))
+        if r["status"] == _native.MP_STS_BAD_LINE:
+            logger.error(f"Bad STS file format at line {r['bad_line']}. Expected at least 4 fields.")
+            return False
+        self._log_sts_summary(r["short"], r["ambig"], r["badsize"], start)
+        return True
+
+    def _load_sts_py(self, filename: str, start: float) -> bool:
+        """load_sts_file restated in Python (engine.py:212-302)."""
         short = ambig = badsize = 0
         W = self.wordsize
         with open(filename, "r") as fh:
@@ -170,6 +223,12 @@ class MerPCR:
                                            direct="-"), key2)
             else:
                 ambig += 1
+        self._log_sts_summary(short, ambig, badsize, start)
+        return True
+
+    def _log_sts_summary(self, short: int, ambig: int, badsize: int, start: float):
+        """Warnings and summary of engine.py:289-302."""
+        W = self.wordsize
         if short:
             logger.warning(f"{short} STSs have primer shorter than word size ({W}): not included in search")
         if ambig:
@@ -267,6 +326,9 @@ class MerPCR:
     def _table_arrays(self):
         """Record arrays for mp_table_create in sts_records order."""
         recs = self.sts_records
+        na = getattr(self, "_native_arrays", None)
+        if na is not None and na[0] is recs and na[1] == len(recs):
+            return na[2]
         if len(self._sts_keys) != len(recs):
             self._sts_keys = [self._hash_value(r.primer1)[1] for r in recs]
         key = np.asarray(self._sts_keys, dtype=np.uint32)
@@ -295,13 +357,55 @@ class MerPCR:
     def encode_sequences(self, sequences: Sequence[str]) -> List[np.ndarray]:
         return [self._codes.sequence_bytes(s) for s in sequences]
 
+    def chunk_plan(self, seq_len: int) -> List[Tuple[int, int]]:
+        """(offset, length) of each chunk the reference's search scans for a record of
+        seq_len bases (engine.py:380-410): T = threads for records of >= 100 kbp, reduced
+        while (T+1)*overlap > n; each chunk overlaps the next by max_pcr_size + M - 1."""
+        t = self.threads if seq_len >= MIN_FILESIZE_FOR_THREADING else 1
+        overlap = self.max_pcr_size + self.margin - 1
+        while t > 1 and (t + 1) * overlap > seq_len:
+            t -= 1
+        size = int((seq_len - (t + 1) * overlap) / t) + 2 * overlap
+        plan, off = [], 0
+        for i in range(t):
+            ln = size if i < t - 1 else seq_len - off
+            plan.append((off, ln))
+            off += ln - overlap
+        return plan
+
     def find_hits(self, fasta_records: Sequence[FASTARecord]) -> np.ndarray:
         """All hits of all records on the GPU, in output order.
 
-        Returns the structured array of mp_hit (pos1, pos2, seq, rec)."""
+        Returns the structured array of mp_hit (pos1, pos2, seq, rec).  With
+        emulate_chunks and threads > 1, every chunk of the reference's plan is searched
+        as its own sequence, hits are shifted to record coordinates, and each record's
+        chunk lists are concatenated in chunk order and stably sorted on pos1
+        (engine.py:412-434) -- overlap hits then appear once per chunk, as in the
+        reference's multi-process output."""
+        data = self.encode_sequences([r.sequence for r in fasta_records])
+        if not (self.emulate_chunks and self.threads > 1):
+            return self._search_device(data)
+        pieces, owner, base = [], [], []
+        for i, d in enumerate(data):
+            for off, ln in self.chunk_plan(len(d)):
+                pieces.append(d[off:off + ln])
+                owner.append(i)
+                base.append(off)
+        hits = self._search_device(pieces)
+        if len(hits):
+            piece = hits["seq"].astype(np.int64)
+            shift = np.asarray(base, dtype=np.uint64)[piece]
+            hits["pos1"] += shift
+            hits["pos2"] += shift
+            hits["seq"] = np.asarray(owner, dtype=np.uint32)[piece]
+            # LSD: stable on pos1, then stable on the record -> chunk order kept on ties
+            hits = hits[np.argsort(hits["pos1"], kind="stable")]
+            hits = hits[np.argsort(hits["seq"], kind="stable")]
+        return hits
+
+    def _search_device(self, data: Sequence[np.ndarray]) -> np.ndarray:
         from .. import _native
         table = self.device_table()
-        data = self.encode_sequences([r.sequence for r in fasta_records])
         genome = _native.Genome(self.device, [len(d) for d in data])
         for i, d in enumerate(data):
             if len(d):

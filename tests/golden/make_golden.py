@@ -3,6 +3,7 @@
 Run only in the build container, where the reference is importable:
 
     PYTHONPATH=/root/reference/src python3 tests/golden/make_golden.py
+    PYTHONPATH=/root/reference/src python3 tests/golden/make_golden.py --chunked   # -T N corpus
 
 The reference never ships with this repository and never runs on the GPU box;
 what is committed is data only: the seeded inputs each case was built from and
@@ -287,7 +288,89 @@ def unit_kats(rng):
     return kat
 
 
+def _plan(n, threads, max_pcr, margin):
+    """Chunk plan of the reference's -T N search (same rule as oracle.chunk_plan); used
+    only to place amplicons on chunk seams."""
+    t = threads if n >= 100000 else 1
+    ov = max_pcr + margin - 1
+    while t > 1 and (t + 1) * ov > n:
+        t -= 1
+    size = int((n - (t + 1) * ov) / t) + 2 * ov
+    out, off = [], 0
+    for i in range(t):
+        ln = size if i < t - 1 else n - off
+        out.append((off, ln))
+        off += ln - ov
+    return out
+
+
+def chunked_cases():
+    """-T N corpus: the reference's chunked search (duplicated overlap hits, chunk-local
+    record ends) on genomes built so that hits fall on chunk seams."""
+    g = random.Random(777)
+    out = []
+
+    def acgt(n):
+        return "".join(g.choice("ACGT") for _ in range(n))
+
+    def plant(seq, pos, amp):
+        return seq[:pos] + amp + seq[pos + len(amp):]
+
+    # 1. planted amplicons on the seams of every T's plan, two orientations
+    p1, p2 = "GATTACAGGCTTACCGTA", "CCTAGGATCGATTGCAAT"
+    prm = dict(wordsize=11, margin=50, mismatches=1, three_prime_match=1, iupac_mode=0,
+               default_pcr_size=240)
+    st = f"SEAM\t{p1}\t{p2}\t180\tseam marker\nSEAM2\t{p2}\t{p1}\t200-240\n"
+    big = acgt(400000)
+    ampf = p1 + acgt(180 - len(p1) - len(p2)) + p2
+    ampr = p2 + acgt(190 - len(p1) - len(p2)) + _rc(p1)
+    for T in (2, 3, 4, 8):
+        for off, ln in _plan(len(big), T, 220, 50)[1:]:    # max_pcr_size = (200+240)//2
+            big = plant(big, off + 10, ampf)            # inside the overlap: found twice
+            big = plant(big, off + 269 - 60, ampr)      # straddles the previous chunk's end
+    small = plant(acgt(60000), 30000, ampf)
+    cases = [("seam", prm, st, [(">big seam test", big), (">small", small)], (1, 2, 3, 4, 8))]
+
+    # 2. dense chance hits (W=4, 4-mer primers): many amplicons truncated by chunk ends
+    prm2 = dict(wordsize=4, margin=20, mismatches=1, three_prime_match=1, iupac_mode=0,
+                default_pcr_size=60)
+    st2 = "".join(f"D{i}\t{acgt(g.randint(4, 6))}\t{acgt(g.randint(4, 6))}\t{g.randint(20, 90)}\n"
+                  for i in range(4))
+    cases.append(("dense", prm2, st2, [(">dense1", acgt(210000)), (">dense2", acgt(100000))], (1, 3, 5)))
+
+    # 3. T reduced by a long product (ov ~ 20k), records at the 100 kbp threshold
+    prm3 = dict(wordsize=8, margin=49, mismatches=0, three_prime_match=2, iupac_mode=1,
+                default_pcr_size=240)
+    q1, q2 = "ACGTTGCAAGGCTA", "TTGACGGCATCAGA"
+    st3 = f"LONG\t{q1}\t{q2}\t20000\nSHORT\t{q2}\t{q1}\t150\nIUP\tACGTRYNNACGTAC\tGGCATTYCAGGA\t120\n"
+    recs3 = []
+    for n in (99999, 100000, 100001, 130000, 250000):
+        sq = acgt(n)
+        for pos in range(500, n - 300, 21011):
+            sq = plant(sq, pos, q2 + acgt(150 - 2 * len(q1)) + q1)         # SHORT '+'
+        for pos in range(1700, n - 20100, 17003):
+            sq = plant(sq, pos, q1)                                         # LONG '+'
+            sq = plant(sq, pos + 20000 - len(q2) + g.randint(-49, 49), q2)
+        recs3.append((f">r{n} len={n}", sq))
+    cases.append(("reduce", prm3, st3, recs3, (1, 4, 8)))
+
+    for name, prm_, st_, recs, ts in cases:
+        outs = {}
+        for T in ts:
+            r = run_ref(prm_, st_, records=recs, threads=T)
+            outs[str(T)] = {"n_hits": r["n_hits"], "output": r["output"]}
+            print("chunked", name, T, r["n_hits"], file=sys.stderr)
+        out.append({"name": name, "params": prm_, "sts_text": st_, "records": [list(x) for x in recs],
+                    "max_pcr_size": r["max_pcr_size"], "by_threads": outs})
+    return out
+
+
 def main():
+    if "--chunked" in sys.argv:
+        logging.disable(logging.CRITICAL)
+        with gzip.open(os.path.join(HERE, "chunked.json.gz"), "wt") as fh:
+            json.dump({"cases": chunked_cases()}, fh, separators=(",", ":"))
+        return
     logging.disable(logging.CRITICAL)
     rng = random.Random(20261015)
     sts_path = os.path.join(DATA, "test.sts")

@@ -178,3 +178,36 @@ def test_sharded_ranges_concatenate_to_whole():
     cat = np.concatenate(parts)
     assert len(whole) > 0
     assert np.array_equal(cat, whole)
+
+
+def test_chunk_emulation_matches_reference_threads():
+    """-T N corpus: with emulate_chunks the GPU output equals the reference's
+    multi-process output line for line (duplicates included); without it, every T
+    gives the exact T=1 output."""
+    for case in load_golden("chunked.json.gz")["cases"]:
+        recs = [FASTARecord(defline=d, sequence=s) for d, s in case["records"]]
+        t1 = case["by_threads"]["1"]["output"].splitlines()
+        with tempfile.TemporaryDirectory() as td:
+            for t, exp in case["by_threads"].items():
+                eng = MerPCR(threads=int(t), emulate_chunks=True, **case["params"])
+                assert _load_sts(eng, case["sts_text"], td)
+                assert eng.max_pcr_size == case["max_pcr_size"]
+                assert _device_lines(eng, recs) == exp["output"].splitlines(), (case["name"], t)
+                eng.emulate_chunks = False
+                assert _device_lines(eng, recs) == t1, (case["name"], t)
+
+
+def test_cli_threads_emulation(tmp_path):
+    """The CLI with -T 4 --emulate-chunks writes the reference's -T 4 output file."""
+    from merpcr_amd.cli import main
+    case = next(c for c in load_golden("chunked.json.gz")["cases"] if c["name"] == "seam")
+    sts = tmp_path / "x.sts"
+    sts.write_text(case["sts_text"])
+    fa = tmp_path / "x.fa"
+    fa.write_text("".join(f"{d}\n{s}\n" for d, s in case["records"]))
+    out = tmp_path / "out.txt"
+    p = case["params"]
+    rc = main([str(sts), str(fa), "-W", str(p["wordsize"]), "-M", str(p["margin"]), "-N", str(p["mismatches"]),
+               "-T", "4", "--emulate-chunks", "-O", str(out)])
+    assert rc == 0
+    assert out.read_text() == case["by_threads"]["4"]["output"]

@@ -106,3 +106,18 @@ def test_cli_fails_cleanly_on_bad_sts(capsys):
         with open(p, "w") as fh:
             fh.write("ONLY\tTHREE\tFIELDS\n")
         assert main([p, data_path("test.fa")]) == 1
+
+
+def test_chunk_plan_matches_oracle():
+    """MerPCR.chunk_plan restates engine.py:380-410 like oracle.chunk_plan does."""
+    import random as _r
+    from oracle import epcr_oracle as O
+    g = _r.Random(5)
+    for _ in range(2000):
+        n = g.choice([0, 1, 99999, 100000, 100001, g.randint(0, 10**7), g.randint(10**5, 10**6)])
+        t = g.randint(1, 64)
+        eng = MerPCR(threads=t, margin=g.randint(0, 10000))
+        eng.max_pcr_size = g.randint(6, 20000)
+        plan = eng.chunk_plan(n)
+        assert plan == O.chunk_plan(n, t, eng.max_pcr_size, eng.margin)
+        assert plan[0][0] == 0 and plan[-1][0] + plan[-1][1] == n

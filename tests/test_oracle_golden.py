@@ -108,3 +108,15 @@ def test_threaded_chunk_semantics():
     for case in load_golden("threaded.json.gz")["cases"]:
         table, lines = _run(case, threads=case["threads"])
         assert lines == _expected_lines(case), case["threads"]
+
+
+def test_chunked_corpus():
+    """-T N corpus (tests/golden/chunked.json.gz): the reference's multi-process chunking,
+    duplicated overlap hits and chunk-local record ends (engine.py:380-434)."""
+    for case in load_golden("chunked.json.gz")["cases"]:
+        params, sts_lines, recs = case_inputs(case)
+        table = O.load_sts_lines(sts_lines, params["wordsize"], params["default_pcr_size"])
+        assert table.max_pcr_size == case["max_pcr_size"]
+        for t, exp in case["by_threads"].items():
+            lines = O.search_lines(recs, table, O.params(**params), threads=int(t))
+            assert lines == exp["output"].splitlines(), (case["name"], t)

@@ -1,0 +1,120 @@
+"""Native STS parser (mp_sts_parse) vs the Python restatement of load_sts_file.
+
+The expected side is MerPCR._load_sts_py, which restates engine.py:193-302 and is
+itself pinned to the reference's recorded load results (max_pcr_size, record counts,
+outputs) by the golden corpora.  Inputs stress the rules the C++ parser re-implements:
+strip() whitespace, '#' comments, CR/CRLF line ends, tab splitting, _parse_pcr_size's
+int() cases (signs, '_' separators, ranges, junk), short and hash-less primers, a
+line with fewer than four fields, and non-ASCII text (verbatim in ids/aliases, Python
+rules for primers and sizes).
+"""
+
+import logging
+import os
+import random
+import time
+
+import pytest
+
+from merpcr_amd import MerPCR, _native
+
+pytestmark = pytest.mark.skipif(not os.path.exists(_native.LIB_PATH), reason="library not built")
+
+SIZES = ["200", "100-300", " 250 ", "+180", "-5", "0", "0-0", "1_000", "1__0", "_5", "5_", "abc", "",
+         "120-", "-", "1-2-3", " 90 - 110 ", "+5-+7", "007", "12a", "3.5", "\x0b42\x0c",
+         "1e3", "10-x", "2-4", "600"]
+PY_ONLY_SIZES = ["99999999999999999999", "٣٠٠"]   # Python int() rules: deferred
+WS = ["", " ", "\t", "\x0b", "\x1c", "　", "\xa0"]
+
+
+def _primer(rng, W):
+    L = rng.choice([W - 1, W, W + 3, 20, 25])
+    alpha = rng.choice(["ACGT", "ACGTacgt", "ACGTN", "ACGTRYKMSWNU", "NNNNNA", "acgtuU"])
+    return "".join(rng.choice(alpha) for _ in range(max(L, 0)))
+
+
+def _sts_text(rng, W):
+    lines = []
+    for i in range(rng.randint(0, 30)):
+        k = rng.random()
+        if k < 0.05:
+            lines.append("# comment\t" + str(i))
+        elif k < 0.1:
+            lines.append(rng.choice(WS))
+        else:
+            f = [rng.choice([f"STS{i}", f"id é{i}", f"s {i}"]), _primer(rng, W), _primer(rng, W),
+                 rng.choice(PY_ONLY_SIZES if rng.random() < 0.01 else SIZES)]
+            if rng.random() < 0.6:
+                f.append(rng.choice(["alias", "(D17S932)  Chr.17, 63.7 cM", "ſ alias", ""]))
+            if rng.random() < 0.1:
+                f.append("extra")
+            line = "\t".join(f)
+            if rng.random() < 0.02:
+                line = "\t".join(f[:3])          # < 4 fields
+            if rng.random() < 0.02:
+                line = line.replace(f[1], f[1] + "ß", 1)   # non-ASCII primer: Python rules
+            lines.append(rng.choice(WS) + line + rng.choice(WS))
+    nl = rng.choice(["\n", "\r\n", "\r"])
+    return nl.join(lines) + (nl if rng.random() < 0.7 else "")
+
+
+def _state(eng):
+    recs = [(r.id, r.primer1, r.primer2, r.pcr_size, r.alias, r.offset, r.hash_offset, r.direct,
+             r.ambig_primer) for r in eng.sts_records]
+    table = {k: [id(r) for r in v] for k, v in eng.sts_table.items()}
+    index = {id(r): i for i, r in enumerate(eng.sts_records)}
+    table = {k: [index[x] for x in v] for k, v in table.items()}
+    return recs, table, eng.max_pcr_size, list(eng._sts_keys)
+
+
+def _load(eng, path, native, caplog):
+    caplog.clear()
+    start = time.time()
+    eng.sts_records, eng.sts_table, eng._sts_keys, eng.max_pcr_size = [], {}, [], 0
+    with caplog.at_level(logging.INFO, logger="merpcr_amd"):
+        if native:
+            ok = eng._load_sts_native(path, start)
+        else:
+            ok = eng._load_sts_py(path, start)
+    msgs = [m for m in caplog.messages if "seconds" not in m]
+    return ok, _state(eng), msgs
+
+
+def test_native_matches_python(tmp_path, caplog):
+    rng = random.Random(99)
+    p = str(tmp_path / "x.sts")
+    n_native = 0
+    for i in range(400):
+        W = rng.choice([3, 4, 8, 11, 16])
+        text = _sts_text(rng, W)
+        with open(p, "w", encoding="utf-8", newline="") as fh:
+            fh.write(text)
+        eng = MerPCR(wordsize=W, default_pcr_size=rng.choice([1, 240, 10000]))
+        exp = _load(eng, p, False, caplog)
+        got = _load(eng, p, True, caplog)
+        if got[0] is None:  # deferred to the Python rules
+            assert "ß" in text or "٣" in text or "99999999999999999999" in text, text
+            continue
+        n_native += 1
+        assert got == exp, (i, text)
+    assert n_native > 300
+
+
+def test_load_sts_file_uses_native_arrays(tmp_path):
+    p = tmp_path / "a.sts"
+    p.write_text("A\tACGTACGTACGTAAA\tTTTGGGCCCAAATTT\t200\talias\nB\tNNNNNNNNNNNN\tACGTTGCAACGTT\t150-250\n")
+    eng = MerPCR(wordsize=8)
+    assert eng.load_sts_file(str(p))
+    assert eng._native_arrays is not None
+    arrays = eng._table_arrays()
+    eng._native_arrays = None
+    py_arrays = eng._table_arrays()
+    for a, b in zip(arrays, py_arrays):
+        assert a.tolist() == b.tolist()
+
+
+def test_invalid_utf8_raises(tmp_path):
+    p = tmp_path / "bad.sts"
+    p.write_bytes(b"A\tACGTACGTACGT\tACGTACGTACGT\t200\t\xff\n")
+    with pytest.raises(UnicodeDecodeError):
+        MerPCR(wordsize=8).load_sts_file(str(p))
