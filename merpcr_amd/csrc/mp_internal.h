@@ -232,17 +232,13 @@ __host__ __device__ __forceinline__ uint32_t filter_index(uint32_t key, uint32_t
 // flag sends the lookup to the full 32-B Entry.
 constexpr uint32_t kHeadFull = 1u;   // flags: read dents[rank] instead
 
-// LDS prefilter index of a seed key (exact for W <= 9, multiplicative hash above);
-// with kLdsHashes == 2 a second index is set too (two-probe Bloom filter).
-#ifndef MP_LDS_HASHES
-#define MP_LDS_HASHES 1
-#endif
-constexpr int kLdsHashes = MP_LDS_HASHES;
-__host__ __device__ __forceinline__ uint32_t lds_index(uint32_t key, int exact) {
-    return exact ? key : (uint32_t)(key * 0x9E3779B1u) >> (32 - kLdsFilterLog2);
-}
-__host__ __device__ __forceinline__ uint32_t lds_index2(uint32_t key) {
-    return (uint32_t)((key ^ 0x5bd1e995u) * 0x85EBCA77u) >> (32 - kLdsFilterLog2);
+// LDS prefilter bit of a seed key.  Exact (bit = key) when 4^W fits (W <= 10);
+// above, the top 20 bits of the key left-aligned in 32 bits: keys that differ only in
+// their last 2W-20 bits share a bit.  In the scan the left-aligned form is the
+// alignbit funnel itself, so a probe costs one shift, one mask and one extract --
+// no multiply (v_mul_lo_u32 issues at quarter rate).
+__host__ __device__ __forceinline__ uint32_t lds_bit(uint32_t key, uint32_t W, bool exact) {
+    return exact ? key : (key << (32u - 2u * W)) >> (32 - kLdsFilterLog2);
 }
 
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {

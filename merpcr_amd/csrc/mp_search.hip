@@ -36,6 +36,11 @@
 #ifndef MP_ABLATE
 #define MP_ABLATE 0
 #endif
+// Genome planes are streamed once per launch: non-temporal loads keep them from
+// evicting the seed-table lines the probes re-read from L2.
+#ifndef MP_NT_STREAM
+#define MP_NT_STREAM 0
+#endif
 
 namespace mp {
 
@@ -564,14 +569,16 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
     [&]<int... T>(std::integer_sequence<int, T...>) {
         ((
             [&] {
-                const uint32_t h = kmer_top<T>(d0, d1, d2) >> shw;
-                const uint32_t li = lds_index(h, kMode == 0);
-                uint32_t bit = (lds[li >> 5] >> (li & 31)) & 1u;
-                if constexpr (kLdsHashes == 2 && kMode != 0) {
-                    const uint32_t l2 = lds_index2(h);
-                    bit &= (lds[l2 >> 5] >> (l2 & 31)) & 1u;
+                const uint32_t x = kmer_top<T>(d0, d1, d2);  // key left-aligned
+                uint32_t wi, bi;
+                if constexpr (kMode == 0) {
+                    wi = x >> (shw + 5u);
+                    bi = (x >> shw) & 31u;
+                } else {  // lds_bit: top 20 bits of the left-aligned key
+                    wi = x >> (37 - kLdsFilterLog2);
+                    bi = (x >> (32 - kLdsFilterLog2)) & 31u;
                 }
-                lmask |= bit << (31 - T);
+                lmask |= __builtin_amdgcn_ubfe(lds[wi], bi, 1u) << (31 - T);
             }()),
          ...);
     }(std::make_integer_sequence<int, 32>{});
@@ -604,7 +611,7 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
                 [&] {
                     const uint32_t h = kmer_top<T>(d0, d1, d2) >> shw;
                     const uint32_t fi = kMode == 1 ? h : filter_index(h, a.filt_log2);
-                    hits |= ((gw[T] >> (fi & 31)) & 1u) << (31 - T);
+                    hits |= __builtin_amdgcn_ubfe(gw[T], fi & 31u, 1u) << (31 - T);
                 }()),
              ...);
         }(std::make_integer_sequence<int, 32>{});
@@ -657,10 +664,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     };
     auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& iv) {
         const uint64_t j = pf_sbase + pf.p_al + (x - pf.super0) * kSuper + (uint64_t)lane * kLanePos;
+#if MP_NT_STREAM
+        w0 = __builtin_nontemporal_load(&a.g2[j >> 5]);
+        w1 = __builtin_nontemporal_load(&a.g2[(j >> 5) + 1]);
+        const uint64_t v0 = __builtin_nontemporal_load(&a.ginv[j >> 6]);
+        const uint64_t v1 = __builtin_nontemporal_load(&a.ginv[(j >> 6) + 1]);
+#else
         w0 = a.g2[j >> 5];
         w1 = a.g2[(j >> 5) + 1];
         const uint64_t v0 = a.ginv[j >> 6];
         const uint64_t v1 = a.ginv[(j >> 6) + 1];
+#endif
         const uint32_t sh = (uint32_t)(j & 32);  // branch-free: both loads always issue
         iv = (v0 << sh) | ((v1 >> (63 - sh)) >> 1);
     };

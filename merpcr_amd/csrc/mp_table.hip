@@ -149,12 +149,8 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         t->lds_exact = (2 * W <= (uint32_t)kLdsFilterLog2);
         std::vector<uint32_t> lfilt(kLdsFilterWords, 0);
         for (uint32_t b = 0; b < nb; ++b) {
-            const uint32_t idx = lds_index(bkey[b], t->lds_exact);
+            const uint32_t idx = lds_bit(bkey[b], W, t->lds_exact);
             lfilt[idx >> 5] |= 1u << (idx & 31);
-            if (kLdsHashes == 2 && !t->lds_exact) {
-                const uint32_t i2 = lds_index2(bkey[b]);
-                lfilt[i2 >> 5] |= 1u << (i2 & 31);
-            }
         }
 
         // ---- records, primer planes and bytes

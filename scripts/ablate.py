@@ -25,12 +25,21 @@ def main():
     ap.add_argument("--build-only", action="store_true")
     args = ap.parse_args()
     from merpcr_amd import _build
-    variants = [int(v) for v in args.variants.split(",")]
+    variants = args.variants.split(",")
     libs = {}
     for v in variants:
-        # 0 = product; 1-5 = MP_ABLATE=v; 12 = product with the 2-probe LDS prefilter
-        defs = () if v == 0 else (("MP_LDS_HASHES=2",) if v == 12 else (f"MP_ABLATE={v}",))
-        path = _build.LIB if v == 0 else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{v}.so")
+        # 0 = product; n = MP_ABLATE=n; nt = non-temporal genome
+        # stream; NAME=VAL[+NAME=VAL...] = those defines
+        if v == "0":
+            defs = ()
+        elif v == "nt":
+            defs = ("MP_NT_STREAM=1",)
+        elif "=" in v:
+            defs = tuple(v.split("+"))
+        else:
+            defs = (f"MP_ABLATE={int(v)}",)
+        tag = "".join(ch if ch.isalnum() else "_" for ch in v)
+        path = _build.LIB if v == "0" else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{tag}.so")
         libs[v] = _build.build_native(defines=defs, lib=path)
     if args.build_only:
         return
