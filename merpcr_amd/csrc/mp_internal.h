@@ -165,6 +165,8 @@ struct Search {
     unsigned long long* counters = nullptr;  // [0] hits, [1] candidates, [2] survivors
     uint4* surv = nullptr;                   // fingerprint survivors {gk lo, gk hi, rec|exact, seq}
     uint64_t surv_cap = 0;
+    uint4* tails = nullptr;                  // multi-record buckets {seed gpos lo, hi, xstart, seq}
+    uint64_t tails_cap = 0;
     SeqSpan* spans = nullptr;
     uint64_t spans_cap = 0;
     int n_cu = 0;

@@ -78,6 +78,8 @@ struct ScanArgs {
     uint64_t cap;
     uint4* surv;
     uint64_t surv_cap;
+    uint4* tails;           // bucket-tail references (seed position + bucket), see tail_kernel
+    uint64_t tails_cap;
 };
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -274,9 +276,6 @@ __device__ __forceinline__ void wave_sync() { wave_sync_lds(); }
 struct WaveLds {           // per-wave LDS scratch of the drain
     uint32_t h_mask[64];   // seed hits of the super-step, per lane (bit 31-i = window i)
     uint32_t h_pre[64];    // exclusive prefix of the per-lane hit counts
-    uint32_t x_pos[64];    // bucket tails of one pass
-    uint32_t x_start[64];
-    uint32_t x_pre[64];
 };
 
 // The current super-step as the wave holds it: lane L owns bases [base + 32L,
@@ -334,17 +333,18 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
     return true;
 }
 
-// Survivor output of a wave: slots are reserved from the global list 64 at a time (one
-// atomic per chunk); unused tail slots of a wave's last chunk are marked empty.
+// Chunked output lists of a wave (fingerprint survivors, bucket-tail references):
+// slots are reserved 64 at a time (one atomic per chunk); unused tail slots of a wave's
+// last chunk are marked empty.
 struct SurvChunk {
     uint64_t base;   // first slot of the current chunk
     uint32_t used;   // slots of it already written (64 = none left)
-    uint32_t total;  // survivors of this wave (statistics)
+    uint32_t total;  // entries of this wave (statistics)
 };
 
-__device__ __forceinline__ void flush_survivors(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, bool surv,
-                                                uint32_t k, uint32_t rec, bool exact, int lane, SurvChunk& C) {
-    const uint64_t m = __ballot(surv);
+__device__ __forceinline__ void append_chunked(unsigned long long* counter, uint4* buf, uint64_t cap, bool on,
+                                               const uint4& v, int lane, SurvChunk& C) {
+    const uint64_t m = __ballot(on);
     if (!m) return;
     const uint32_t cnt = (uint32_t)__popcll(m);
     C.total += cnt;
@@ -352,16 +352,13 @@ __device__ __forceinline__ void flush_survivors(const ScanArgs& a, const SuperRe
     uint64_t nbase = C.base;
     if (cnt > avail) {
         unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(&a.counters[2], 64ull);
+        if (lane == 0) b = atomicAdd(counter, 64ull);
         nbase = shfl64((uint64_t)b, 0);
     }
-    if (surv) {
+    if (on) {
         const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         const uint64_t idx = r < avail ? C.base + C.used + r : nbase + (r - avail);
-        if (idx < a.surv_cap) {
-            const uint64_t gk = sbase + k;
-            a.surv[idx] = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec | (exact ? 0x80000000u : 0u), R.seq);
-        }
+        if (idx < cap) buf[idx] = v;
     }
     if (cnt > avail) {
         C.base = nbase;
@@ -371,10 +368,17 @@ __device__ __forceinline__ void flush_survivors(const ScanArgs& a, const SuperRe
     }
 }
 
-__device__ __forceinline__ void close_survivors(const ScanArgs& a, int lane, const SurvChunk& C) {
+__device__ __forceinline__ void flush_survivors(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, bool surv,
+                                                uint32_t k, uint32_t rec, bool exact, int lane, SurvChunk& C) {
+    const uint64_t gk = sbase + k;
+    append_chunked(&a.counters[2], a.surv, a.surv_cap, surv,
+                   make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec | (exact ? 0x80000000u : 0u), R.seq), lane, C);
+}
+
+__device__ __forceinline__ void close_chunked(uint4* buf, uint64_t cap, int lane, const SurvChunk& C) {
     const uint32_t i = C.used + (uint32_t)lane;
-    if (C.used < 64u && i < 64u && C.base + i < a.surv_cap)
-        a.surv[C.base + i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // empty slot
+    if (C.used < 64u && i < 64u && C.base + i < cap)
+        buf[C.base + i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // empty slot
 }
 
 // Entry of a compact head: all-plain fingerprint over l1 bases, single-record bucket.
@@ -429,43 +433,22 @@ __device__ __forceinline__ uint32_t seed_offset(const WaveLds& L, uint32_t e) {
     return lo * kLanePos + (uint32_t)__clz(m);
 }
 
-// Candidate test of one bucket head per lane, survivors, then the bucket tails.
+// Candidate test of one bucket head per lane; a bucket with more records leaves a
+// reference (seed position, bucket) for tail_kernel, which tests the other records.
 template <int kMode>
 __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRegs& R, uint64_t sbase,
                                                 uint32_t n, bool have, uint32_t pos, const Entry& e0, uint64_t Gp,
-                                                uint32_t exp_, int lane, uint32_t& ncand, WaveLds& L,
-                                                SurvChunk& C) {
+                                                uint32_t exp_, int lane, uint32_t& ncand, SurvChunk& C,
+                                                SurvChunk& TC) {
     uint32_t sk = 0;
     bool ex0 = false;
     const bool surv = candidate(a, R, sbase, n, have, pos, e0, ncand, sk, Gp, exp_, true, ex0);
     flush_survivors(a, R, sbase, surv, sk, e0.rec, ex0, lane, C);
-    const uint32_t xc = have ? e0.count - 1u : 0u;
-    const uint32_t incl = wave_incl_scan(xc, lane);
-    const uint32_t total = __shfl(incl, 63, 64);
-    if (total) {
-        L.x_pos[lane] = pos;
-        L.x_start[lane] = e0.xstart;
-        L.x_pre[lane] = incl - xc;
-        wave_sync();
-        for (uint32_t c0 = 0; c0 < total; c0 += 64) {
-            const uint32_t c = c0 + (uint32_t)lane;
-            const bool act = c < total;
-            uint32_t lo = 0;
-            if (act) {
-                uint32_t hi = 64;  // last lane with x_pre <= c
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (L.x_pre[mid] <= c) lo = mid;
-                    else hi = mid;
-                }
-            }
-            Entry ej{};
-            if (act) ej = a.ents[L.x_start[lo] + (c - L.x_pre[lo])];
-            bool ex2 = false;
-            const bool s2 = candidate(a, R, sbase, n, act, L.x_pos[lo], ej, ncand, sk, 0, 0, false, ex2);
-            flush_survivors(a, R, sbase, s2, sk, ej.rec, ex2, lane, C);
-        }
-        wave_sync();
+    const bool tail = have && e0.count > 1u;
+    if (__any(tail)) {
+        const uint64_t gp = sbase + pos;
+        append_chunked(&a.counters[4], a.tails, a.tails_cap, tail,
+                       make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), e0.xstart, R.seq), lane, TC);
     }
 }
 
@@ -474,7 +457,7 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
 template <int kMode>
 __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
                                             uint32_t qn, int lane, uint32_t& ncand, WaveLds& L,
-                                            SurvChunk& C) {
+                                            SurvChunk& C, SurvChunk& TC) {
     const uint32_t shw = 64u - 2u * (uint32_t)a.W;
     for (uint32_t b = 0; b < qn; b += 128) {
         const uint32_t ea = b + (uint32_t)lane, eb = ea + 64;
@@ -513,8 +496,8 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
         ncand += (hva && e0a.rec == 0xFFFFFFFFu) + (hvb && e0b.rec == 0xFFFFFFFFu);
         continue;
 #endif
-        heads_and_tails<kMode>(a, R, sbase, n, hva, pa, e0a, Ga, xa, lane, ncand, L, C);
-        if (b + 64 < qn) heads_and_tails<kMode>(a, R, sbase, n, hvb, pb, e0b, Gb, xb, lane, ncand, L, C);
+        heads_and_tails<kMode>(a, R, sbase, n, hva, pa, e0a, Ga, xa, lane, ncand, C, TC);
+        if (b + 64 < qn) heads_and_tails<kMode>(a, R, sbase, n, hvb, pb, e0b, Gb, xb, lane, ncand, C, TC);
     }
 }
 
@@ -641,6 +624,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     WaveLds& L = s_wl[w];
     uint32_t ncand = 0;
     SurvChunk C{0, 64u, 0u};
+    SurvChunk TC{0, 64u, 0u};
 
     uint64_t ss = (uint64_t)blockIdx.x * kWaves + (uint64_t)w;
     // span of the super-step being prefetched, cached in registers (wave-uniform): the
@@ -716,19 +700,83 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             L.h_mask[lane] = hits;
             L.h_pre[lane] = incl - c;
             wave_sync();
-            drain_seeds<kMode>(a, R, sbase, n, total, lane, ncand, L, C);
+            drain_seeds<kMode>(a, R, sbase, n, total, lane, ncand, L, C, TC);
             wave_sync();
         }
 #endif
         ss = nx;
     }
-    close_survivors(a, lane, C);
+    close_chunked(a.surv, a.surv_cap, lane, C);
+    close_chunked(a.tails, a.tails_cap, lane, TC);
     // candidate statistics, one atomic per wave
     uint32_t tot = ncand;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
     if (lane == 0 && tot) atomicAdd(&a.counters[1], (unsigned long long)tot);
     if (lane == 0 && C.total) atomicAdd(&a.counters[3], (unsigned long long)C.total);
+}
+
+// Bucket tails: one lane per reference left by the scan (a seed whose key names more
+// than one record).  The lane walks the bucket's other records in order -- each is the
+// same (seed position, record) candidate the reference's loop over sts_table[h] tests
+// (engine.py:480-489) -- and appends fingerprint survivors to the survivor list.
+__global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t n_refs = min<uint64_t>(a.counters[4], a.tails_cap);
+    const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
+    uint32_t ncand = 0, nsurv = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); b < n_refs; b += stride) {
+        const uint64_t i = b + (uint64_t)lane;
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+        if (i < n_refs) v = a.tails[i];
+        const bool valid = !(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu);
+        uint64_t sbase = 0, gp = 0;
+        uint32_t n = 0, cnt = 0;
+        if (valid) {
+            gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            sbase = a.seq_base[v.w];
+            n = (uint32_t)a.seq_len[v.w];
+            cnt = a.ents[v.z].count;
+        }
+        const uint32_t pos = (uint32_t)(gp - sbase);
+        for (uint32_t j = 0; __any(j < cnt); ++j) {
+            bool act = j < cnt;
+            Entry e{};
+            if (act) e = a.ents[v.z + j];
+            const uint32_t k = pos - e.hash_off;
+            act = act && pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
+            act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
+            bool surv = false, exact = false;
+            if (act) {
+                ++ncand;
+                const uint64_t G = ext2(a.g2, sbase + k);
+                const uint32_t ex = (uint32_t)(ext1(exc, sbase + k) >> 32);
+                surv = !fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact);
+            }
+            const uint64_t m = __ballot(surv);
+            if (!m) continue;
+            const uint32_t c = (uint32_t)__popcll(m);
+            nsurv += surv;
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(&a.counters[2], (unsigned long long)c);
+            base = (unsigned long long)shfl64((uint64_t)base, 0);
+            if (surv) {
+                const uint64_t idx = base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
+                const uint64_t gk = sbase + k;
+                if (idx < a.surv_cap)
+                    a.surv[idx] = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
+            }
+        }
+    }
+    uint32_t t1 = ncand, t2 = nsurv;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        t1 += __shfl_xor(t1, o, 64);
+        t2 += __shfl_xor(t2, o, 64);
+    }
+    if (lane == 0 && t1) atomicAdd(&a.counters[1], (unsigned long long)t1);
+    if (lane == 0 && t2) atomicAdd(&a.counters[3], (unsigned long long)t2);
 }
 
 // One wave per fingerprint survivor: exact primer-1 compare unless the fingerprint was
@@ -786,6 +834,7 @@ static void free_search(Search* s) {
     hipFree(s->keys); hipFree(s->tmp_hi); hipFree(s->tmp_lo); hipFree(s->out); hipFree(s->sort_tmp);
     hipFree(s->counters); hipFree(s->spans);
     hipFree(s->surv);
+    hipFree(s->tails);
     if (s->ev0) hipEventDestroy(s->ev0);
     if (s->ev1) hipEventDestroy(s->ev1);
     if (s->ev2) hipEventDestroy(s->ev2);
@@ -812,6 +861,15 @@ static int alloc_surv(Search* s, uint64_t cap) {
     s->surv_cap = 0;
     MP_HIP_CHECK(hipMalloc(&s->surv, cap * sizeof(uint4)));
     s->surv_cap = cap;
+    return MP_OK;
+}
+
+static int alloc_tails(Search* s, uint64_t cap) {
+    hipFree(s->tails);
+    s->tails = nullptr;
+    s->tails_cap = 0;
+    MP_HIP_CHECK(hipMalloc(&s->tails, cap * sizeof(uint4)));
+    s->tails_cap = cap;
     return MP_OK;
 }
 
@@ -842,6 +900,7 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
         }
         rc = alloc_hits(s, 1 << 16);
         if (!rc) rc = alloc_surv(s, 1 << 20);
+        if (!rc) rc = alloc_tails(s, 1 << 18);
     } while (0);
     if (rc) {
         free_search(s);
@@ -929,31 +988,41 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
     a.g_lo = g_lo; a.g_hi = g_hi;
 
-    unsigned long long cnt[4] = {0, 0, 0, 0};
+    unsigned long long cnt[6] = {0, 0, 0, 0, 0, 0};
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
                                                        (uint64_t)s->n_cu * kBlocksPerCU);
-    // scan: seeds -> fingerprint survivors (grow the survivor list and rerun on overflow)
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    // scan: seeds -> fingerprint survivors + bucket-tail references -> tail survivors
+    // (grow the survivor / reference lists and rerun on overflow)
+    for (int attempt = 0; attempt < 3; ++attempt) {
         a.hit_hi = s->keys;
         a.hit_lo = s->keys + s->cap;
         a.counters = s->counters;
         a.cap = s->cap;
         a.surv = s->surv;
         a.surv_cap = s->surv_cap;
-        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 32, st));
+        a.tails = s->tails;
+        a.tails_cap = s->tails_cap;
+        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 48, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
         if (t->lds_exact) hipLaunchKernelGGL(scan_kernel<0>, dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct) hipLaunchKernelGGL(scan_kernel<1>, dim3(grid), dim3(kBlock), 0, st, a);
         else hipLaunchKernelGGL(scan_kernel<2>, dim3(grid), dim3(kBlock), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
+        if (t->max_bucket > 1) {
+            hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
+            MP_HIP_CHECK(hipGetLastError());
+        }
         MP_HIP_CHECK(hipEventRecord(s->ev1, st));
-        MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 32, hipMemcpyDeviceToHost, st));
+        MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 48, hipMemcpyDeviceToHost, st));
         MP_HIP_CHECK(hipStreamSynchronize(st));
-        if (cnt[2] <= s->surv_cap) break;
-        int rc = alloc_surv(s, cnt[2] + cnt[2] / 4 + 1024);
+        if (cnt[2] <= s->surv_cap && cnt[4] <= s->tails_cap) break;
+        int rc = MP_OK;
+        if (cnt[4] > s->tails_cap) rc = alloc_tails(s, cnt[4] + cnt[4] / 4 + 1024);
+        if (!rc && cnt[2] > s->surv_cap) rc = alloc_surv(s, cnt[2] + cnt[2] / 2 + 1024);
         if (rc) return rc;
     }
-    if (cnt[2] > s->surv_cap) return fail(MP_E_STATE, "mp_search_run: survivor list overflow after growth");
+    if (cnt[2] > s->surv_cap || cnt[4] > s->tails_cap)
+        return fail(MP_E_STATE, "mp_search_run: survivor list overflow after growth");
     MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->ev1));
     s->n_candidates = cnt[1];
     s->n_survivors = cnt[3];

@@ -216,6 +216,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         for (uint32_t b = 0; b < nb; ++b) {  // bucket heads carry the bucket's size
             ents[boff[b]].count = bcount[b];
             ents[boff[b]].xstart = boff[b] + 1;
+            for (uint32_t j = 1; j < bcount[b]; ++j) ents[boff[b] + j].count = bcount[b] - 1;  // tail length
         }
         std::vector<uint2> rk;
         std::vector<Entry> dents;
