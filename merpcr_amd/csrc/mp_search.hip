@@ -273,9 +273,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 
 __device__ __forceinline__ void wave_sync() { wave_sync_lds(); }
 
-struct WaveLds {           // per-wave LDS scratch of the drain
-    uint32_t h_mask[64];   // seed hits of the super-step, per lane (bit 31-i = window i)
-    uint32_t h_pre[64];    // exclusive prefix of the per-lane hit counts
+// Per-wave seed queue: the super-step offsets of its seed hits, in window order.  The
+// LDS left beside the 128 KiB prefilter (160 KiB per CU) holds 1008 per wave; a denser
+// super-step is drained in rounds.
+constexpr uint32_t kSeedQ = 1008;
+struct WaveLds {
+    uint16_t q[kSeedQ];
 };
 
 // The current super-step as the wave holds it: lane L owns bases [base + 32L,
@@ -417,22 +420,6 @@ __device__ __forceinline__ bool bucket_head(const ScanArgs& a, uint32_t h, Entry
     }
 }
 
-// Drain a wave's seed queue: one lane per queued seed looks up its bucket head and
-// tests it; bucket tails are expanded 64 candidates at a time.  Every pass yields at
-// most 64 survivors.
-// e-th seed of the super-step: lane by prefix search, window by n-th set bit.
-__device__ __forceinline__ uint32_t seed_offset(const WaveLds& L, uint32_t e) {
-    uint32_t lo = 0, hi = 64;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (L.h_pre[mid] <= e) lo = mid;
-        else hi = mid;
-    }
-    uint32_t m = L.h_mask[lo];
-    for (uint32_t r = e - L.h_pre[lo]; r; --r) m &= ~(0x80000000u >> __clz(m));
-    return lo * kLanePos + (uint32_t)__clz(m);
-}
-
 // Candidate test of one bucket head per lane; a bucket with more records leaves a
 // reference (seed position, bucket) for tail_kernel, which tests the other records.
 template <int kMode>
@@ -462,8 +449,8 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
     for (uint32_t b = 0; b < qn; b += 128) {
         const uint32_t ea = b + (uint32_t)lane, eb = ea + 64;
         const bool la = ea < qn, lb = eb < qn;
-        const uint32_t pa = R.base + (la ? seed_offset(L, ea) : 0u);
-        const uint32_t pb = R.base + (lb ? seed_offset(L, eb) : 0u);
+        const uint32_t pa = R.base + (la ? (uint32_t)L.q[ea] : 0u);
+        const uint32_t pb = R.base + (lb ? (uint32_t)L.q[eb] : 0u);
         uint64_t Ga, Gb;
         uint32_t xa, xb;
         window_from_regs(a, R, sbase, pa, true, Ga, xa);
@@ -696,11 +683,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 #if MP_ABLATE == 1 || MP_ABLATE == 3
         ncand += total;
 #else
-        if (total) {
-            L.h_mask[lane] = hits;
-            L.h_pre[lane] = incl - c;
+        // queue this super-step's seed offsets (lane-major = window order) and drain them
+        for (uint32_t rb = 0; rb < total; rb += kSeedQ) {
+            uint32_t m = hits, q = incl - c;
+            while (m) {
+                const uint32_t i = (uint32_t)__clz(m);
+                m &= ~(0x80000000u >> i);
+                if (q - rb < kSeedQ) L.q[q - rb] = (uint16_t)((uint32_t)lane * kLanePos + i);
+                ++q;
+            }
             wave_sync();
-            drain_seeds<kMode>(a, R, sbase, n, total, lane, ncand, L, C, TC);
+            drain_seeds<kMode>(a, R, sbase, n, min(total - rb, kSeedQ), lane, ncand, L, C, TC);
             wave_sync();
         }
 #endif

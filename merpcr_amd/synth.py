@@ -191,8 +191,18 @@ def build_genome_torch(total: int, records: int, sts: Optional[STSSet], seed: in
         amps, starts = amplicons(sts, total, seed, N, M, W)
         ends = starts + np.array([len(a) for a in amps])
         b0, r0 = to_buf(starts)
-        # drop amplicons that would straddle a record boundary
+        # drop amplicons that would straddle a record boundary, and any that overlaps an
+        # earlier-starting kept one (a scatter with duplicate indices has no defined
+        # winner on the GPU, which made the genome differ between processes)
         keep = (starts - rec_start[r0] + (ends - starts)) <= np.array(lens)[r0]
+        last_end = -1
+        for i in np.argsort(starts, kind="stable"):
+            if not keep[i]:
+                continue
+            if starts[i] < last_end:
+                keep[i] = False
+            else:
+                last_end = ends[i]
         amps = [a for a, k in zip(amps, keep) if k]
         b0 = b0[keep]
         data = np.frombuffer(b"".join(amps), dtype=np.uint8)
