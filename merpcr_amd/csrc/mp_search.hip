@@ -33,6 +33,7 @@
 //   3: neither                      4: drain stops after the bucket lookup
 //   5: fingerprint only (survivors are counted, not pair-checked)
 //   6: pair kernel stops after loading the record   7: pair kernel skips the primer-2 compares
+//   8: pair kernel skips its final hit flush          9: pair kernel never writes hits
 #ifndef MP_ABLATE
 #define MP_ABLATE 0
 #endif
@@ -88,9 +89,9 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Character of exception base j: the run index entry with the largest start <= j,
-// searched between the directory bounds of j's 4096-base block.
-__device__ __forceinline__ uint8_t exc_char(const ScanArgs& a, uint64_t j) {
+// Run of exception base j: the run index entry with the largest start <= j, searched
+// between the directory bounds of j's 4096-base block.
+__device__ __forceinline__ uint64_t exc_run(const ScanArgs& a, uint64_t j) {
     const uint64_t b = j >> kDirShift;
     uint64_t lo = a.xr_dir[b];
     uint64_t hi = min<uint64_t>((uint64_t)a.xr_dir[b + 1] + 1, a.n_xr);
@@ -99,44 +100,85 @@ __device__ __forceinline__ uint8_t exc_char(const ScanArgs& a, uint64_t j) {
         if (a.xr_start[mid] <= j) lo = mid;
         else hi = mid;
     }
-    return a.xr_char[lo];
+    return lo;
+}
+
+// Byte i (0..31) of the 36 primer bytes held as nine 32-bit words.
+__device__ __forceinline__ uint8_t byte_of(const uint32_t (&w)[9], uint32_t i) {
+    uint32_t v = w[0];
+#pragma unroll
+    for (int q = 1; q < 9; ++q) v = (i >> 2) == (uint32_t)q ? w[q] : v;
+    return (uint8_t)(v >> (8 * (i & 3)));
+}
+
+// Exception bases of a window (bit 31-i of ex): their characters come from the run
+// index, walked forward once from the first one; each is compared with the primer
+// character as engine.py:613-631 does and its mismatch bit (62-2i of mmv) set or
+// cleared.  Rare (windows touching non-ACGT bases), so kept out of line.
+__device__ __forceinline__ uint64_t exception_mismatches(const ScanArgs& a, uint32_t ex, uint64_t gpos_c, uint32_t ch_c,
+                                                     uint64_t mmv) {
+    const uint32_t c0 = ch_c & ~3u, sh = ch_c & 3u;
+    uint32_t pw[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) pw[q] = *reinterpret_cast<const uint32_t*>(a.pchars + c0 + 4u * q);
+    uint64_t j = exc_run(a, gpos_c + (uint32_t)__clz(ex));
+    uint8_t gch = a.xr_char[j];
+    uint64_t nxt = j + 1 < a.n_xr ? a.xr_start[j + 1] : ~0ull;
+    while (ex) {
+        const int i = __clz(ex);
+        ex &= ~(0x80000000u >> i);
+        const uint64_t pos = gpos_c + (uint32_t)i;
+        while (pos >= nxt) {  // a later run starts inside the window
+            ++j;
+            gch = a.xr_char[j];
+            nxt = j + 1 < a.n_xr ? a.xr_start[j + 1] : ~0ull;
+        }
+        const bool ok = char_match(gch, byte_of(pw, sh + (uint32_t)i), a.I);
+        const uint64_t bit = 1ull << (62 - 2 * i);
+        mmv = ok ? (mmv & ~bit) : (mmv | bit);
+    }
+    return mmv;
+}
+
+// One chunk (bases c .. c+len-1, len <= 32) of _compare_seqs (engine.py:599-642):
+// genome window G (2-bit, base c on top) and its exception bits ex (bit 31-i) against
+// the primer's accept planes P.  Adds the chunk's mismatches to mm; false on a
+// protected mismatch or more than N.
+__device__ __forceinline__ bool chunk_ok(const ScanArgs& a, uint64_t G, uint32_t ex, uint64_t P0, uint64_t P1,
+                                         uint64_t P2, uint64_t P3, uint64_t gpos_c, uint32_t ch_c, int len, uint32_t c,
+                                         uint32_t L, bool plus, int& mm) {
+    const uint64_t lo = G & kEven, hi = (G >> 1) & kEven;
+    const uint64_t nlo = lo ^ kEven, nhi = hi ^ kEven;
+    const uint64_t match = (nhi & nlo & P0) | (nhi & lo & P1) | (hi & nlo & P2) | (hi & lo & P3);
+    const uint64_t inside = sp_lt(len);
+    uint64_t mmv = ~match & inside;
+    if (len < 32) ex &= ~(0xFFFFFFFFu >> len);
+    if (ex) mmv = exception_mismatches(a, ex, gpos_c, ch_c, mmv);
+    uint64_t prot;
+    if (plus) {
+        const int64_t a0 = (int64_t)L - a.X - (int64_t)c;  // first protected local position
+        prot = inside & ~sp_lt((int)max<int64_t>(min<int64_t>(a0, 32), 0));
+    } else {
+        const int64_t b0 = (int64_t)a.X - (int64_t)c;  // protected local positions < b0
+        prot = sp_lt((int)max<int64_t>(min<int64_t>(b0, len), 0));
+    }
+    if (mmv & prot) return false;
+    mm += __popcll(mmv);
+    return mm <= a.N;
 }
 
 // _compare_seqs (engine.py:599-642) of the L genome bases at global gpos against
 // one primer: protected positions are i >= L-X on the '+' strand (plus == true)
 // and i < X on the '-' strand; any protected mismatch or more than N fails.
-__device__ bool primer_ok(const ScanArgs& a, uint64_t gpos, uint32_t L, uint32_t pl, uint32_t ch,
-                          bool plus) {
+__device__ __forceinline__ bool primer_ok(const ScanArgs& a, uint64_t gpos, uint32_t L, uint32_t pl, uint32_t ch,
+                                          bool plus) {
     int mm = 0;
     for (uint32_t c = 0; c < L; c += 32) {
         const int len = (int)min(32u, L - c);
         const uint64_t G = ext2(a.g2, gpos + c);
+        const uint32_t ex = (uint32_t)(ext1(a.gexc, gpos + c) >> 32);
         const uint64_t* P = a.planes + (uint64_t)(pl + (c >> 5)) * 4;
-        const uint64_t lo = G & kEven, hi = (G >> 1) & kEven;
-        const uint64_t nlo = lo ^ kEven, nhi = hi ^ kEven;
-        const uint64_t match = (nhi & nlo & P[0]) | (nhi & lo & P[1]) | (hi & nlo & P[2]) | (hi & lo & P[3]);
-        const uint64_t inside = sp_lt(len);
-        uint64_t mmv = ~match & inside;
-        uint32_t ex = (uint32_t)(ext1(a.gexc, gpos + c) >> 32);
-        if (len < 32) ex &= ~(0xFFFFFFFFu >> len);
-        while (ex) {
-            const int i = __clz(ex);
-            ex &= ~(0x80000000u >> i);
-            const bool ok = char_match(exc_char(a, gpos + c + (uint32_t)i), a.pchars[ch + c + (uint32_t)i], a.I);
-            const uint64_t bit = 1ull << (62 - 2 * i);
-            mmv = ok ? (mmv & ~bit) : (mmv | bit);
-        }
-        uint64_t prot;
-        if (plus) {
-            const int64_t a0 = (int64_t)L - a.X - (int64_t)c;  // first protected local position
-            prot = inside & ~sp_lt((int)max<int64_t>(min<int64_t>(a0, 32), 0));
-        } else {
-            const int64_t b0 = (int64_t)a.X - (int64_t)c;  // protected local positions < b0
-            prot = sp_lt((int)max<int64_t>(min<int64_t>(b0, len), 0));
-        }
-        if (mmv & prot) return false;
-        mm += __popcll(mmv);
-        if (mm > a.N) return false;
+        if (!chunk_ok(a, G, ex, P[0], P[1], P[2], P[3], gpos + c, ch + c, len, c, L, plus, mm)) return false;
     }
     return true;
 }
@@ -180,6 +222,12 @@ __device__ __forceinline__ bool fp_reject(const ScanArgs& a, uint64_t G, uint32_
     return __popcll(d) > a.N;
 }
 
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Per-wave hit staging (pair kernel): hits collect in LDS and leave in batches of up
 // to 127 with one atomic reservation -- a returning atomic on one global counter
 // sustains only ~88 per microsecond (MI355X_MICROARCH.md, dequeue), far below the hit rate.
@@ -215,13 +263,14 @@ __device__ __forceinline__ void stage_flush(const ScanArgs& a, HitStage& S, int 
 __device__ void pair_check_wave(const ScanArgs& a, uint64_t sbase, uint32_t n, uint32_t k, uint32_t rec,
                                 bool p1_exact, int lane, HitStage& S) {
     const DevRec r = a.recs[rec];
+    const uint32_t rk = a.rank[rec];
     const uint64_t gk = sbase + k;
 #if MP_ABLATE == 6
     if (r.l1 != 0xFFFFFFFFu) return;
 #endif
-    if (!p1_exact && !primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true)) return;
     const uint32_t avail = n - k - r.l1;
     if (avail < r.l2) return;
+    if (!p1_exact && !primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true)) return;
     uint32_t e;
     int hi;
     if (r.size > n - k) {
@@ -232,20 +281,56 @@ __device__ void pair_check_wave(const ScanArgs& a, uint64_t sbase, uint32_t n, u
         hi = (int)min<uint32_t>((uint32_t)a.M, n - k - e);
     }
     const int lo = (int)max<int64_t>(0, min<int64_t>(a.M, (int64_t)e - r.l1 - r.l2));
-    const uint32_t rk = a.rank[rec];
     const int ntry = lo + hi + 1;
+    // The genome bases every try reads, [P0, Pl + l2), are staged in registers as 2-bit
+    // words and exception words (one of each per lane); each lane then takes its
+    // window by shuffles.  One load round trip covers ~2000 bases (every try of the
+    // usual M and primer lengths); longer stretches are restaged per (try block, chunk).
+    const uint64_t P0 = gk + e - r.l2 - (uint32_t)lo;   // global start of the first try
+    const uint64_t last = P0 + (uint64_t)(ntry - 1) + r.l2 - 1;  // last base any try reads
+    const uint64_t wlast = (last >> 5) + 1, elast = (last >> 6) + 1;
+    uint64_t sw = ~0ull, se = ~0ull;  // staged word bases
+    uint64_t gw = 0, ew = 0;
+    uint32_t pchunk = ~0u;
+    uint64_t Q0 = 0, Q1 = 0, Q2 = 0, Q3 = 0;
     for (int b = 0; b < ntry; b += 64) {  // wave-uniform trip count
         const int d = -lo + b + lane;
-        bool hit = false;
-        if (b + lane < ntry) {
-            const int64_t p2 = (int64_t)k + e - r.l2 + d;
-            const bool inb = !(d <= 0 && (int64_t)k + r.l1 > p2) && p2 + r.l2 <= (int64_t)n;
+        const bool act = b + lane < ntry;
+        const int64_t p2 = (int64_t)k + e - r.l2 + d;
+        const bool inb = act && !(d <= 0 && (int64_t)k + r.l1 > p2) && p2 + r.l2 <= (int64_t)n;
+        const uint64_t gp = P0 + (uint64_t)(b + lane);
+        bool ok = true;
+        int mm = 0;
+        for (uint32_t c = 0; c < r.l2; c += 32) {
+            const uint64_t lo_pos = P0 + (uint64_t)b + c;  // window range of this (block, chunk)
+            const uint64_t hi_pos = lo_pos + 63 + 31;
+            if ((lo_pos >> 5) < sw || (hi_pos >> 5) + 1 > sw + 63 || (lo_pos >> 6) < se ||
+                (hi_pos >> 6) + 1 > se + 63) {  // wave-uniform: (re)stage
+                sw = lo_pos >> 5;
+                se = lo_pos >> 6;
+                gw = sw + (uint64_t)lane <= wlast ? a.g2[sw + (uint64_t)lane] : 0ull;
+                ew = se + (uint64_t)lane <= elast ? a.gexc[se + (uint64_t)lane] : 0ull;
+            }
+            if ((c >> 5) != pchunk) {
+                pchunk = c >> 5;
+                const uint64_t* pp = a.planes + (uint64_t)(r.p2_pl + pchunk) * 4;
+                Q0 = pp[0]; Q1 = pp[1]; Q2 = pp[2]; Q3 = pp[3];
+            }
+            const uint64_t q = gp + c;
+            const int rw = (int)((q >> 5) - sw), rs = (int)(q & 31);
+            const int re = (int)((q >> 6) - se), es = (int)(q & 63);
+            const uint64_t x0 = shfl64(gw, rw & 63), x1 = shfl64(gw, (rw + 1) & 63);
+            const uint64_t y0 = shfl64(ew, re & 63), y1 = shfl64(ew, (re + 1) & 63);
+            const uint64_t G = rs ? (x0 << (2 * rs)) | (x1 >> (64 - 2 * rs)) : x0;
+            const uint32_t ex = (uint32_t)((es ? (y0 << es) | (y1 >> (64 - es)) : y0) >> 32);
 #if MP_ABLATE == 7
-            hit = inb && p2 == -12345;
+            ok = ok && (G != ex || q == 0);
 #else
-            hit = inb && primer_ok(a, sbase + (uint64_t)p2, r.l2, r.p2_pl, r.p2_ch, false);
+            if (inb && ok)
+                ok = chunk_ok(a, G, ex, Q0, Q1, Q2, Q3, q, r.p2_ch + c, (int)min(32u, r.l2 - c), c, r.l2, false, mm);
 #endif
         }
+        const bool hit = inb && ok;
         const uint64_t m = __ballot(hit);
         if (m) {
             const uint32_t at = S.n;
@@ -257,7 +342,15 @@ __device__ void pair_check_wave(const ScanArgs& a, uint64_t sbase, uint32_t n, u
             wave_sync_lds();
             if (lane == 0) S.n = at + (uint32_t)__popcll(m);
             wave_sync_lds();
+#if MP_ABLATE == 9
+            if (S.n >= 64) {
+                wave_sync_lds();
+                if (lane == 0) S.n = 0;
+                wave_sync_lds();
+            }
+#else
             if (S.n >= 64) stage_flush(a, S, lane);
+#endif
         }
     }
 }
@@ -288,12 +381,6 @@ struct SuperRegs {
     uint32_t base;
     uint32_t seq;
 };
-
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
-    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
-    return ((uint64_t)hi << 32) | lo;
-}
 
 // 32 bases (2-bit, base p on top) and their exception bits (bit 31-i) starting at
 // sequence position p, with p - base in [0, kSuper): from the owning lane's registers.
@@ -783,15 +870,22 @@ __global__ __launch_bounds__(256) void pair_kernel(ScanArgs a, uint64_t n_surv) 
     if (lane == 0) S.n = 0;
     wave_sync_lds();
     const uint64_t stride = (uint64_t)gridDim.x * 4;
-    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n_surv; i += stride) {
-        const uint4 v = a.surv[i];
-        if (v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu) continue;  // wave-uniform
-        const uint64_t gk = (uint64_t)v.x | ((uint64_t)v.y << 32);
-        const uint64_t sbase = a.seq_base[v.w];
-        const uint32_t n = (uint32_t)a.seq_len[v.w];
-        pair_check_wave(a, sbase, n, (uint32_t)(gk - sbase), v.z & 0x7FFFFFFFu, (v.z >> 31) != 0, lane, S);
+    const uint4 empty = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+    uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    uint4 v = i < n_surv ? a.surv[i] : empty;
+    for (; i < n_surv; i += stride) {
+        const uint4 vn = i + stride < n_surv ? a.surv[i + stride] : empty;  // next survivor, in flight
+        if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {  // wave-uniform
+            const uint64_t gk = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            const uint64_t sbase = a.seq_base[v.w];
+            const uint32_t n = (uint32_t)a.seq_len[v.w];
+            pair_check_wave(a, sbase, n, (uint32_t)(gk - sbase), v.z & 0x7FFFFFFFu, (v.z >> 31) != 0, lane, S);
+        }
+        v = vn;
     }
+#if MP_ABLATE != 8 && MP_ABLATE != 9
     stage_flush(a, S, lane);
+#endif
 }
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
