@@ -24,6 +24,7 @@
 //      wave (primer_ok: bit-sliced accept planes, exception bases resolved through the
 //      run index; lanes split the amplicon-end offsets) and emit 128-bit order keys.
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 #include "mp_internal.h"
@@ -507,9 +508,12 @@ __device__ __forceinline__ bool bucket_head(const ScanArgs& a, uint32_t h, Entry
     }
 }
 
-// Candidate test of one bucket head per lane; a bucket with more records leaves a
-// reference (seed position, bucket) for tail_kernel, which tests the other records.
-template <int kMode>
+// Candidate test of one bucket head per lane, then the bucket tails.  kInline (tables
+// whose buckets are mostly multi-record, e.g. W=8 with 100k STS): the wave expands the
+// tails itself, 64 candidates per pass, each lane finding its bucket by a shuffle
+// search over the inclusive tail-count scan.  Otherwise a bucket with more records
+// leaves a reference (seed position, bucket) for tail_kernel.
+template <int kMode, bool kInline>
 __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRegs& R, uint64_t sbase,
                                                 uint32_t n, bool have, uint32_t pos, const Entry& e0, uint64_t Gp,
                                                 uint32_t exp_, int lane, uint32_t& ncand, SurvChunk& C,
@@ -519,7 +523,31 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
     const bool surv = candidate(a, R, sbase, n, have, pos, e0, ncand, sk, Gp, exp_, true, ex0);
     flush_survivors(a, R, sbase, surv, sk, e0.rec, ex0, lane, C);
     const bool tail = have && e0.count > 1u;
-    if (__any(tail)) {
+    if (!__any(tail)) return;
+    if constexpr (kInline) {
+        const uint32_t xc = tail ? e0.count - 1u : 0u;
+        const uint32_t incl = wave_incl_scan(xc, lane);
+        const uint32_t total = __shfl(incl, 63, 64);
+        for (uint32_t c0 = 0; c0 < total; c0 += 64) {
+            const uint32_t c = c0 + (uint32_t)lane;
+            const bool act = c < total;
+            uint32_t src = 0;  // number of lanes whose inclusive count is <= c
+#pragma unroll
+            for (uint32_t step = 32; step; step >>= 1) {
+                const uint32_t v = (uint32_t)__shfl((int)incl, (int)(src + step - 1), 64);
+                if (v <= c) src += step;
+            }
+            src = min(src, 63u);
+            const uint32_t xpos = (uint32_t)__shfl((int)pos, (int)src, 64);
+            const uint32_t xstart = (uint32_t)__shfl((int)e0.xstart, (int)src, 64);
+            const uint32_t xpre = (uint32_t)__shfl((int)(incl - xc), (int)src, 64);
+            Entry ej{};
+            if (act) ej = a.ents[xstart + (c - xpre)];
+            bool ex2 = false;
+            const bool s2 = candidate(a, R, sbase, n, act, xpos, ej, ncand, sk, 0, 0, false, ex2);
+            flush_survivors(a, R, sbase, s2, sk, ej.rec, ex2, lane, C);
+        }
+    } else {
         const uint64_t gp = sbase + pos;
         append_chunked(&a.counters[4], a.tails, a.tails_cap, tail,
                        make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), e0.xstart, R.seq), lane, TC);
@@ -528,7 +556,7 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
 
 // Drain a super-step's seeds, two per lane per pass (128 per pass): both lanes'
 // lookup chains (rank word -> bucket head) are in flight together.
-template <int kMode>
+template <int kMode, bool kInline>
 __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
                                             uint32_t qn, int lane, uint32_t& ncand, WaveLds& L,
                                             SurvChunk& C, SurvChunk& TC) {
@@ -570,8 +598,8 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
         ncand += (hva && e0a.rec == 0xFFFFFFFFu) + (hvb && e0b.rec == 0xFFFFFFFFu);
         continue;
 #endif
-        heads_and_tails<kMode>(a, R, sbase, n, hva, pa, e0a, Ga, xa, lane, ncand, C, TC);
-        if (b + 64 < qn) heads_and_tails<kMode>(a, R, sbase, n, hvb, pb, e0b, Gb, xb, lane, ncand, C, TC);
+        heads_and_tails<kMode, kInline>(a, R, sbase, n, hva, pa, e0a, Ga, xa, lane, ncand, C, TC);
+        if (b + 64 < qn) heads_and_tails<kMode, kInline>(a, R, sbase, n, hvb, pb, e0b, Gb, xb, lane, ncand, C, TC);
     }
 }
 
@@ -679,7 +707,7 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
 // ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
 // The next super-step's plane words are loaded before the current one is processed.
-template <int kMode>
+template <int kMode, bool kInline>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
@@ -780,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                 ++q;
             }
             wave_sync();
-            drain_seeds<kMode>(a, R, sbase, n, min(total - rb, kSeedQ), lane, ncand, L, C, TC);
+            drain_seeds<kMode, kInline>(a, R, sbase, n, min(total - rb, kSeedQ), lane, ncand, L, C, TC);
             wave_sync();
         }
 #endif
@@ -1091,11 +1119,23 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         a.tails_cap = s->tails_cap;
         MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 48, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-        if (t->lds_exact) hipLaunchKernelGGL(scan_kernel<0>, dim3(grid), dim3(kBlock), 0, st, a);
-        else if (t->filt_direct) hipLaunchKernelGGL(scan_kernel<1>, dim3(grid), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL(scan_kernel<2>, dim3(grid), dim3(kBlock), 0, st, a);
+        // bucket tails inline when most buckets hold several records, else tail_kernel
+        bool inl = t->n_rec > t->n_keys + t->n_keys / 4;
+        if (const char* f = std::getenv("MP_TAILS")) {  // tests: force one tail path
+            if (f[0] == 'i') inl = true;
+            if (f[0] == 'k') inl = false;
+        }
+        if (inl) {
+            if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
+            else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true>), dim3(grid), dim3(kBlock), 0, st, a);
+            else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        } else {
+            if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
+            else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, false>), dim3(grid), dim3(kBlock), 0, st, a);
+            else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
+        }
         MP_HIP_CHECK(hipGetLastError());
-        if (t->max_bucket > 1) {
+        if (!inl && t->max_bucket > 1) {
             hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }

@@ -83,8 +83,13 @@ def test_dense_repeat_order():
     assert lines == case["output"].splitlines()
 
 
+@pytest.mark.parametrize("tails", ["auto", "inline", "kernel"])
 @pytest.mark.parametrize("name", ["random_cases.json.gz", "special_cases.json.gz"])
-def test_golden_corpus(name):
+def test_golden_corpus(name, tails, monkeypatch):
+    """Every recorded reference case, with the multi-record bucket tails expanded by the
+    table's default path and by each of the two paths forced (MP_TAILS)."""
+    if tails != "auto":
+        monkeypatch.setenv("MP_TAILS", tails)
     cases = load_golden(name)["cases"]
     bad = []
     for i, case in enumerate(cases):
@@ -211,3 +216,33 @@ def test_cli_threads_emulation(tmp_path):
                "-T", "4", "--emulate-chunks", "-O", str(out)])
     assert rc == 0
     assert out.read_text() == case["by_threads"]["4"]["output"]
+
+
+@pytest.mark.parametrize("tails", ["inline", "kernel"])
+@pytest.mark.parametrize("W,n_sts,glen,N,I,iupac", [(8, 4000, 3_000_000, 1, 0, 0.0), (11, 20000, 4_000_000, 1, 1, 0.1)])
+def test_dense_tables_vs_c_oracle(tails, W, n_sts, glen, N, I, iupac, monkeypatch):
+    """Larger tables (multi-record buckets everywhere at W=8) through both tail paths,
+    against the C oracle byte for byte, with planted amplicons and N runs."""
+    from merpcr_amd import synth
+    from oracle import c_oracle as C
+    monkeypatch.setenv("MP_TAILS", tails)
+    sts = synth.make_sts(n_sts, seed=7, W=W, iupac=iupac)
+    rng = np.random.default_rng(3)
+    g = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, glen)].copy()
+    for _ in range(30):
+        a = int(rng.integers(0, glen - 3000))
+        g[a:a + int(rng.integers(50, 3000))] = ord("N")
+    amps, starts = synth.amplicons(sts, glen, 7, N, 50, W)
+    for amp, st in list(zip(amps, starts))[:: 3]:
+        if st + len(amp) <= glen:
+            g[st:st + len(amp)] = np.frombuffer(amp, dtype=np.uint8)
+    seq = g.tobytes().decode("ascii")
+    prm = dict(wordsize=W, mismatches=N, iupac_mode=I, margin=50)
+    eng = MerPCR(**prm)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts.text(), td)
+    hits = eng.find_hits([FASTARecord(defline=">chrD", sequence=seq)])
+    table = O.load_sts_lines(sts.text().splitlines(True), W, 240)
+    ref = C.search(table, [g], O.params(**prm), 8)
+    assert len(ref) > 100
+    assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes()
