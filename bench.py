@@ -205,11 +205,12 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scan_ms, pair_ms, order_ms, nhits = [], [], [], 0
+    scan_ms, tail_ms, pair_ms, order_ms, nhits = [], [], [], [], 0
     for _ in range(args.steps):
         nhits = step()
         ls = search.last_stats()
         scan_ms.append(ls["scan_ms"])
+        tail_ms.append(ls["tail_ms"])
         pair_ms.append(ls["pair_ms"])
         order_ms.append(ls["order_ms"])
     torch.cuda.synchronize()
@@ -258,6 +259,7 @@ def main():
         "hits": int(tot_hits),
         "hits_per_s": round(tot_hits / t_step, 1),
         "scan_kernel_ms": round(kern_s * 1e3, 3),
+        "tail_kernel_ms": round(float(np.mean(tail_ms)), 3),
         "pair_kernel_ms": round(float(np.mean(pair_ms)), 3),
         "order_ms": round(float(np.mean(order_ms)), 3),
         "survivors": st["survivors"],

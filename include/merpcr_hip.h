@@ -120,14 +120,14 @@ int mp_search_fetch(void* search, mp_hit* out, uint64_t cap, void* stream);
 int mp_search_fetch_device(void* search, mp_hit* dev_out, uint64_t cap, void* stream);
 /* Device pointer to the sorted hits of the last run (n_hits entries of mp_hit). */
 int mp_search_device_hits(void* search, const mp_hit** dev_hits);
-/* Duration of the last run's scan kernel (HIP events on the run's stream), the
+/* Duration of the last run's scan kernel alone (HIP events on the run's stream), the
  * number of candidate seeds it verified and the windows it scanned. */
 int mp_search_last_stats(void* search, float* scan_ms, uint64_t* n_windows, uint64_t* n_candidates);
 /* Seeds whose primer-1 fingerprint could not reject them (pair-checked). */
 int mp_search_survivors(void* search, uint64_t* n_survivors);
-/* Last run's stage times (HIP events on the run's stream): seed scan kernel,
- * survivor pair-check kernel, ordering (sort + decode). */
-int mp_search_timing(void* search, float* scan_ms, float* pair_ms, float* order_ms);
+/* Last run's stage times (HIP events on the run's stream): seed scan kernel alone,
+ * bucket-tail kernel, survivor pair-check kernel, ordering (sort + decode). */
+int mp_search_timing(void* search, float* scan_ms, float* tail_ms, float* pair_ms, float* order_ms);
 void mp_search_destroy(void* search);
 
 /* ---- FASTA input (replaces FASTALoader.load_file, src/merpcr/io/fasta.py:18-71) --

@@ -86,7 +86,7 @@ def _sig(lib):
     lib.mp_search_device_hits.argtypes = [P, POINTER(c_void_p)]
     lib.mp_search_last_stats.argtypes = [P, POINTER(c_float), u64p, u64p]
     lib.mp_search_survivors.argtypes = [P, u64p]
-    lib.mp_search_timing.argtypes = [P, POINTER(c_float), POINTER(c_float), POINTER(c_float)]
+    lib.mp_search_timing.argtypes = [P, POINTER(c_float), POINTER(c_float), POINTER(c_float), POINTER(c_float)]
     lib.mp_search_destroy.argtypes = [P]
     lib.mp_search_destroy.restype = None
     lib.mp_fasta_load.argtypes = [c_char_p, POINTER(c_void_p)]
@@ -244,10 +244,10 @@ class Search:
         check(lib().mp_search_last_stats(self._h, ctypes.byref(ms), ctypes.byref(nw), ctypes.byref(nc)))
         sv = c_uint64()
         check(lib().mp_search_survivors(self._h, ctypes.byref(sv)))
-        t1, t2, t3 = c_float(), c_float(), c_float()
-        check(lib().mp_search_timing(self._h, ctypes.byref(t1), ctypes.byref(t2), ctypes.byref(t3)))
+        t1, t0, t2, t3 = c_float(), c_float(), c_float(), c_float()
+        check(lib().mp_search_timing(self._h, ctypes.byref(t1), ctypes.byref(t0), ctypes.byref(t2), ctypes.byref(t3)))
         return {"scan_ms": ms.value, "windows": nw.value, "candidates": nc.value, "survivors": sv.value,
-                "pair_ms": t2.value, "order_ms": t3.value}
+                "tail_ms": t0.value, "pair_ms": t2.value, "order_ms": t3.value}
 
     def close(self):
         if self._h:

@@ -172,8 +172,8 @@ struct Search {
     int n_cu = 0;
     uint64_t n_hits = 0;
     uint64_t n_windows = 0, n_candidates = 0, n_survivors = 0;
-    float scan_ms = 0.f, pair_ms = 0.f, order_ms = 0.f;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+    float scan_ms = 0.f, tail_ms = 0.f, pair_ms = 0.f, order_ms = 0.f;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, evt = nullptr;
 };
 
 // ---------------------------------------------------------------- device helpers

@@ -828,14 +828,36 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 // than one record).  The lane walks the bucket's other records in order -- each is the
 // same (seed position, record) candidate the reference's loop over sts_table[h] tests
 // (engine.py:480-489) -- and appends fingerprint survivors to the survivor list.
+// Survivors of a tail_kernel block collect in LDS and leave in batches with one
+// returning atomic: one per wave-iteration would serialise on the single list counter
+// (returning atomics on one address: ~88 per microsecond, MI355X_MICROARCH.md).
+constexpr uint32_t kTailBuf = 512;
+__device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32_t& n_sh,
+                                           unsigned long long& base_sh) {
+    __syncthreads();
+    const uint32_t cnt = min(n_sh, kTailBuf);
+    if (threadIdx.x == 0 && cnt) base_sh = atomicAdd(&a.counters[2], (unsigned long long)cnt);
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < cnt; t += blockDim.x)
+        if (base_sh + t < a.surv_cap) a.surv[base_sh + t] = buf[t];
+    __syncthreads();
+    if (threadIdx.x == 0) n_sh = 0;
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
+    __shared__ uint4 s_buf[kTailBuf];
+    __shared__ uint32_t s_n;
+    __shared__ unsigned long long s_base;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint64_t n_refs = min<uint64_t>(a.counters[4], a.tails_cap);
     const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
     uint32_t ncand = 0, nsurv = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t b = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); b < n_refs; b += stride) {
-        const uint64_t i = b + (uint64_t)lane;
+    for (uint64_t b = (uint64_t)blockIdx.x * 256; b < n_refs; b += stride) {  // block-uniform
+        const uint64_t i = b + threadIdx.x;
         uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
         if (i < n_refs) v = a.tails[i];
         const bool valid = !(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu);
@@ -848,35 +870,31 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
             cnt = a.ents[v.z].count;
         }
         const uint32_t pos = (uint32_t)(gp - sbase);
-        for (uint32_t j = 0; __any(j < cnt); ++j) {
-            bool act = j < cnt;
-            Entry e{};
-            if (act) e = a.ents[v.z + j];
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const Entry e = a.ents[v.z + j];
             const uint32_t k = pos - e.hash_off;
-            act = act && pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
-            act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
-            bool surv = false, exact = false;
-            if (act) {
-                ++ncand;
-                const uint64_t G = ext2(a.g2, sbase + k);
-                const uint32_t ex = (uint32_t)(ext1(exc, sbase + k) >> 32);
-                surv = !fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact);
-            }
-            const uint64_t m = __ballot(surv);
-            if (!m) continue;
-            const uint32_t c = (uint32_t)__popcll(m);
-            nsurv += surv;
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(&a.counters[2], (unsigned long long)c);
-            base = (unsigned long long)shfl64((uint64_t)base, 0);
-            if (surv) {
-                const uint64_t idx = base + (uint64_t)__popcll(m & ((1ull << lane) - 1ull));
-                const uint64_t gk = sbase + k;
-                if (idx < a.surv_cap)
-                    a.surv[idx] = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
+            if (pos < e.hash_off || (uint64_t)k + e.l1 > n || sbase + k < a.g_lo || sbase + k >= a.g_hi) continue;
+            ++ncand;
+            const uint64_t G = ext2(a.g2, sbase + k);
+            const uint32_t ex = (uint32_t)(ext1(exc, sbase + k) >> 32);
+            bool exact = false;
+            if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) continue;
+            ++nsurv;
+            const uint64_t gk = sbase + k;
+            const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
+            const uint32_t at = atomicAdd(&s_n, 1u);
+            if (at < kTailBuf) {
+                s_buf[at] = sv;
+            } else {  // block buffer full (a burst of survivors): straight to the list
+                const unsigned long long g = atomicAdd(&a.counters[2], 1ull);
+                if (g < a.surv_cap) a.surv[g] = sv;
             }
         }
+        __syncthreads();
+        if (s_n >= kTailBuf / 2) tail_flush(a, s_buf, s_n, s_base);  // every thread reads s_n between barriers
+        __syncthreads();
     }
+    tail_flush(a, s_buf, s_n, s_base);
     uint32_t t1 = ncand, t2 = nsurv;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -954,6 +972,7 @@ static void free_search(Search* s) {
     if (s->ev1) hipEventDestroy(s->ev1);
     if (s->ev2) hipEventDestroy(s->ev2);
     if (s->ev3) hipEventDestroy(s->ev3);
+    if (s->evt) hipEventDestroy(s->evt);
     delete s;
 }
 
@@ -1009,7 +1028,8 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
             s->n_cu <= 0)
             s->n_cu = 256;
         if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
-            hipEventCreate(&s->ev2) != hipSuccess || hipEventCreate(&s->ev3) != hipSuccess) {
+            hipEventCreate(&s->ev2) != hipSuccess || hipEventCreate(&s->ev3) != hipSuccess ||
+            hipEventCreate(&s->evt) != hipSuccess) {
             rc = fail(MP_E_HIP, "event creation failed");
             break;
         }
@@ -1071,7 +1091,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     s->n_windows = windows;
     s->n_candidates = 0;
     s->n_hits = 0;
-    s->scan_ms = 0.f;
+    s->scan_ms = s->tail_ms = 0.f;
     if (n_hits) *n_hits = 0;
     if (!tiles) return MP_OK;
     const uint32_t n_real_spans = (uint32_t)spans.size();
@@ -1135,6 +1155,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
         }
         MP_HIP_CHECK(hipGetLastError());
+        MP_HIP_CHECK(hipEventRecord(s->evt, st));
         if (!inl && t->max_bucket > 1) {
             hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
@@ -1150,7 +1171,8 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     }
     if (cnt[2] > s->surv_cap || cnt[4] > s->tails_cap)
         return fail(MP_E_STATE, "mp_search_run: survivor list overflow after growth");
-    MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->ev1));
+    MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
+    MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
     s->n_candidates = cnt[1];
     s->n_survivors = cnt[3];
     // pair-check: survivors -> hits (grow the hit buffer and rerun this stage on overflow)
@@ -1237,10 +1259,11 @@ MP_EXPORT int mp_search_survivors(void* search, uint64_t* n_survivors) {
     return MP_OK;
 }
 
-MP_EXPORT int mp_search_timing(void* search, float* scan_ms, float* pair_ms, float* order_ms) {
+MP_EXPORT int mp_search_timing(void* search, float* scan_ms, float* tail_ms, float* pair_ms, float* order_ms) {
     Search* s = (Search*)search;
     if (!s) return fail(MP_E_ARG, "mp_search_timing: null search");
     if (scan_ms) *scan_ms = s->scan_ms;
+    if (tail_ms) *tail_ms = s->tail_ms;
     if (pair_ms) *pair_ms = s->pair_ms;
     if (order_ms) *order_ms = s->order_ms;
     return MP_OK;

@@ -75,7 +75,7 @@ def main():
             n = s.run()
             ms.append(s.last_stats()["scan_ms"])
         st = s.last_stats()
-        out[v] = {"scan_ms": round(sum(ms) / len(ms), 3), "pair_ms": round(st["pair_ms"], 3),
+        out[v] = {"scan_ms": round(sum(ms) / len(ms), 3), "tail_ms": round(st["tail_ms"], 3), "pair_ms": round(st["pair_ms"], 3),
                   "hits": n, "candidates": st["candidates"], "survivors": st["survivors"]}
         print(f"variant {v}: {out[v]}", flush=True)
         s.close(); genome.close(); table.close()

@@ -26,10 +26,13 @@ if bench:
     open(os.path.join(dst, f"{tag}_bench.json"), "w").write(bench[-1])
 pmc = {}
 for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv"))):
-    agg = collections.defaultdict(list)
+    per = collections.defaultdict(float)  # (dispatch, counter) -> sum over instances
     for r in csv.DictReader(open(f)):
         if "scan_kernel" in r["Kernel_Name"]:
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+    agg = collections.defaultdict(list)
+    for (_, c), v in per.items():
+        agg[c].append(v)
     for k, v in agg.items():
         pmc[k] = sum(v) / len(v)
 trace_ns = None
