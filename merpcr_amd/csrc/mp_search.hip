@@ -43,6 +43,13 @@
 #ifndef MP_NT_STREAM
 #define MP_NT_STREAM 0
 #endif
+// 32-bit fingerprint path for the common bucket head (seed at the primer start, plain
+// primer, at most 16 bases after the seed) and a wave-uniform skip of the owned-range
+// test when the whole super-step is owned.
+#ifndef MP_FASTFP
+#define MP_FASTFP 1
+#endif
+
 
 namespace mp {
 
@@ -381,6 +388,7 @@ struct SuperRegs {
     uint64_t w0, w1, iv;
     uint32_t base;
     uint32_t seq;
+    bool owned;   // every amplicon start k this super-step can produce is in [g_lo, g_hi)
 };
 
 // 32 bases (2-bit, base p on top) and their exception bits (bit 31-i) starting at
@@ -410,13 +418,40 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
                                           uint64_t Gpos, uint32_t expos, bool reuse, bool& exact) {
     const uint32_t k = pos - e.hash_off;
     act = act && pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
-    act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
+#if MP_FASTFP
+    if (!R.owned)
+#endif
+        act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
     uint64_t G = Gpos;
     uint32_t ex = expos;
     if (!reuse || !__all(!act || e.hash_off == 0)) {  // some seed is not at the primer start
         const bool in_regs = k >= R.base && k - R.base < kSuper;
         window_from_regs(a, R, sbase, act ? k : R.base, !act || in_regs, G, ex);
     }
+#if MP_FASTFP
+    // seed at the primer start and a plain primer: bases [0, W) matched exactly, so only
+    // the <= 16 bases after the seed can mismatch -- one 32-bit XOR/popcount
+    const uint32_t W = (uint32_t)a.W;
+    const uint32_t L = (uint32_t)e.l1 - W;
+    const uint32_t inm = L >= 16u ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (2u * L));
+    // (no exception base anywhere in the primer: a genome U in the seed is a literal
+    // mismatch against the primer's T although their 2-bit codes agree)
+    const bool fast = e.hash_off == 0 && e.l1 >= W && L <= 16u && (e.l1 >= 32u ? ex : ex & ~(0xFFFFFFFFu >> e.l1)) == 0 &&
+                      e.pmask == sp_lt((int)e.l1);
+    if (__all(!act || fast)) {
+        if (!act) return false;
+        ++ncand;
+        const uint32_t g = (uint32_t)((G << (2u * W)) >> 32), c = (uint32_t)((e.code << (2u * W)) >> 32);
+        const uint32_t x = g ^ c;
+        const uint32_t d = (x | (x >> 1)) & 0x55555555u & inm;
+        const int32_t p0 = (int32_t)L - a.X;  // protected: relative positions >= L - X
+        const uint32_t prot = p0 <= 0 ? inm : (p0 >= 16 ? 0u : inm & (0xFFFFFFFFu >> (2 * p0)));
+        exact = true;
+        if ((d & prot) || __popc(d) > a.N) return false;
+        k_out = k;
+        return true;
+    }
+#endif
     if (!act) return false;
     ++ncand;
     if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) return false;
@@ -683,6 +718,8 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
                     gw[T] = (h * 2654435761u) >> 27 == 0 ? 0xFFFFFFFFu : 0u;
                     (void)on; (void)fi;
 #else
+                    // kMode 1: the rank words' bits -- the same lines the drain reads next
+                    // for the seeds that pass (a separate bits-only bitmap measured slower)
                     if constexpr (kMode == 1) gw[T] = a.rk[on ? (fi >> 5) : 0u].x;
                     else gw[T] = a.filt[on ? (fi >> 5) : 0u];
 #endif
@@ -779,6 +816,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         R.iv = niv;
         R.base = sp.p_al + (uint32_t)(ss - sp.super0) * kSuper;
         R.seq = sp.seq;
+        R.owned = (a.g_lo == 0 || sbase + R.base >= a.g_lo + 65536u) && sbase + R.base + kSuper <= a.g_hi;
         const uint32_t pb = R.base + (uint32_t)lane * kLanePos;
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
         const uint32_t okm = window_ok_mask(R.iv, W) &
