@@ -117,7 +117,7 @@ struct Table {
     uint32_t* filt = nullptr;     // W >= 14: hashed presence filter
     uint2* rk = nullptr;          // W <= 13: rank bitmap
     Entry* dents = nullptr;       // W <= 13: bucket heads by key rank
-    uint4* dents16 = nullptr;     // W <= 13: compact heads {code lo, code hi, rec, off|l1<<8|flags<<16}
+    uint2* dents8 = nullptr;      // W <= 13: 8-B heads {primer-1 bases W..W+15, rec | (l1-W)<<26 | full<<31}
     Slot* slots = nullptr;        // W >= 14
     Entry* ents = nullptr;
     DevRec* recs = nullptr;
@@ -229,10 +229,12 @@ __host__ __device__ __forceinline__ uint32_t filter_index(uint32_t key, uint32_t
     return (uint32_t)(((uint64_t)key * 0xD6E8FEB86659FD93ull) >> (64 - log2bits));
 }
 
-// Compact bucket head (16 B): usable when the primer-1 fingerprint is "all plain" over
-// l1 <= 32 bases (pmask derivable from l1) and the bucket has no tail; otherwise the
-// flag sends the lookup to the full 32-B Entry.
-constexpr uint32_t kHeadFull = 1u;   // flags: read dents[rank] instead
+// 8-B bucket head: for a single-record bucket whose seed is primer 1's first W bases,
+// primer 1 plain (one A/C/G/T per position) and at most W + 16 bases long, the seed
+// key plus the 2-bit code of bases W..W+15 restate the whole 32-B Entry; any other
+// head sets kHead8Full and the lookup reads the full Entry.
+constexpr uint32_t kHead8Full = 0x80000000u;
+constexpr uint32_t kHead8RecBits = 26;
 
 // LDS prefilter bit of a seed key.  Exact (bit = key) when 4^W fits (W <= 10);
 // above, the top 20 bits of the key left-aligned in 32 bits: keys that differ only in

@@ -69,7 +69,7 @@ struct ScanArgs {
     uint32_t filt_log2;
     const uint2* rk;        // W <= 13: rank bitmap
     const Entry* dents;     // W <= 13: bucket heads by rank
-    const uint4* dents16;   // W <= 13: compact heads
+    const uint2* dents8;    // W <= 13: 8-B heads
     const uint32_t* lfilt;
     const Slot* slots;
     uint32_t slot_log2;
@@ -507,13 +507,14 @@ __device__ __forceinline__ void close_chunked(uint4* buf, uint64_t cap, int lane
         buf[C.base + i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // empty slot
 }
 
-// Entry of a compact head: all-plain fingerprint over l1 bases, single-record bucket.
-__device__ __forceinline__ Entry compact_head(const uint4 c) {
+// Entry of an 8-B head (see kHead8Full): the seed key h supplies primer-1 bases [0, W).
+__device__ __forceinline__ Entry head8_entry(const uint2 c, uint32_t h, uint32_t W) {
     Entry e;
-    e.code = (uint64_t)c.x | ((uint64_t)c.y << 32);
-    e.rec = c.z;
-    e.hash_off = (uint16_t)(c.w & 0xFFu);
-    e.l1 = (uint16_t)((c.w >> 8) & 0xFFu);
+    const uint32_t L = c.y >> kHead8RecBits;  // l1 - W (kHead8Full clear)
+    e.code = ((uint64_t)h << (64 - 2 * W)) | ((uint64_t)c.x << (32 - 2 * W));
+    e.rec = c.y & ((1u << kHead8RecBits) - 1u);
+    e.hash_off = 0;
+    e.l1 = (uint16_t)(W + L);
     e.pmask = sp_lt((int)e.l1);
     e.xstart = 0;
     e.count = 1;
@@ -615,15 +616,15 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
             hvb = (rb.x >> (hb & 31u)) & 1u;
             const uint32_t qa = ra.y + (uint32_t)__popc(ra.x & ((1u << (ha & 31u)) - 1u));
             const uint32_t qb = rb.y + (uint32_t)__popc(rb.x & ((1u << (hb & 31u)) - 1u));
-            const uint4 ca = hva ? a.dents16[qa] : make_uint4(0, 0, 0, 0);
-            const uint4 cb = hvb ? a.dents16[qb] : make_uint4(0, 0, 0, 0);
+            const uint2 ca = hva ? a.dents8[qa] : make_uint2(0, 0);
+            const uint2 cb = hvb ? a.dents8[qb] : make_uint2(0, 0);
             if (hva) {
-                if (ca.w >> 16) e0a = a.dents[qa];  // full entry: IUPAC/long primer or bucket tail
-                else e0a = compact_head(ca);
+                if (ca.y & kHead8Full) e0a = a.dents[qa];  // full entry: IUPAC/long primer or bucket tail
+                else e0a = head8_entry(ca, ha, (uint32_t)a.W);
             }
             if (hvb) {
-                if (cb.w >> 16) e0b = a.dents[qb];
-                else e0b = compact_head(cb);
+                if (cb.y & kHead8Full) e0b = a.dents[qb];
+                else e0b = head8_entry(cb, hb, (uint32_t)a.W);
             }
         } else {
             hva = la && bucket_head<kMode>(a, ha, e0a);
@@ -1153,7 +1154,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.has_u = g->has_u ? 1 : 0;
     a.seq_base = g->d_base; a.seq_len = g->d_len;
     a.spans = s->spans; a.n_spans = n_real_spans;
-    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents16 = t->dents16; a.lfilt = t->lfilt;
+    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
     a.planes = t->planes; a.pchars = t->pchars;

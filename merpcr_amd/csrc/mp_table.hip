@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents16); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -220,7 +220,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         }
         std::vector<uint2> rk;
         std::vector<Entry> dents;
-        std::vector<uint4> dents16;
+        std::vector<uint2> dents8;
         std::vector<Slot> slots;
         if (t->filt_direct) {
             // rank bitmap over the exact 4^W presence bitmap; heads in key order
@@ -232,7 +232,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 acc += (uint32_t)__builtin_popcount(filt[w]);
             }
             dents.resize(std::max<uint32_t>(nb, 1));
-            dents16.resize(std::max<uint32_t>(nb, 1));
+            dents8.resize(std::max<uint32_t>(nb, 1));
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint32_t k = bkey[b];
                 const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
@@ -240,13 +240,12 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 dents[rank] = e;
                 const uint64_t plain_all = e.l1 >= 32 ? 0x5555555555555555ull
                                                       : (e.l1 ? (0x5555555555555555ull & (~0ull << (64 - 2 * e.l1))) : 0ull);
-                const bool compact = e.count == 1 && e.l1 <= 32 && e.hash_off <= 255 && e.pmask == plain_all;
-                uint4 c;
-                c.x = (uint32_t)e.code;
-                c.y = (uint32_t)(e.code >> 32);
-                c.z = e.rec;
-                c.w = compact ? ((uint32_t)e.hash_off | ((uint32_t)e.l1 << 8)) : (kHeadFull << 16);
-                dents16[rank] = c;
+                const bool fast = e.count == 1 && e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 16 &&
+                                  e.pmask == plain_all && e.rec < (1u << kHead8RecBits);
+                uint2 c;
+                c.x = fast ? (uint32_t)((e.code << (2 * W)) >> 32) : 0u;  // bases W..W+15
+                c.y = fast ? (e.rec | ((uint32_t)(e.l1 - W) << kHead8RecBits)) : kHead8Full;
+                dents8[rank] = c;
             }
             filt.assign(1, 0);
         } else {
@@ -279,7 +278,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->slots, slots.data(), slots.size(), &bytes))) break;
         if ((rc = upload(&t->rk, rk.data(), rk.size(), &bytes))) break;
         if ((rc = upload(&t->dents, dents.data(), dents.size(), &bytes))) break;
-        if ((rc = upload(&t->dents16, dents16.data(), dents16.size(), &bytes))) break;
+        if ((rc = upload(&t->dents8, dents8.data(), dents8.size(), &bytes))) break;
         if ((rc = upload(&t->ents, ents.data(), ents.size(), &bytes))) break;
         if ((rc = upload(&t->recs, recs.data(), recs.size(), &bytes))) break;
         if ((rc = upload(&t->rank, rank.data(), rank.size(), &bytes))) break;
