@@ -87,7 +87,7 @@ struct ScanArgs {
     uint64_t cap;
     uint4* surv;
     uint64_t surv_cap;
-    uint4* tails;           // bucket-tail references (seed position + bucket), see tail_kernel
+    uint4* tails;           // bucket-tail references (2 x uint4 each), see tail_kernel
     uint64_t tails_cap;
 };
 
@@ -468,8 +468,9 @@ struct SurvChunk {
     uint32_t total;  // entries of this wave (statistics)
 };
 
+template <int kStride = 1>
 __device__ __forceinline__ void append_chunked(unsigned long long* counter, uint4* buf, uint64_t cap, bool on,
-                                               const uint4& v, int lane, SurvChunk& C) {
+                                               const uint4& v, int lane, SurvChunk& C, const uint4& v2 = uint4{}) {
     const uint64_t m = __ballot(on);
     if (!m) return;
     const uint32_t cnt = (uint32_t)__popcll(m);
@@ -484,7 +485,10 @@ __device__ __forceinline__ void append_chunked(unsigned long long* counter, uint
     if (on) {
         const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         const uint64_t idx = r < avail ? C.base + C.used + r : nbase + (r - avail);
-        if (idx < cap) buf[idx] = v;
+        if (idx < cap) {
+            buf[idx * kStride] = v;
+            if constexpr (kStride == 2) buf[idx * 2 + 1] = v2;
+        }
     }
     if (cnt > avail) {
         C.base = nbase;
@@ -501,10 +505,11 @@ __device__ __forceinline__ void flush_survivors(const ScanArgs& a, const SuperRe
                    make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec | (exact ? 0x80000000u : 0u), R.seq), lane, C);
 }
 
+template <int kStride = 1>
 __device__ __forceinline__ void close_chunked(uint4* buf, uint64_t cap, int lane, const SurvChunk& C) {
     const uint32_t i = C.used + (uint32_t)lane;
     if (C.used < 64u && i < 64u && C.base + i < cap)
-        buf[C.base + i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // empty slot
+        buf[(C.base + i) * kStride] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // empty slot
 }
 
 // Entry of an 8-B head (see kHead8Full): the seed key h supplies primer-1 bases [0, W).
@@ -584,9 +589,13 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
             flush_survivors(a, R, sbase, s2, sk, ej.rec, ex2, lane, C);
         }
     } else {
+        // 32-B reference: seed position, bucket, sequence, and the seed window itself
+        // (window, exception bits, bases left in the sequence), so that tail_kernel tests
+        // records seeded at their primer start without touching the genome again
         const uint64_t gp = sbase + pos;
-        append_chunked(&a.counters[4], a.tails, a.tails_cap, tail,
-                       make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), e0.xstart, R.seq), lane, TC);
+        append_chunked<2>(&a.counters[4], a.tails, a.tails_cap, tail,
+                          make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), e0.xstart, R.seq), lane, TC,
+                          make_uint4((uint32_t)Gp, (uint32_t)(Gp >> 32), exp_, n - pos));
     }
 }
 
@@ -854,7 +863,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         ss = nx;
     }
     close_chunked(a.surv, a.surv_cap, lane, C);
-    close_chunked(a.tails, a.tails_cap, lane, TC);
+    close_chunked<2>(a.tails, a.tails_cap, lane, TC);
     // candidate statistics, one atomic per wave
     uint32_t tot = ncand;
 #pragma unroll
@@ -897,36 +906,41 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t b = (uint64_t)blockIdx.x * 256; b < n_refs; b += stride) {  // block-uniform
         const uint64_t i = b + threadIdx.x;
-        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-        if (i < n_refs) v = a.tails[i];
-        const bool valid = !(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu);
-        uint64_t sbase = 0, gp = 0;
-        uint32_t n = 0, cnt = 0;
-        if (valid) {
-            gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
-            sbase = a.seq_base[v.w];
-            n = (uint32_t)a.seq_len[v.w];
-            cnt = a.ents[v.z].count;
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
+        if (i < n_refs) {
+            v = a.tails[2 * i];
+            w = a.tails[2 * i + 1];
         }
-        const uint32_t pos = (uint32_t)(gp - sbase);
-        for (uint32_t j = 0; j < cnt; ++j) {
-            const Entry e = a.ents[v.z + j];
-            const uint32_t k = pos - e.hash_off;
-            if (pos < e.hash_off || (uint64_t)k + e.l1 > n || sbase + k < a.g_lo || sbase + k >= a.g_hi) continue;
-            ++ncand;
-            const uint64_t G = ext2(a.g2, sbase + k);
-            const uint32_t ex = (uint32_t)(ext1(exc, sbase + k) >> 32);
-            bool exact = false;
-            if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) continue;
-            ++nsurv;
-            const uint64_t gk = sbase + k;
-            const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
-            const uint32_t at = atomicAdd(&s_n, 1u);
-            if (at < kTailBuf) {
-                s_buf[at] = sv;
-            } else {  // block buffer full (a burst of survivors): straight to the list
-                const unsigned long long g = atomicAdd(&a.counters[2], 1ull);
-                if (g < a.surv_cap) a.surv[g] = sv;
+        if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
+            const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
+            const uint32_t rem = w.w;                                    // bases from the seed to the end
+            Entry e = a.ents[v.z];                                       // its count = tail length
+            const uint32_t cnt = e.count;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                if (j) e = a.ents[v.z + j];
+                const uint64_t gk = gp - e.hash_off;
+                if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) continue;  // k + l1 > n / not owned
+                uint64_t G = Gs;
+                uint32_t ex = w.z;
+                if (e.hash_off) {  // seed inside the primer: bounds and window from the genome
+                    const uint64_t sbase = a.seq_base[v.w];
+                    if (gp - sbase < e.hash_off) continue;  // k < 0
+                    G = ext2(a.g2, gk);
+                    ex = (uint32_t)(ext1(exc, gk) >> 32);
+                }
+                ++ncand;
+                bool exact = false;
+                if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) continue;
+                ++nsurv;
+                const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
+                const uint32_t at = atomicAdd(&s_n, 1u);
+                if (at < kTailBuf) {
+                    s_buf[at] = sv;
+                } else {  // block buffer full (a burst of survivors): straight to the list
+                    const unsigned long long g = atomicAdd(&a.counters[2], 1ull);
+                    if (g < a.surv_cap) a.surv[g] = sv;
+                }
             }
         }
         __syncthreads();
@@ -1041,7 +1055,7 @@ static int alloc_tails(Search* s, uint64_t cap) {
     hipFree(s->tails);
     s->tails = nullptr;
     s->tails_cap = 0;
-    MP_HIP_CHECK(hipMalloc(&s->tails, cap * sizeof(uint4)));
+    MP_HIP_CHECK(hipMalloc(&s->tails, cap * 2 * sizeof(uint4)));
     s->tails_cap = cap;
     return MP_OK;
 }
