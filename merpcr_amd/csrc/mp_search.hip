@@ -962,7 +962,8 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
 // already exact, then the amplicon pair-check with lanes over the offsets.
 // Persistent: each wave strides over the survivor list (empty slots skipped) and stages
 // its hits in LDS.
-__global__ __launch_bounds__(256) void pair_kernel(ScanArgs a, uint64_t n_surv) {
+__global__ __launch_bounds__(256) void pair_kernel(ScanArgs a) {
+    const uint64_t n_surv = min<uint64_t>(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
     __shared__ HitStage s_st[4];
     const int lane = threadIdx.x & 63;
     HitStage& S = s_st[threadIdx.x >> 6];
@@ -1179,9 +1180,16 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     unsigned long long cnt[6] = {0, 0, 0, 0, 0, 0};
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
                                                        (uint64_t)s->n_cu * kBlocksPerCU);
-    // scan: seeds -> fingerprint survivors + bucket-tail references -> tail survivors
-    // (grow the survivor / reference lists and rerun on overflow)
-    for (int attempt = 0; attempt < 3; ++attempt) {
+    // scan -> fingerprint survivors (+ bucket-tail references -> tail survivors) -> pair
+    // check -> hit keys, back to back on the stream with one host synchronisation; the
+    // pair kernel reads the survivor count on the device.  A list that overflowed is
+    // grown and the whole pass rerun.
+    bool inl = t->n_rec > t->n_keys + t->n_keys / 4;  // bucket tails inline vs tail_kernel
+    if (const char* f = std::getenv("MP_TAILS")) {    // tests: force one tail path
+        if (f[0] == 'i') inl = true;
+        if (f[0] == 'k') inl = false;
+    }
+    for (int attempt = 0; attempt < 4; ++attempt) {
         a.hit_hi = s->keys;
         a.hit_lo = s->keys + s->cap;
         a.counters = s->counters;
@@ -1192,12 +1200,6 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         a.tails_cap = s->tails_cap;
         MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 48, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-        // bucket tails inline when most buckets hold several records, else tail_kernel
-        bool inl = t->n_rec > t->n_keys + t->n_keys / 4;
-        if (const char* f = std::getenv("MP_TAILS")) {  // tests: force one tail path
-            if (f[0] == 'i') inl = true;
-            if (f[0] == 'k') inl = false;
-        }
         if (inl) {
             if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
             else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -1214,41 +1216,26 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             MP_HIP_CHECK(hipGetLastError());
         }
         MP_HIP_CHECK(hipEventRecord(s->ev1, st));
+        hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * 5), dim3(256), 0, st, a);
+        MP_HIP_CHECK(hipGetLastError());
+        MP_HIP_CHECK(hipEventRecord(s->ev2, st));
         MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 48, hipMemcpyDeviceToHost, st));
         MP_HIP_CHECK(hipStreamSynchronize(st));
-        if (cnt[2] <= s->surv_cap && cnt[4] <= s->tails_cap) break;
+        if (cnt[2] <= s->surv_cap && cnt[4] <= s->tails_cap && cnt[0] <= s->cap) break;
         int rc = MP_OK;
         if (cnt[4] > s->tails_cap) rc = alloc_tails(s, cnt[4] + cnt[4] / 4 + 1024);
         if (!rc && cnt[2] > s->surv_cap) rc = alloc_surv(s, cnt[2] + cnt[2] / 2 + 1024);
+        // hits are produced from the survivors only when those all fit
+        if (!rc && cnt[2] <= s->surv_cap && cnt[0] > s->cap) rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
         if (rc) return rc;
     }
-    if (cnt[2] > s->surv_cap || cnt[4] > s->tails_cap)
-        return fail(MP_E_STATE, "mp_search_run: survivor list overflow after growth");
+    if (cnt[2] > s->surv_cap || cnt[4] > s->tails_cap || cnt[0] > s->cap)
+        return fail(MP_E_STATE, "mp_search_run: list overflow after growth");
     MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
     MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
+    MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     s->n_candidates = cnt[1];
     s->n_survivors = cnt[3];
-    // pair-check: survivors -> hits (grow the hit buffer and rerun this stage on overflow)
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        a.hit_hi = s->keys;
-        a.hit_lo = s->keys + s->cap;
-        a.cap = s->cap;
-        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 8, st));
-        MP_HIP_CHECK(hipEventRecord(s->ev1, st));
-        if (cnt[2]) {
-            const uint32_t pgrid = (uint32_t)std::min<uint64_t>((cnt[2] + 3) / 4, (uint64_t)s->n_cu * 8);
-            hipLaunchKernelGGL(pair_kernel, dim3(pgrid), dim3(256), 0, st, a, (uint64_t)cnt[2]);
-            MP_HIP_CHECK(hipGetLastError());
-        }
-        MP_HIP_CHECK(hipEventRecord(s->ev2, st));
-        MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 8, hipMemcpyDeviceToHost, st));
-        MP_HIP_CHECK(hipStreamSynchronize(st));
-        if (cnt[0] <= s->cap) break;
-        int rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
-        if (rc) return rc;
-    }
-    if (cnt[0] > s->cap) return fail(MP_E_STATE, "mp_search_run: hit buffer overflow after growth");
-    MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     const uint64_t nh = cnt[0];
     int rc = sort_hits(s, nh, st);
     if (rc) return rc;
