@@ -35,6 +35,7 @@
 //   5: fingerprint only (survivors are counted, not pair-checked)
 //   6: pair kernel stops after loading the record   7: pair kernel skips the primer-2 compares
 //   8: pair kernel skips its final hit flush          9: pair kernel never writes hits
+//  10: pair kernel stages synthetic words instead of loading the genome
 #ifndef MP_ABLATE
 #define MP_ABLATE 0
 #endif
@@ -263,102 +264,151 @@ __device__ __forceinline__ void stage_flush(const ScanArgs& a, HitStage& S, int 
     wave_sync_lds();
 }
 
-// _match_sts (engine.py:507-597) for one fingerprint survivor (record `rec`, amplicon
-// start k), executed by the whole wave: unless the fingerprint test was already exact,
-// every lane re-checks primer 1 (same addresses, broadcast loads); the lanes split the
-// amplicon-end offsets d in [-lo, hi] (the reference's try order is restored by the
-// device sort through try_rank(d)).
-__device__ void pair_check_wave(const ScanArgs& a, uint64_t sbase, uint32_t n, uint32_t k, uint32_t rec,
-                                bool p1_exact, int lane, HitStage& S) {
-    const DevRec r = a.recs[rec];
-    const uint32_t rk = a.rank[rec];
-    const uint64_t gk = sbase + k;
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
+    return ((uint64_t)rl32((uint32_t)(v >> 32), j) << 32) | rl32((uint32_t)v, j);
+}
+
+// _match_sts (engine.py:507-597) for the fingerprint survivors of a wave, 64 at a time.
+// Phase 1, lane per survivor: the survivor, its sequence and record, the product-size
+// bounds e/lo/hi and (unless the fingerprint was exact) the primer-1 compare, all in
+// parallel.  Phase 2, one survivor at a time (its values broadcast from its lane): the
+// genome bases every try reads, [P0, last], are staged in registers as 2-bit words and
+// exception words (one each per lane, one load round trip for ~2000 bases; longer
+// stretches restage per block of tries and primer chunk), each lane takes the window of
+// one amplicon-end offset d by shuffles and compares primer 2 -- by one 2-bit XOR and
+// popcount when primer 2 is plain (one base per position) and no exception base is in
+// the windows, else through the accept planes.  The reference's try order 0, -1, +1,
+// ... is restored by the device sort through try_rank(d).
+__device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_surv, int lane, HitStage& S) {
+    const uint64_t i = base + (uint64_t)lane;
+    uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+    if (i < n_surv) v = a.surv[i];
+    bool keep = !(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu);
+    const uint64_t gk = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    const uint32_t rec = v.z & 0x7FFFFFFFu;
+    uint64_t sbase = 0;
+    uint32_t n = 0;
+    DevRec r{};
+    uint32_t rk = 0;
+    if (keep) {
+        sbase = a.seq_base[v.w];
+        n = (uint32_t)a.seq_len[v.w];
+        r = a.recs[rec];
+        rk = a.rank[rec];
+    }
+    const uint32_t k = (uint32_t)(gk - sbase);
+    keep = keep && n - k - r.l1 >= r.l2;
 #if MP_ABLATE == 6
-    if (r.l1 != 0xFFFFFFFFu) return;
+    keep = keep && r.l1 == 0xFFFFFFFFu;
 #endif
-    const uint32_t avail = n - k - r.l1;
-    if (avail < r.l2) return;
-    if (!p1_exact && !primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true)) return;
-    uint32_t e;
-    int hi;
+    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);
+    uint32_t e = 0;
+    int hi = 0;
     if (r.size > n - k) {
         e = n - k;
-        hi = 0;
     } else {
         e = r.size;
         hi = (int)min<uint32_t>((uint32_t)a.M, n - k - e);
     }
     const int lo = (int)max<int64_t>(0, min<int64_t>(a.M, (int64_t)e - r.l1 - r.l2));
-    const int ntry = lo + hi + 1;
-    // The genome bases every try reads, [P0, Pl + l2), are staged in registers as 2-bit
-    // words and exception words (one of each per lane); each lane then takes its
-    // window by shuffles.  One load round trip covers ~2000 bases (every try of the
-    // usual M and primer lengths); longer stretches are restaged per (try block, chunk).
-    const uint64_t P0 = gk + e - r.l2 - (uint32_t)lo;   // global start of the first try
-    const uint64_t last = P0 + (uint64_t)(ntry - 1) + r.l2 - 1;  // last base any try reads
-    const uint64_t wlast = (last >> 5) + 1, elast = (last >> 6) + 1;
-    uint64_t sw = ~0ull, se = ~0ull;  // staged word bases
-    uint64_t gw = 0, ew = 0;
-    uint32_t pchunk = ~0u;
-    uint64_t Q0 = 0, Q1 = 0, Q2 = 0, Q3 = 0;
-    for (int b = 0; b < ntry; b += 64) {  // wave-uniform trip count
-        const int d = -lo + b + lane;
-        const bool act = b + lane < ntry;
-        const int64_t p2 = (int64_t)k + e - r.l2 + d;
-        const bool inb = act && !(d <= 0 && (int64_t)k + r.l1 > p2) && p2 + r.l2 <= (int64_t)n;
-        const uint64_t gp = P0 + (uint64_t)(b + lane);
-        bool ok = true;
-        int mm = 0;
-        for (uint32_t c = 0; c < r.l2; c += 32) {
-            const uint64_t lo_pos = P0 + (uint64_t)b + c;  // window range of this (block, chunk)
-            const uint64_t hi_pos = lo_pos + 63 + 31;
-            if ((lo_pos >> 5) < sw || (hi_pos >> 5) + 1 > sw + 63 || (lo_pos >> 6) < se ||
-                (hi_pos >> 6) + 1 > se + 63) {  // wave-uniform: (re)stage
-                sw = lo_pos >> 5;
-                se = lo_pos >> 6;
-                gw = sw + (uint64_t)lane <= wlast ? a.g2[sw + (uint64_t)lane] : 0ull;
-                ew = se + (uint64_t)lane <= elast ? a.gexc[se + (uint64_t)lane] : 0ull;
-            }
-            if ((c >> 5) != pchunk) {
-                pchunk = c >> 5;
-                const uint64_t* pp = a.planes + (uint64_t)(r.p2_pl + pchunk) * 4;
-                Q0 = pp[0]; Q1 = pp[1]; Q2 = pp[2]; Q3 = pp[3];
-            }
-            const uint64_t q = gp + c;
-            const int rw = (int)((q >> 5) - sw), rs = (int)(q & 31);
-            const int re = (int)((q >> 6) - se), es = (int)(q & 63);
-            const uint64_t x0 = shfl64(gw, rw & 63), x1 = shfl64(gw, (rw + 1) & 63);
-            const uint64_t y0 = shfl64(ew, re & 63), y1 = shfl64(ew, (re + 1) & 63);
-            const uint64_t G = rs ? (x0 << (2 * rs)) | (x1 >> (64 - 2 * rs)) : x0;
-            const uint32_t ex = (uint32_t)((es ? (y0 << es) | (y1 >> (64 - es)) : y0) >> 32);
+    uint64_t todo = __ballot(keep);
+    while (todo) {
+        const int j = (int)__builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint64_t jgk = rl64(gk, j);
+        const uint32_t jn = rl32(n, j), jk = rl32(k, j), je = rl32(e, j);
+        const uint32_t jl1 = rl32(r.l1, j), jl2 = rl32(r.l2, j), jpl = rl32(r.p2_pl, j), jch = rl32(r.p2_ch, j);
+        const uint32_t jrk = rl32(rk, j);
+        const int jlo = (int)rl32((uint32_t)lo, j), jhi = (int)rl32((uint32_t)hi, j);
+        const int ntry = jlo + jhi + 1;
+        const uint64_t P0 = jgk + je - jl2 - (uint32_t)jlo;            // global start of the first try
+        const uint64_t last = P0 + (uint64_t)(ntry - 1) + jl2 - 1;     // last base any try reads
+        const uint64_t wlast = (last >> 5) + 1, elast = (last >> 6) + 1;
+        uint64_t sw = ~0ull, se = ~0ull;  // staged word bases (wave-uniform)
+        uint64_t gw = 0, ew = 0;
+        uint32_t pchunk = ~0u;
+        uint64_t Q0 = 0, Q1 = 0, Q2 = 0, Q3 = 0;
+        // plain primer 2 within 32 bases: its 2-bit code and protected positions (uniform)
+        bool plain2 = false;
+        uint64_t code2 = 0, in2 = 0, prot2 = 0;
+        for (int b = 0; b < ntry; b += 64) {
+            const int d = -jlo + b + lane;
+            const int64_t p2 = (int64_t)jk + je - jl2 + d;
+            const bool inb = b + lane < ntry && !(d <= 0 && (int64_t)jk + jl1 > p2) && p2 + jl2 <= (int64_t)jn;
+            const uint64_t gp = P0 + (uint64_t)(b + lane);
+            bool ok = true;
+            int mm = 0;
+            for (uint32_t c = 0; c < jl2; c += 32) {
+                const uint64_t lo_pos = P0 + (uint64_t)b + c;  // windows of this (block, chunk)
+                const uint64_t hi_pos = lo_pos + 63 + 31;
+                if ((lo_pos >> 5) < sw || (hi_pos >> 5) + 1 > sw + 63 || (lo_pos >> 6) < se ||
+                    (hi_pos >> 6) + 1 > se + 63) {
+                    sw = lo_pos >> 5;
+                    se = lo_pos >> 6;
+#if MP_ABLATE == 10
+                    gw = sw * 0x9E3779B97F4A7C15ull + (uint64_t)lane;
+                    ew = 0;
+#else
+                    gw = sw + (uint64_t)lane <= wlast ? a.g2[sw + (uint64_t)lane] : 0ull;
+                    ew = se + (uint64_t)lane <= elast ? a.gexc[se + (uint64_t)lane] : 0ull;
+#endif
+                }
+                if ((c >> 5) != pchunk) {
+                    pchunk = c >> 5;
+                    const uint64_t* pp = a.planes + (uint64_t)(jpl + pchunk) * 4;
+                    Q0 = pp[0]; Q1 = pp[1]; Q2 = pp[2]; Q3 = pp[3];
+                    if (jl2 <= 32u) {
+                        in2 = sp_lt((int)jl2);
+                        const uint64_t two = (Q0 & Q1) | (Q0 & Q2) | (Q0 & Q3) | (Q1 & Q2) | (Q1 & Q3) | (Q2 & Q3);
+                        plain2 = two == 0 && ((Q0 | Q1 | Q2 | Q3) & in2) == in2;
+                        code2 = ((Q1 | Q3) & kEven) | (((Q2 | Q3) & kEven) << 1);
+                        prot2 = sp_lt(min(a.X, (int)jl2));  // '-' strand: positions < X
+                    }
+                }
+                const uint64_t q = gp + c;
+                const int rw = (int)((q >> 5) - sw), rs = (int)(q & 31);
+                const int re = (int)((q >> 6) - se), es = (int)(q & 63);
+                const uint64_t x0 = shfl64(gw, rw & 63), x1 = shfl64(gw, (rw + 1) & 63);
+                const uint64_t y0 = shfl64(ew, re & 63), y1 = shfl64(ew, (re + 1) & 63);
+                const uint64_t G = rs ? (x0 << (2 * rs)) | (x1 >> (64 - 2 * rs)) : x0;
+                const uint32_t ex = (uint32_t)((es ? (y0 << es) | (y1 >> (64 - es)) : y0) >> 32);
+                const int len = (int)min(32u, jl2 - c);
+                const uint32_t exl = len >= 32 ? ex : ex & ~(0xFFFFFFFFu >> len);
 #if MP_ABLATE == 7
-            ok = ok && (G != ex || q == 0);
+                ok = ok && (G != ex || q == 0);
 #else
-            if (inb && ok)
-                ok = chunk_ok(a, G, ex, Q0, Q1, Q2, Q3, q, r.p2_ch + c, (int)min(32u, r.l2 - c), c, r.l2, false, mm);
+                if (plain2 && __all(!inb || exl == 0)) {
+                    const uint64_t x = G ^ code2;
+                    const uint64_t dm = (x | (x >> 1)) & in2;
+                    ok = !(dm & prot2) && __popcll(dm) <= a.N;
+                } else if (inb && ok) {
+                    ok = chunk_ok(a, G, ex, Q0, Q1, Q2, Q3, q, jch + c, len, c, jl2, false, mm);
+                }
 #endif
-        }
-        const bool hit = inb && ok;
-        const uint64_t m = __ballot(hit);
-        if (m) {
-            const uint32_t at = S.n;
-            if (hit) {
-                const uint32_t i = at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                S.hi[i] = gk;
-                S.lo[i] = ((uint64_t)rk << 32) | try_rank(d);
             }
-            wave_sync_lds();
-            if (lane == 0) S.n = at + (uint32_t)__popcll(m);
-            wave_sync_lds();
+            const bool hit = inb && ok;
+            const uint64_t m = __ballot(hit);
+            if (m) {
+                const uint32_t at = S.n;
+                if (hit) {
+                    const uint32_t idx = at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                    S.hi[idx] = jgk;
+                    S.lo[idx] = ((uint64_t)jrk << 32) | try_rank(d);
+                }
+                wave_sync_lds();
+                if (lane == 0) S.n = at + (uint32_t)__popcll(m);
+                wave_sync_lds();
 #if MP_ABLATE == 9
-            if (S.n >= 64) {
-                wave_sync_lds();
-                if (lane == 0) S.n = 0;
-                wave_sync_lds();
-            }
+                if (S.n >= 64) {
+                    wave_sync_lds();
+                    if (lane == 0) S.n = 0;
+                    wave_sync_lds();
+                }
 #else
-            if (S.n >= 64) stage_flush(a, S, lane);
+                if (S.n >= 64) stage_flush(a, S, lane);
 #endif
+            }
         }
     }
 }
@@ -969,20 +1019,9 @@ __global__ __launch_bounds__(256) void pair_kernel(ScanArgs a) {
     HitStage& S = s_st[threadIdx.x >> 6];
     if (lane == 0) S.n = 0;
     wave_sync_lds();
-    const uint64_t stride = (uint64_t)gridDim.x * 4;
-    const uint4 empty = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-    uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    uint4 v = i < n_surv ? a.surv[i] : empty;
-    for (; i < n_surv; i += stride) {
-        const uint4 vn = i + stride < n_surv ? a.surv[i + stride] : empty;  // next survivor, in flight
-        if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {  // wave-uniform
-            const uint64_t gk = (uint64_t)v.x | ((uint64_t)v.y << 32);
-            const uint64_t sbase = a.seq_base[v.w];
-            const uint32_t n = (uint32_t)a.seq_len[v.w];
-            pair_check_wave(a, sbase, n, (uint32_t)(gk - sbase), v.z & 0x7FFFFFFFu, (v.z >> 31) != 0, lane, S);
-        }
-        v = vn;
-    }
+    const uint64_t stride = (uint64_t)gridDim.x * 4 * 64;
+    for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; b < n_surv; b += stride)
+        pair_check_batch(a, b, n_surv, lane, S);
 #if MP_ABLATE != 8 && MP_ABLATE != 9
     stage_flush(a, S, lane);
 #endif
