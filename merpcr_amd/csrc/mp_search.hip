@@ -50,6 +50,11 @@
 #ifndef MP_FASTFP
 #define MP_FASTFP 1
 #endif
+// survivors per pair-check batch (lanes of the prologue); smaller batches spread the
+// per-survivor loop over more waves
+#ifndef MP_PBATCH
+#define MP_PBATCH 32
+#endif
 
 
 namespace mp {
@@ -283,7 +288,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
 __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_surv, int lane, HitStage& S) {
     const uint64_t i = base + (uint64_t)lane;
     uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-    if (i < n_surv) v = a.surv[i];
+    if (lane < MP_PBATCH && i < n_surv) v = a.surv[i];
     bool keep = !(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu);
     const uint64_t gk = (uint64_t)v.x | ((uint64_t)v.y << 32);
     const uint32_t rec = v.z & 0x7FFFFFFFu;
@@ -1019,8 +1024,8 @@ __global__ __launch_bounds__(256) void pair_kernel(ScanArgs a) {
     HitStage& S = s_st[threadIdx.x >> 6];
     if (lane == 0) S.n = 0;
     wave_sync_lds();
-    const uint64_t stride = (uint64_t)gridDim.x * 4 * 64;
-    for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; b < n_surv; b += stride)
+    const uint64_t stride = (uint64_t)gridDim.x * 4 * MP_PBATCH;
+    for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * MP_PBATCH; b < n_surv; b += stride)
         pair_check_batch(a, b, n_surv, lane, S);
 #if MP_ABLATE != 8 && MP_ABLATE != 9
     stage_flush(a, S, lane);
