@@ -674,14 +674,16 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
         Entry e0a{}, e0b{};
         bool hva, hvb;
         if constexpr (kMode != 2) {
-            const uint2 ra = la ? a.rk[ha >> 5] : make_uint2(0, 0);
-            const uint2 rb = lb ? a.rk[hb >> 5] : make_uint2(0, 0);
-            hva = (ra.x >> (ha & 31u)) & 1u;
-            hvb = (rb.x >> (hb & 31u)) & 1u;
+            // unconditional loads (index 0 when unused): both lanes' chains issue together
+            // instead of one branch-and-wait per load
+            const uint2 ra = a.rk[la ? (ha >> 5) : 0u];
+            const uint2 rb = a.rk[lb ? (hb >> 5) : 0u];
+            hva = la && ((ra.x >> (ha & 31u)) & 1u);
+            hvb = lb && ((rb.x >> (hb & 31u)) & 1u);
             const uint32_t qa = ra.y + (uint32_t)__popc(ra.x & ((1u << (ha & 31u)) - 1u));
             const uint32_t qb = rb.y + (uint32_t)__popc(rb.x & ((1u << (hb & 31u)) - 1u));
-            const uint2 ca = hva ? a.dents8[qa] : make_uint2(0, 0);
-            const uint2 cb = hvb ? a.dents8[qb] : make_uint2(0, 0);
+            const uint2 ca = a.dents8[hva ? qa : 0u];
+            const uint2 cb = a.dents8[hvb ? qb : 0u];
             if (hva) {
                 if (ca.y & kHead8Full) e0a = a.dents[qa];  // full entry: IUPAC/long primer or bucket tail
                 else e0a = head8_entry(ca, ha, (uint32_t)a.W);
