@@ -118,6 +118,8 @@ struct Table {
     uint2* rk = nullptr;          // W <= 13: rank bitmap
     Entry* dents = nullptr;       // W <= 13: bucket heads by key rank
     uint2* dents8 = nullptr;      // W <= 13: 8-B heads {primer-1 bases W..W+15, rec | (l1-W)<<26 | full<<31}
+    uint2* binfo = nullptr;       // W <= kDenseMaxW: per key rank {first ents index, records}
+    uint4* ents16 = nullptr;      // W <= kDenseMaxW: 16-B form of every ents entry (see kDense16Full)
     Slot* slots = nullptr;        // W >= 14
     Entry* ents = nullptr;
     DevRec* recs = nullptr;
@@ -235,6 +237,13 @@ __host__ __device__ __forceinline__ uint32_t filter_index(uint32_t key, uint32_t
 // head sets kHead8Full and the lookup reads the full Entry.
 constexpr uint32_t kHead8Full = 0x80000000u;
 constexpr uint32_t kHead8RecBits = 26;
+// Tables with W <= 9 run dense_kernel: the rank bitmap (4^W / 4 bytes <= 64 KiB) lives in
+// LDS and each lane walks its own seeds' buckets.
+constexpr uint32_t kDenseMaxW = 9;
+// 16-B entry of dense_kernel: {primer-1 bases W..31 (2-bit, top-aligned; lo, hi words),
+// rec | (l1 - W) << 26 | full << 31, 0}; "full" (seed not at the primer start, primer
+// not plain, longer than 32 bases, rec >= 2^26) sends the test to the 32-B Entry.
+constexpr uint32_t kDense16Full = 0x80000000u;
 
 // LDS prefilter bit of a seed key.  Exact (bit = key) when 4^W fits (W <= 10);
 // above, the top 20 bits of the key left-aligned in 32 bits: keys that differ only in

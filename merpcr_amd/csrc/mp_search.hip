@@ -76,6 +76,8 @@ struct ScanArgs {
     const uint2* rk;        // W <= 13: rank bitmap
     const Entry* dents;     // W <= 13: bucket heads by rank
     const uint2* dents8;    // W <= 13: 8-B heads
+    const uint2* binfo;     // W <= kDenseMaxW: bucket {first entry, records} by key rank
+    const uint4* ents16;    // W <= kDenseMaxW: 16-B entries
     const uint32_t* lfilt;
     const Slot* slots;
     uint32_t slot_log2;
@@ -929,6 +931,182 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     if (lane == 0 && C.total) atomicAdd(&a.counters[3], (unsigned long long)C.total);
 }
 
+// Dense seeds (W <= kDenseMaxW, e.g. W=8: ~95% of windows hit one of 62k keys, 3.2 records
+// each).  The exact rank bitmap (4^W / 4 bytes) is staged in LDS; every lane walks its own
+// 32 windows: a seed window's rank gives its bucket {first entry, records} and the lane
+// tests the bucket's records one per iteration from their 8-B form (rec, l1 - W and
+// primer-1 bases W..W+15; the window and its exception bits come from the lane's own
+// registers) -- no seed queue, no shuffles, no head/tail split.  Records whose 8-B form is
+// flagged (seed not at the primer start, IUPAC or long primer) use the full Entry.
+__global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
+    __shared__ uint2 s_rk[(1u << (2 * kDenseMaxW)) / 32];
+    const uint32_t W = (uint32_t)a.W;
+    const uint32_t nrk = max(1u, (1u << (2 * W)) / 32);
+    for (uint32_t i = threadIdx.x; i < nrk; i += kBlock) s_rk[i] = a.rk[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+    const uint64_t n_supers = a.spans[a.n_spans].super0;
+    const uint32_t shw = 32u - 2u * W;
+    const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
+    // the last X positions of a primer are 3'-protected (engine.py:605-611): the lowest
+    // min(X, 32) 2-bit slots of a right-aligned difference word
+    const uint64_t protx = a.X >= 32 ? ~0ull : ((1ull << (2 * a.X)) - 1ull);
+    uint32_t ncand = 0;
+    SurvChunk C{0, 64u, 0u};
+
+    uint64_t ss = (uint64_t)blockIdx.x * kWaves + (uint64_t)w;
+    SeqSpan pf{};
+    pf.super0 = 1;
+    uint64_t pf_end = 0, pf_sbase = 0;
+    uint32_t pf_n = 0;
+    auto locate = [&](uint64_t x) {
+        if (x >= pf.super0 && x < pf_end) return;
+        uint32_t lo = 0, hi = a.n_spans;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.spans[mid].super0 <= x) lo = mid;
+            else hi = mid;
+        }
+        pf = a.spans[lo];
+        pf_end = a.spans[lo + 1].super0;
+        pf_sbase = a.seq_base[pf.seq];
+        pf_n = (uint32_t)a.seq_len[pf.seq];
+    };
+    auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& iv) {
+        const uint64_t j = pf_sbase + pf.p_al + (x - pf.super0) * kSuper + (uint64_t)lane * kLanePos;
+        w0 = a.g2[j >> 5];
+        w1 = a.g2[(j >> 5) + 1];
+        const uint64_t v0 = a.ginv[j >> 6];
+        const uint64_t v1 = a.ginv[(j >> 6) + 1];
+        const uint32_t sh = (uint32_t)(j & 32);
+        iv = (v0 << sh) | ((v1 >> (63 - sh)) >> 1);
+    };
+    uint64_t nw0 = 0, nw1 = 0, niv = 0;
+    if (ss < n_supers) {
+        locate(ss);
+        words(ss, nw0, nw1, niv);
+    }
+    while (ss < n_supers) {
+        const SeqSpan sp = pf;
+        const uint64_t sbase = pf_sbase;
+        const uint32_t n = pf_n;
+        const uint64_t w0 = nw0, w1 = nw1, iv = niv;
+        const uint32_t base = sp.p_al + (uint32_t)(ss - sp.super0) * kSuper;
+        const bool owned = (a.g_lo == 0 || sbase + base >= a.g_lo + 65536u) && sbase + base + kSuper <= a.g_hi;
+        const uint32_t pb = base + (uint32_t)lane * kLanePos;
+        const uint32_t d0 = (uint32_t)(w0 >> 32), d1 = (uint32_t)w0, d2 = (uint32_t)(w1 >> 32);
+        const uint32_t okm = window_ok_mask(iv, W) &
+                             bit_range((int)sp.p_lo - (int)pb, (int)min<int64_t>((int64_t)sp.p_hi - pb, 32));
+        uint32_t seeds = 0;
+        [&]<int... T>(std::integer_sequence<int, T...>) {
+            ((
+                [&] {
+                    const uint32_t h = kmer_top<T>(d0, d1, d2) >> shw;
+                    seeds |= __builtin_amdgcn_ubfe(s_rk[h >> 5].x, h & 31u, 1u) << (31 - T);
+                }()),
+             ...);
+        }(std::make_integer_sequence<int, 32>{});
+        seeds &= okm;
+        const uint64_t nx = ss + stride;
+        if (nx < n_supers) {  // next super-step's words, in flight during this one
+            locate(nx);
+            words(nx, nw0, nw1, niv);
+        }
+        // lane-serial walk over the lane's seed buckets, four records per iteration; the
+        // next seed's bucket info is loaded while the current bucket is tested
+        uint32_t m = seeds;
+        uint32_t ni = 0, cur = 0, end = 0, pos = 0, h = 0, ex = 0;
+        uint2 nbi = make_uint2(0, 0);
+        bool have_n = false, seed_slow = false;
+        uint64_t G = 0, Gt = 0;
+        auto fetch = [&]() {  // rank of the next seed window and its bucket {first, count}
+            ni = (uint32_t)__clz(m);
+            m &= ~(0x80000000u >> ni);
+            const uint64_t Gi = ni ? (w0 << (2 * ni)) | (w1 >> (64 - 2 * ni)) : w0;
+            const uint32_t hi_ = (uint32_t)(Gi >> (64 - 2 * W));
+            const uint2 rw = s_rk[hi_ >> 5];
+            nbi = a.binfo[rw.y + (uint32_t)__popc(rw.x & ((1u << (hi_ & 31u)) - 1u))];
+            have_n = true;
+        };
+        if (m) fetch();
+        while (__any(have_n || cur < end)) {
+            if (cur >= end && have_n) {  // start the next bucket, fetch the one after
+                G = ni ? (w0 << (2 * ni)) | (w1 >> (64 - 2 * ni)) : w0;
+                Gt = G << (2 * W);       // window bases W..31, aligned with the entries' tails
+                h = (uint32_t)(G >> (64 - 2 * W));
+                pos = pb + ni;
+                ex = (uint32_t)((iv << ni) >> 32);
+                if (a.has_u) ex = (uint32_t)(ext1(a.gexc, sbase + pos) >> 32);
+                seed_slow = ex != 0;     // an exception base in the window: full test path
+                cur = nbi.x;
+                end = nbi.x + nbi.y;
+                have_n = false;
+                if (m) fetch();
+            }
+            uint4 c16[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c16[j] = a.ents16[cur + j < end ? cur + j : 0u];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool valid = cur + j < end;
+                const uint32_t y = c16[j].z;
+                const bool slow = valid && ((y & kDense16Full) || seed_slow);
+                // fast test: plain primer seeded at its start; bases [0, W) matched exactly,
+                // mismatches counted over bases W..l1-1 by one 2-bit XOR/popcount
+                const uint32_t L = (y >> kHead8RecBits) & 31u;
+                bool act = valid && !slow && pos + W + L <= n;
+                if (!owned) act = act && sbase + pos >= a.g_lo && sbase + pos < a.g_hi;
+                // bases W..l1-1 right-aligned: the primer's last base in the lowest slot, so
+                // the 3'-protected positions are the lowest X slots (mask in protx)
+                const uint64_t y2 = ((Gt ^ (((uint64_t)c16[j].y << 32) | c16[j].x)) >> (63 - 2 * L)) >> 1;
+                const uint64_t dm = (y2 | (y2 >> 1)) & kEven;
+                bool surv = act && !(dm & protx) && __popcll(dm) <= a.N;
+                bool exact = true;
+                uint32_t rec = y & ((1u << kHead8RecBits) - 1u), k = pos;
+                ncand += act;
+                if (__any(slow)) {  // rare: full Entry through the general test
+                    if (slow) {
+                        const Entry e = a.ents[cur + j];
+                        k = pos - e.hash_off;
+                        rec = e.rec;
+                        bool act2 = pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
+                        if (!owned) act2 = act2 && sbase + k >= a.g_lo && sbase + k < a.g_hi;
+                        surv = false;
+                        if (act2) {
+                            ++ncand;
+                            uint64_t Gk = G;
+                            uint32_t xk = ex;
+                            if (e.hash_off) {  // window of a record seeded inside its primer
+                                Gk = ext2(a.g2, sbase + k);
+                                xk = (uint32_t)(ext1(exc, sbase + k) >> 32);
+                            }
+                            surv = !fp_reject(a, Gk, xk, e.l1, e.code, e.pmask, exact);
+                        }
+                    }
+                }
+                if (__any(surv)) {
+                    const uint64_t gk = sbase + k;
+                    append_chunked(&a.counters[2], a.surv, a.surv_cap, surv,
+                                   make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec | (exact ? 0x80000000u : 0u),
+                                              sp.seq),
+                                   lane, C);
+                }
+            }
+            cur = min(cur + 4u, end);
+        }
+        ss = nx;
+    }
+    close_chunked(a.surv, a.surv_cap, lane, C);
+    uint32_t tot = ncand;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    if (lane == 0 && tot) atomicAdd(&a.counters[1], (unsigned long long)tot);
+    if (lane == 0 && C.total) atomicAdd(&a.counters[3], (unsigned long long)C.total);
+}
+
 // Bucket tails: one lane per reference left by the scan (a seed whose key names more
 // than one record).  The lane walks the bucket's other records in order -- each is the
 // same (seed position, record) candidate the reference's loop over sts_table[h] tests
@@ -1215,6 +1393,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.has_u = g->has_u ? 1 : 0;
     a.seq_base = g->d_base; a.seq_len = g->d_len;
     a.spans = s->spans; a.n_spans = n_real_spans;
+    a.binfo = t->binfo; a.ents16 = t->ents16;
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
@@ -1235,6 +1414,9 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         if (f[0] == 'i') inl = true;
         if (f[0] == 'k') inl = false;
     }
+    // W <= kDenseMaxW: dense_kernel (rank bitmap in LDS, lane-serial bucket walk)
+    bool dense = (uint32_t)t->prm.wordsize <= kDenseMaxW;
+    if (const char* f = std::getenv("MP_DENSE")) dense = dense && f[0] != '0';  // tests: old path
     for (int attempt = 0; attempt < 4; ++attempt) {
         a.hit_hi = s->keys;
         a.hit_lo = s->keys + s->cap;
@@ -1246,7 +1428,9 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         a.tails_cap = s->tails_cap;
         MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 48, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-        if (inl) {
+        if (dense) {
+            hipLaunchKernelGGL(dense_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+        } else if (inl) {
             if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
             else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true>), dim3(grid), dim3(kBlock), 0, st, a);
             else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -1257,7 +1441,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         }
         MP_HIP_CHECK(hipGetLastError());
         MP_HIP_CHECK(hipEventRecord(s->evt, st));
-        if (!inl && t->max_bucket > 1) {
+        if (!dense && !inl && t->max_bucket > 1) {
             hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }

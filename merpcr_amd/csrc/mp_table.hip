@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->binfo); hipFree(t->ents16); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -218,8 +218,22 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             ents[boff[b]].xstart = boff[b] + 1;
             for (uint32_t j = 1; j < bcount[b]; ++j) ents[boff[b] + j].count = bcount[b] - 1;  // tail length
         }
+        // 8-B form of an entry: rec, l1 - W and primer-1 bases W..W+15, for plain
+        // single-chunk primers seeded at their first base; others are flagged full
+        auto entry8 = [&](const Entry& e) {
+            const uint64_t plain_all = e.l1 >= 32 ? 0x5555555555555555ull
+                                                  : (e.l1 ? (0x5555555555555555ull & (~0ull << (64 - 2 * e.l1))) : 0ull);
+            const bool fast = e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 16 && e.pmask == plain_all &&
+                              e.rec < (1u << kHead8RecBits);
+            uint2 c;
+            c.x = fast ? (uint32_t)((e.code << (2 * W)) >> 32) : 0u;  // bases W..W+15
+            c.y = fast ? (e.rec | ((uint32_t)(e.l1 - W) << kHead8RecBits)) : kHead8Full;
+            return c;
+        };
         std::vector<uint2> rk;
         std::vector<Entry> dents;
+        std::vector<uint2> binfo;
+        std::vector<uint4> ents16;
         std::vector<uint2> dents8;
         std::vector<Slot> slots;
         if (t->filt_direct) {
@@ -233,19 +247,28 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             }
             dents.resize(std::max<uint32_t>(nb, 1));
             dents8.resize(std::max<uint32_t>(nb, 1));
+            if (W <= kDenseMaxW) {
+                binfo.resize(std::max<uint32_t>(nb, 1), make_uint2(0, 0));
+                ents16.resize(std::max<uint32_t>(n_rec, 1), make_uint4(0, 0, kDense16Full, 0));
+                for (uint32_t i = 0; i < n_rec; ++i) {
+                    const Entry& e = ents[i];
+                    const uint64_t plain_all = e.l1 >= 32 ? 0x5555555555555555ull
+                                                          : (e.l1 ? (0x5555555555555555ull & (~0ull << (64 - 2 * e.l1))) : 0ull);
+                    const bool fast = e.hash_off == 0 && e.l1 >= W && e.l1 <= 32 && e.pmask == plain_all &&
+                                      e.rec < (1u << kHead8RecBits);
+                    if (!fast) continue;
+                    const uint64_t tail = e.code << (2 * W);  // bases W..31, top-aligned
+                    ents16[i] = make_uint4((uint32_t)tail, (uint32_t)(tail >> 32),
+                                           e.rec | ((uint32_t)(e.l1 - W) << kHead8RecBits), 0u);
+                }
+            }
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint32_t k = bkey[b];
                 const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
                 const Entry& e = ents[boff[b]];
                 dents[rank] = e;
-                const uint64_t plain_all = e.l1 >= 32 ? 0x5555555555555555ull
-                                                      : (e.l1 ? (0x5555555555555555ull & (~0ull << (64 - 2 * e.l1))) : 0ull);
-                const bool fast = e.count == 1 && e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 16 &&
-                                  e.pmask == plain_all && e.rec < (1u << kHead8RecBits);
-                uint2 c;
-                c.x = fast ? (uint32_t)((e.code << (2 * W)) >> 32) : 0u;  // bases W..W+15
-                c.y = fast ? (e.rec | ((uint32_t)(e.l1 - W) << kHead8RecBits)) : kHead8Full;
-                dents8[rank] = c;
+                dents8[rank] = e.count == 1 ? entry8(e) : make_uint2(0u, kHead8Full);
+                if (W <= kDenseMaxW) binfo[rank] = make_uint2(boff[b], bcount[b]);
             }
             filt.assign(1, 0);
         } else {
@@ -279,6 +302,8 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->rk, rk.data(), rk.size(), &bytes))) break;
         if ((rc = upload(&t->dents, dents.data(), dents.size(), &bytes))) break;
         if ((rc = upload(&t->dents8, dents8.data(), dents8.size(), &bytes))) break;
+        if ((rc = upload(&t->binfo, binfo.data(), binfo.size(), &bytes))) break;
+        if ((rc = upload(&t->ents16, ents16.data(), ents16.size(), &bytes))) break;
         if ((rc = upload(&t->ents, ents.data(), ents.size(), &bytes))) break;
         if ((rc = upload(&t->recs, recs.data(), recs.size(), &bytes))) break;
         if ((rc = upload(&t->rank, rank.data(), rank.size(), &bytes))) break;

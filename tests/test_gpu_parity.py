@@ -86,10 +86,12 @@ def test_dense_repeat_order():
 @pytest.mark.parametrize("tails", ["auto", "inline", "kernel"])
 @pytest.mark.parametrize("name", ["random_cases.json.gz", "special_cases.json.gz"])
 def test_golden_corpus(name, tails, monkeypatch):
-    """Every recorded reference case, with the multi-record bucket tails expanded by the
-    table's default path and by each of the two paths forced (MP_TAILS)."""
+    """Every recorded reference case through the default kernels (dense_kernel for W <= 9),
+    and again through scan_kernel with the multi-record bucket tails forced to each of its
+    two paths (MP_DENSE=0, MP_TAILS)."""
     if tails != "auto":
         monkeypatch.setenv("MP_TAILS", tails)
+        monkeypatch.setenv("MP_DENSE", "0")
     cases = load_golden(name)["cases"]
     bad = []
     for i, case in enumerate(cases):
@@ -218,14 +220,18 @@ def test_cli_threads_emulation(tmp_path):
     assert out.read_text() == case["by_threads"]["4"]["output"]
 
 
-@pytest.mark.parametrize("tails", ["inline", "kernel"])
-@pytest.mark.parametrize("W,n_sts,glen,N,I,iupac", [(8, 4000, 3_000_000, 1, 0, 0.0), (11, 20000, 4_000_000, 1, 1, 0.1)])
+@pytest.mark.parametrize("tails", ["auto", "inline", "kernel"])
+@pytest.mark.parametrize("W,n_sts,glen,N,I,iupac", [(8, 4000, 3_000_000, 1, 0, 0.0), (9, 6000, 2_000_000, 2, 1, 0.1),
+                                                    (11, 20000, 4_000_000, 1, 1, 0.1)])
 def test_dense_tables_vs_c_oracle(tails, W, n_sts, glen, N, I, iupac, monkeypatch):
-    """Larger tables (multi-record buckets everywhere at W=8) through both tail paths,
-    against the C oracle byte for byte, with planted amplicons and N runs."""
+    """Larger tables (multi-record buckets everywhere at W=8) through the default kernels
+    and through scan_kernel with both tail paths, against the C oracle byte for byte, with
+    planted amplicons and N runs."""
     from merpcr_amd import synth
     from oracle import c_oracle as C
-    monkeypatch.setenv("MP_TAILS", tails)
+    if tails != "auto":
+        monkeypatch.setenv("MP_TAILS", tails)
+        monkeypatch.setenv("MP_DENSE", "0")
     sts = synth.make_sts(n_sts, seed=7, W=W, iupac=iupac)
     rng = np.random.default_rng(3)
     g = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, glen)].copy()
