@@ -1049,48 +1049,65 @@ __global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
             uint4 c16[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) c16[j] = a.ents16[cur + j < end ? cur + j : 0u];
+            // fast tests of the four slots (plain primers seeded at their start; bases [0, W)
+            // matched exactly, mismatches over bases W..l1-1 by one 2-bit XOR/popcount with
+            // the primer's last base in the lowest slot, so the 3'-protected positions are the
+            // lowest X slots), then one branch for any slot needing the full test and one for
+            // any survivor
+            bool slow[4], surv[4];
+            uint32_t slowm = 0, survm = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const bool valid = cur + j < end;
                 const uint32_t y = c16[j].z;
-                const bool slow = valid && ((y & kDense16Full) || seed_slow);
-                // fast test: plain primer seeded at its start; bases [0, W) matched exactly,
-                // mismatches counted over bases W..l1-1 by one 2-bit XOR/popcount
+                slow[j] = valid && ((y & kDense16Full) || seed_slow);
                 const uint32_t L = (y >> kHead8RecBits) & 31u;
-                bool act = valid && !slow && pos + W + L <= n;
+                bool act = valid && !slow[j] && pos + W + L <= n;
                 if (!owned) act = act && sbase + pos >= a.g_lo && sbase + pos < a.g_hi;
-                // bases W..l1-1 right-aligned: the primer's last base in the lowest slot, so
-                // the 3'-protected positions are the lowest X slots (mask in protx)
                 const uint64_t y2 = ((Gt ^ (((uint64_t)c16[j].y << 32) | c16[j].x)) >> (63 - 2 * L)) >> 1;
                 const uint64_t dm = (y2 | (y2 >> 1)) & kEven;
-                bool surv = act && !(dm & protx) && __popcll(dm) <= a.N;
-                bool exact = true;
-                uint32_t rec = y & ((1u << kHead8RecBits) - 1u), k = pos;
+                surv[j] = act && !(dm & protx) && __popcll(dm) <= a.N;
                 ncand += act;
-                if (__any(slow)) {  // rare: full Entry through the general test
-                    if (slow) {
-                        const Entry e = a.ents[cur + j];
-                        k = pos - e.hash_off;
-                        rec = e.rec;
-                        bool act2 = pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
-                        if (!owned) act2 = act2 && sbase + k >= a.g_lo && sbase + k < a.g_hi;
-                        surv = false;
-                        if (act2) {
-                            ++ncand;
-                            uint64_t Gk = G;
-                            uint32_t xk = ex;
-                            if (e.hash_off) {  // window of a record seeded inside its primer
-                                Gk = ext2(a.g2, sbase + k);
-                                xk = (uint32_t)(ext1(exc, sbase + k) >> 32);
-                            }
-                            surv = !fp_reject(a, Gk, xk, e.l1, e.code, e.pmask, exact);
+                slowm |= (uint32_t)slow[j] << j;
+                survm |= (uint32_t)surv[j] << j;
+            }
+            uint32_t rec[4], kk[4];
+            bool exact[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                rec[j] = c16[j].z & ((1u << kHead8RecBits) - 1u);
+                kk[j] = pos;
+                exact[j] = true;
+            }
+            if (__any(slowm != 0)) {  // rare: full Entry through the general test
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (!slow[j]) continue;
+                    const Entry e = a.ents[cur + j];
+                    kk[j] = pos - e.hash_off;
+                    rec[j] = e.rec;
+                    bool act2 = pos >= e.hash_off && (uint64_t)kk[j] + e.l1 <= n;
+                    if (!owned) act2 = act2 && sbase + kk[j] >= a.g_lo && sbase + kk[j] < a.g_hi;
+                    surv[j] = false;
+                    if (act2) {
+                        ++ncand;
+                        uint64_t Gk = G;
+                        uint32_t xk = ex;
+                        if (e.hash_off) {  // window of a record seeded inside its primer
+                            Gk = ext2(a.g2, sbase + kk[j]);
+                            xk = (uint32_t)(ext1(exc, sbase + kk[j]) >> 32);
                         }
+                        surv[j] = !fp_reject(a, Gk, xk, e.l1, e.code, e.pmask, exact[j]);
                     }
+                    survm = (survm & ~(1u << j)) | ((uint32_t)surv[j] << j);
                 }
-                if (__any(surv)) {
-                    const uint64_t gk = sbase + k;
-                    append_chunked(&a.counters[2], a.surv, a.surv_cap, surv,
-                                   make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec | (exact ? 0x80000000u : 0u),
+            }
+            if (__any(survm != 0)) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint64_t gk = sbase + kk[j];
+                    append_chunked(&a.counters[2], a.surv, a.surv_cap, surv[j],
+                                   make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec[j] | (exact[j] ? 0x80000000u : 0u),
                                               sp.seq),
                                    lane, C);
                 }
