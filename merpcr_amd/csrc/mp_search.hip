@@ -788,9 +788,17 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
                     (void)on; (void)fi;
 #else
                     // kMode 1: the rank words' bits -- the same lines the drain reads next
-                    // for the seeds that pass (a separate bits-only bitmap measured slower)
-                    if constexpr (kMode == 1) gw[T] = a.rk[on ? (fi >> 5) : 0u].x;
-                    else gw[T] = a.filt[on ? (fi >> 5) : 0u];
+                    // for the seeds that pass (a separate bits-only bitmap measured slower).
+                    // Byte offset (h >> 5) * 8 straight from the funnel, masked to 0 by the
+                    // sign-extended LDS bit: shift, and, bfe, and -- no select
+                    if constexpr (kMode == 1) {
+                        const uint32_t off = (kmer_top<T>(d0, d1, d2) >> (shw + 2u)) & ~7u;
+                        const uint32_t sel = (uint32_t)__builtin_amdgcn_sbfe((int)lmask, 31 - T, 1);
+                        gw[T] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(a.rk) + (off & sel));
+                        (void)on; (void)fi;
+                    } else {
+                        gw[T] = a.filt[on ? (fi >> 5) : 0u];
+                    }
 #endif
                 }()),
              ...);
