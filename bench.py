@@ -142,6 +142,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cores))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-bytes-to-output-text pass")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="diagnostic: time only rank 0's owned range of an N-way split on this one GPU "
+                         "(no collective); the JSON line is then not the metric")
     args = ap.parse_args()
 
     import torch
@@ -179,7 +182,7 @@ def main():
     genome.seal(stream)
     pack_s = time.time() - t_pack
     search = _native.Search(table, genome)
-    rng = shard_ranges(lens, world)[rank]
+    rng = shard_ranges(lens, args.shard_of)[0] if args.shard_of > 1 else shard_ranges(lens, world)[rank]
     setup_s = time.time() - t_setup
     log(f"[rank {rank}] setup {setup_s:.1f}s (pack {pack_s:.2f}s) records={len(lens)} bases={sum(lens)} "
         f"sts={n_sts} recs={table.n_rec} planted={planted} table={table.stats()} genome={genome.stats()}")
@@ -242,7 +245,7 @@ def main():
     traffic, traffic_src = pmc_traffic(workload) if world == 1 else (None, None)
     out = {
         "metric": METRIC,
-        "value": round(bases / t_step / 1e9, 4),
+        "value": round(bases / max(args.shard_of, 1) / t_step / 1e9, 4),
         "unit": "Gbp/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -272,6 +275,8 @@ def main():
                                        "gfx950-corrected; includes Infinity-Cache hits)" if traffic else None,
                      "kernel": "mp::scan_kernel", "alg_bytes_per_launch": int(alg_bytes)},
     }
+    if args.shard_of > 1:
+        out["diagnostic"] = f"rank 0 of a {args.shard_of}-way owned-range split, alone on one GPU (not the metric)"
     if world == 1 and not args.no_e2e:
         out["e2e"] = end_to_end(eng, table, names, lens, buf, offs, local, stream)
     if world == 1 and not args.no_cpu_baseline:

@@ -287,10 +287,11 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
 // popcount when primer 2 is plain (one base per position) and no exception base is in
 // the windows, else through the accept planes.  The reference's try order 0, -1, +1,
 // ... is restored by the device sort through try_rank(d).
-__device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_surv, int lane, HitStage& S) {
+__device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_surv, uint32_t batch, int lane,
+                                 HitStage& S) {
     const uint64_t i = base + (uint64_t)lane;
     uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-    if (lane < MP_PBATCH && i < n_surv) v = a.surv[i];
+    if ((uint32_t)lane < batch && i < n_surv) v = a.surv[i];
     bool keep = !(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu);
     const uint64_t gk = (uint64_t)v.x | ((uint64_t)v.y << 32);
     const uint32_t rec = v.z & 0x7FFFFFFFu;
@@ -1229,11 +1230,32 @@ __global__ __launch_bounds__(256) void pair_kernel(ScanArgs a) {
     HitStage& S = s_st[threadIdx.x >> 6];
     if (lane == 0) S.n = 0;
     wave_sync_lds();
-    const uint64_t stride = (uint64_t)gridDim.x * 4 * MP_PBATCH;
-    for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * MP_PBATCH; b < n_surv; b += stride)
-        pair_check_batch(a, b, n_surv, lane, S);
+    // survivors per wave batch: up to MP_PBATCH, fewer when the list is short, so that
+    // every resident wave gets work (a batch is checked one survivor at a time)
+    const uint64_t waves = (uint64_t)gridDim.x * 4;
+    const uint32_t batch = (uint32_t)max<uint64_t>(4, min<uint64_t>(MP_PBATCH, (n_surv + waves - 1) / waves));
+    const uint64_t stride = waves * batch;
+    for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * batch; b < n_surv; b += stride)
+        pair_check_batch(a, b, n_surv, batch, lane, S);
 #if MP_ABLATE != 8 && MP_ABLATE != 9
-    stage_flush(a, S, lane);
+    // the block's four stages leave with one returning atomic: one per wave at the end of
+    // the kernel would serialise ~5k atomics on the hit counter (~88 per microsecond)
+    __syncthreads();
+    __shared__ unsigned long long s_base;
+    if (threadIdx.x == 0) {
+        const uint32_t tot = s_st[0].n + s_st[1].n + s_st[2].n + s_st[3].n;
+        s_base = tot ? atomicAdd(&a.counters[0], (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6;
+    uint64_t off = s_base;
+    for (int q = 0; q < w; ++q) off += s_st[q].n;
+    for (uint32_t i = (uint32_t)lane; i < S.n; i += 64) {
+        if (off + i < a.cap) {
+            a.hit_hi[off + i] = S.hi[i];
+            a.hit_lo[off + i] = S.lo[i];
+        }
+    }
 #endif
 }
 

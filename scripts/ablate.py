@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--shard-of", type=int, default=1, help="search only rank 0's owned range of an N-way split")
     args = ap.parse_args()
     from merpcr_amd import _build
     variants = args.variants.split(",")
@@ -69,10 +70,12 @@ def main():
             genome.put_device(r, buf.data_ptr() + int(offs[r]), n)
         genome.seal()
         s = _native.Search(table, genome)
-        s.run()
+        from merpcr_amd.dist import shard_ranges
+        rng = shard_ranges(lens, args.shard_of)[0] if args.shard_of > 1 else None
+        s.run(rng)
         ms = []
         for _ in range(args.steps):
-            n = s.run()
+            n = s.run(rng)
             ms.append(s.last_stats()["scan_ms"])
         st = s.last_stats()
         out[v] = {"scan_ms": round(sum(ms) / len(ms), 3), "tail_ms": round(st["tail_ms"], 3), "pair_ms": round(st["pair_ms"], 3),
