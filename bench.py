@@ -7,8 +7,11 @@ A step is one full pass of the hot path over the resident genome: seed scan +
 primer verify + pair-check kernel, device ordering of the hits and the hit-count
 readback (mp_search_run); for N > 1 also the RCCL gatherv of every rank's hits
 to rank 0.  Inputs (seed table + packed genome) are resident in HBM before the
-timed region.  Multi-GPU: one process per GPU, the (sequence, k) space split in
-equal contiguous owned ranges (strong scaling: total work fixed).
+timed region.  Multi-GPU: one process per GPU.  Default --scaling weak: the job is
+N genomes' worth of contigs, contig-sharded, one config-sized set of records per
+rank (each rank's contigs drawn from its own seed), so per-GPU work is fixed and
+`value` = all ranks' bases / the slowest rank's step time.  --scaling strong
+splits ONE genome's (sequence, k) space into equal contiguous owned ranges.
 
 Prints ONE JSON line on rank 0.
 """
@@ -142,6 +145,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cores))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-bytes-to-output-text pass")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: each rank scans its own config-sized contig set (N x the genome); "
+                         "strong: one genome split in N owned ranges")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time only rank 0's owned range of an N-way split on this one GPU "
                          "(no collective); the JSON line is then not the metric")
@@ -171,8 +177,9 @@ def main():
         eng._sts_path = fh.name
     assert eng.load_sts_file(eng._sts_path)
     table = eng.device_table()
+    weak = args.scaling == "weak"
     names, lens, buf, offs, planted = synth.build_genome_torch(
-        total, cfg["records"], sts, seed=1, N=cfg["N"], M=cfg["M"], W=cfg["W"], nrun=cfg["nrun"], device=dev)
+        total, cfg["records"], sts, seed=1 + (rank if weak else 0), N=cfg["N"], M=cfg["M"], W=cfg["W"], nrun=cfg["nrun"], device=dev)
     torch.cuda.synchronize()
     genome = _native.Genome(local, lens)
     stream = torch.cuda.current_stream().cuda_stream
@@ -182,7 +189,12 @@ def main():
     genome.seal(stream)
     pack_s = time.time() - t_pack
     search = _native.Search(table, genome)
-    rng = shard_ranges(lens, args.shard_of)[0] if args.shard_of > 1 else shard_ranges(lens, world)[rank]
+    if args.shard_of > 1:
+        rng = shard_ranges(lens, args.shard_of)[0]
+    elif weak:
+        rng = None          # this rank's own contigs, whole
+    else:
+        rng = shard_ranges(lens, world)[rank]
     setup_s = time.time() - t_setup
     log(f"[rank {rank}] setup {setup_s:.1f}s (pack {pack_s:.2f}s) records={len(lens)} bases={sum(lens)} "
         f"sts={n_sts} recs={table.n_rec} planted={planted} table={table.stats()} genome={genome.stats()}")
@@ -199,7 +211,7 @@ def main():
             if comm.numel() < need:
                 comm = torch.empty(need * 2, dtype=torch.uint8, device=dev)
             search.fetch_device(comm.data_ptr(), comm.numel() // HIT_BYTES, stream)
-            gather_hits(comm, n)
+            gather_hits(comm, n, seq_base=rank * len(lens) if weak else 0)
         return n
 
     for _ in range(args.warmup):
@@ -221,7 +233,8 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     st = search.last_stats()
-    local_stats = torch.tensor([elapsed, float(nhits), float(st["windows"]), float(np.mean(scan_ms))],
+    local_stats = torch.tensor([elapsed, float(nhits), float(st["windows"]), float(np.mean(scan_ms)),
+                                float(sum(lens))],
                                dtype=torch.float64, device=dev)
     if world > 1:
         mx = local_stats.clone()
@@ -230,35 +243,41 @@ def main():
         torch.distributed.all_reduce(sm, op=torch.distributed.ReduceOp.SUM)
         elapsed = float(mx[0])
         tot_hits, tot_windows = float(sm[1]), float(sm[2])
+        tot_bases = float(sm[4]) if weak else float(sum(lens))
     else:
         tot_hits, tot_windows = float(nhits), float(st["windows"])
+        tot_bases = float(sum(lens))
     if rank != 0:
         torch.distributed.destroy_process_group()
         return
-    bases = float(sum(lens))
+    bases = float(sum(lens))          # one rank's genome (= the whole job's at N=1 or strong)
     t_step = elapsed / args.steps
     kern_s = float(np.mean(scan_ms)) / 1e3
     alg_bytes = BYTES_PER_BASE * st["windows"] + BYTES_PER_HIT * nhits  # rank 0's scan launch
     achieved = alg_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
     workload = (f"{args.config}: {n_sts} STS vs {bases / 1e9:.3f} Gbp ({len(lens)} records), "
                 f"W={cfg['W']} N={cfg['N']} M={cfg['M']} I={cfg['I']}")
+    if world > 1 and weak:
+        workload += f" per rank ({world} contig sets, {tot_bases / 1e9:.3f} Gbp in all)"
     traffic, traffic_src = pmc_traffic(workload) if world == 1 else (None, None)
     out = {
         "metric": METRIC,
-        "value": round(bases / max(args.shard_of, 1) / t_step / 1e9, 4),
+        "value": round(tot_bases / max(args.shard_of, 1) / t_step / 1e9, 4),
         "unit": "Gbp/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(t_step * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded generator, merpcr_amd/synth.py; genome generated in HBM)",
         "config": {"workload": workload,
                    "sts": n_sts, "records": len(lens), "bases": int(bases), "W": cfg["W"], "N": cfg["N"],
-                   "M": cfg["M"], "I": cfg["I"], "parallelism": f"owned-k shards x{world}"},
+                   "M": cfg["M"], "I": cfg["I"],
+                   "parallelism": (f"contig shards x{world} (per-rank contig set, RCCL hit gatherv)" if weak
+                                   else f"owned-k shards x{world} (RCCL hit gatherv)")},
         "hits": int(tot_hits),
         "hits_per_s": round(tot_hits / t_step, 1),
         "scan_kernel_ms": round(kern_s * 1e3, 3),

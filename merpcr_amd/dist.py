@@ -15,6 +15,11 @@ back by pickling.  Here one process drives one GPU (torch.distributed, backend
   ``gather_hits`` is a gatherv: an all_gather of per-rank counts, then one
   point-to-point transfer per rank into rank 0's buffer.  There is no other
   data-path collective.
+* Contig sharding (``contig_shards``): each rank holds only its own whole
+  records (a contiguous run of the file's records, balanced by bases) and
+  scans them completely; ``gather_hits(..., seq_base=first record)`` shifts
+  the rank-local record index to the file's before the gatherv, so rank 0
+  again receives the file-ordered hit list.
 """
 
 from __future__ import annotations
@@ -49,14 +54,33 @@ def shard_ranges(lengths: Sequence[int], world: int) -> List[Tuple[int, int, int
     return out
 
 
-def gather_hits(local, n_local: int, group=None, dst: int = 0) -> Optional[object]:
+def contig_shards(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """Contiguous record ranges [first, last) per rank, balanced by bases (whole records)."""
+    lens = np.asarray(lengths, dtype=np.int64)
+    cum = np.concatenate([[0], np.cumsum(lens)])
+    total = int(cum[-1])
+    cuts = [0]
+    for r in range(1, world):
+        c = int(np.searchsorted(cum, total * r // world, side="left"))
+        cuts.append(min(max(c, cuts[-1]), len(lens)))
+    cuts.append(len(lens))
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def gather_hits(local, n_local: int, group=None, dst: int = 0, seq_base: int = 0) -> Optional[object]:
     """Gather per-rank hit byte buffers (torch uint8 tensors) to rank ``dst``.
 
-    ``local`` holds at least n_local * 24 bytes.  Returns the concatenated
-    tensor on rank ``dst`` (rank order), None elsewhere.
+    ``local`` holds at least n_local * 24 bytes.  ``seq_base`` (contig sharding)
+    is added to every hit's record index first, in place.  Returns the
+    concatenated tensor on rank ``dst`` (rank order), None elsewhere.
     """
     import torch
     import torch.distributed as dist
+
+    if seq_base and n_local:
+        # mp_hit = {u64 pos1, u64 pos2, u32 seq, u32 rec}: seq is int32 word 4 of 6
+        words = local[:n_local * HIT_BYTES].view(torch.int32).view(n_local, HIT_BYTES // 4)
+        words[:, 4] += seq_base
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)

@@ -11,7 +11,7 @@ import socket
 import numpy as np
 import pytest
 
-from merpcr_amd.dist import HIT_BYTES, as_hits, gather_hits, shard_ranges
+from merpcr_amd.dist import HIT_BYTES, as_hits, contig_shards, gather_hits, shard_ranges
 
 
 def test_shard_ranges_tile_the_genome():
@@ -22,6 +22,16 @@ def test_shard_ranges_tile_the_genome():
         assert rs[-1][1] == len(lens) and rs[-1][3] == 0
         for a, b in zip(rs[:-1], rs[1:]):
             assert (a[1], a[3]) == (b[0], b[2])
+
+
+def test_contig_shards_balance_whole_records():
+    lens = [250, 10, 10, 200, 190, 5, 0, 180]
+    for world in (1, 2, 3, 4, 8, 11):
+        rs = contig_shards(lens, world)
+        assert len(rs) == world and rs[0][0] == 0 and rs[-1][1] == len(lens)
+        assert all(a[1] == b[0] for a, b in zip(rs[:-1], rs[1:]))
+        assert all(a <= b for a, b in rs)
+    assert contig_shards(lens, 2) == [(0, 4), (4, 8)]
 
 
 def _free_port():
@@ -56,8 +66,15 @@ def _worker(rank, world, port, q):
     mine = whole[(key >= lo) & (key < hi)]
     buf = torch.from_numpy(np.frombuffer(mine.tobytes() + b"\0" * HIT_BYTES, dtype=np.uint8).copy())
     got = gather_hits(buf, len(mine))
+    ok = rank != 0 or as_hits(got).tobytes() == whole.tobytes()
+    # contig sharding: this rank searches only its own whole records, indices local to them
+    fa, fb = contig_shards([len(s) for s in seqs], world)[rank]
+    part = C.search(table, seqs[fa:fb], prm) if fb > fa else whole[:0]
+    buf = torch.from_numpy(np.frombuffer(part.tobytes() + b"\0" * HIT_BYTES, dtype=np.uint8).copy())
+    got = gather_hits(buf, len(part), seq_base=fa)
     if rank == 0:
-        q.put((as_hits(got).tobytes() == whole.tobytes(), len(whole)))
+        ok = ok and as_hits(got).tobytes() == whole.tobytes()
+        q.put((ok, len(whole)))
     dist.barrier()
     dist.destroy_process_group()
 
