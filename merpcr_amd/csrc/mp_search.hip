@@ -421,13 +421,30 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
     }
 }
 
+#ifndef MP_DPP_SCAN
+#define MP_DPP_SCAN 1
+#endif
+// Inclusive wave64 prefix sum.  DPP form: row_shr 1/2/4/8 within each 16-lane row, then
+// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- six VALU ops with no LDS round
+// trip, where the shuffle form is six dependent ds_bpermute waits.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#if MP_DPP_SCAN
+    (void)lane;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+#else
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(v, o, 64);
         if (lane >= o) v += y;
     }
     return v;
+#endif
 }
 
 __device__ __forceinline__ void wave_sync() { wave_sync_lds(); }
@@ -626,7 +643,7 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
     if constexpr (kInline) {
         const uint32_t xc = tail ? e0.count - 1u : 0u;
         const uint32_t incl = wave_incl_scan(xc, lane);
-        const uint32_t total = __shfl(incl, 63, 64);
+        const uint32_t total = rl32(incl, 63);
         for (uint32_t c0 = 0; c0 < total; c0 += 64) {
             const uint32_t c = c0 + (uint32_t)lane;
             const bool act = c < total;
@@ -910,7 +927,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         // publish this super-step's seed hits: per-lane masks + prefix of their counts
         const uint32_t c = (uint32_t)__popc(hits);
         const uint32_t incl = wave_incl_scan(c, lane);
-        const uint32_t total = __shfl(incl, 63, 64);
+        const uint32_t total = rl32(incl, 63);
 #if MP_ABLATE == 1 || MP_ABLATE == 3
         ncand += total;
 #else
@@ -947,7 +964,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 // primer-1 bases W..W+15; the window and its exception bits come from the lane's own
 // registers) -- no seed queue, no shuffles, no head/tail split.  Records whose 8-B form is
 // flagged (seed not at the primer start, IUPAC or long primer) use the full Entry.
+#ifndef MP_DENSE_SLOTS
+#define MP_DENSE_SLOTS 4
+#endif
 __global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
+    constexpr int kDS = MP_DENSE_SLOTS;  // bucket records tested per lane-iteration
     __shared__ uint2 s_rk[(1u << (2 * kDenseMaxW)) / 32];
     const uint32_t W = (uint32_t)a.W;
     const uint32_t nrk = max(1u, (1u << (2 * W)) / 32);
@@ -1055,18 +1076,24 @@ __global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
                 have_n = false;
                 if (m) fetch();
             }
-            uint4 c16[4];
+            uint4 c16[kDS];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) c16[j] = a.ents16[cur + j < end ? cur + j : 0u];
+            for (int j = 0; j < kDS; ++j) {
+#if MP_ABLATE == 11
+                c16[j] = make_uint4(cur * 2654435761u + j, cur ^ 0x5bd1e995u, (cur & 0xFFFFu) | (10u << kHead8RecBits), 0u);
+#else
+                c16[j] = a.ents16[cur + j < end ? cur + j : 0u];
+#endif
+            }
             // fast tests of the four slots (plain primers seeded at their start; bases [0, W)
             // matched exactly, mismatches over bases W..l1-1 by one 2-bit XOR/popcount with
             // the primer's last base in the lowest slot, so the 3'-protected positions are the
             // lowest X slots), then one branch for any slot needing the full test and one for
             // any survivor
-            bool slow[4], surv[4];
+            bool slow[kDS], surv[kDS];
             uint32_t slowm = 0, survm = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < kDS; ++j) {
                 const bool valid = cur + j < end;
                 const uint32_t y = c16[j].z;
                 slow[j] = valid && ((y & kDense16Full) || seed_slow);
@@ -1080,17 +1107,17 @@ __global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
                 slowm |= (uint32_t)slow[j] << j;
                 survm |= (uint32_t)surv[j] << j;
             }
-            uint32_t rec[4], kk[4];
-            bool exact[4];
+            uint32_t rec[kDS], kk[kDS];
+            bool exact[kDS];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < kDS; ++j) {
                 rec[j] = c16[j].z & ((1u << kHead8RecBits) - 1u);
                 kk[j] = pos;
                 exact[j] = true;
             }
             if (__any(slowm != 0)) {  // rare: full Entry through the general test
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kDS; ++j) {
                     if (!slow[j]) continue;
                     const Entry e = a.ents[cur + j];
                     kk[j] = pos - e.hash_off;
@@ -1113,7 +1140,7 @@ __global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
             }
             if (__any(survm != 0)) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kDS; ++j) {
                     const uint64_t gk = sbase + kk[j];
                     append_chunked(&a.counters[2], a.surv, a.surv_cap, surv[j],
                                    make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec[j] | (exact[j] ? 0x80000000u : 0u),
@@ -1121,7 +1148,7 @@ __global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
                                    lane, C);
                 }
             }
-            cur = min(cur + 4u, end);
+            cur = min(cur + (uint32_t)kDS, end);
         }
         ss = nx;
     }
