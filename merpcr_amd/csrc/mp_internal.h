@@ -118,8 +118,12 @@ struct Table {
     uint2* rk = nullptr;          // W <= 13: rank bitmap
     Entry* dents = nullptr;       // W <= 13: bucket heads by key rank
     uint2* dents8 = nullptr;      // W <= 13: 8-B heads {primer-1 bases W..W+15, rec | (l1-W)<<26 | full<<31}
-    uint2* binfo = nullptr;       // W <= kDenseMaxW: per key rank {first ents index, records}
-    uint4* ents16 = nullptr;      // W <= kDenseMaxW: 16-B form of every ents entry (see kDense16Full)
+    uint2* binfo = nullptr;       // W <= kDenseMaxW: per key rank {first padded entry, records}
+    uint16_t* dfilt = nullptr;    // W <= kDenseMaxW: 2-B filter word per padded entry (kDenseAlways...)
+    uint4* dgrp = nullptr;        // W <= kDenseMaxW: per 32 keys {bits, escape bits, first oct, 0}
+    Entry* dents_pad = nullptr;   // W <= kDenseMaxW: ents with every bucket padded to a multiple of 4
+    uint32_t dense_F = 0;         // bases after the seed the filter words hold
+    uint32_t dense_M = 0;         // their mismatch mask in both halves of a 32-bit word pair
     Slot* slots = nullptr;        // W >= 14
     Entry* ents = nullptr;
     DevRec* recs = nullptr;
@@ -240,10 +244,17 @@ constexpr uint32_t kHead8RecBits = 26;
 // Tables with W <= 9 run dense_kernel: the rank bitmap (4^W / 4 bytes <= 64 KiB) lives in
 // LDS and each lane walks its own seeds' buckets.
 constexpr uint32_t kDenseMaxW = 9;
-// 16-B entry of dense_kernel: {primer-1 bases W..31 (2-bit, top-aligned; lo, hi words),
-// rec | (l1 - W) << 26 | full << 31, 0}; "full" (seed not at the primer start, primer
-// not plain, longer than 32 bases, rec >= 2^26) sends the test to the 32-B Entry.
-constexpr uint32_t kDense16Full = 0x80000000u;
+// Filter word of a dense_kernel entry (16 bits): primer-1 bases W..W+F-1 (2-bit, base W
+// in bits 15:14), F <= 7 fixed per table, flags in bits 1:0.  A seed window whose bases
+// W..W+F-1 differ from them in more than N positions cannot be a survivor (a mismatch at a
+// plain primer position is a real one; a genome exception base there reads as 'A' and can
+// only hide mismatches under I=0, and windows with exception bases take the full test
+// under I=1), so only the words that pass reach the 32-B Entry.  Buckets of up to eight
+// records take one 16-B oct of filter words: one load per seed window.
+constexpr uint32_t kDenseAlways = 1u;   // entry not filterable (seed inside the primer, short or IUPAC primer)
+constexpr uint32_t kDensePad = 2u;      // padding slot of an oct
+constexpr uint32_t kDenseMaxF = 7;
+constexpr uint32_t kDenseOct = 8;
 
 // LDS prefilter bit of a seed key.  Exact (bit = key) when 4^W fits (W <= 10);
 // above, the top 20 bits of the key left-aligned in 32 bits: keys that differ only in

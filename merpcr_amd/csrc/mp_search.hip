@@ -76,8 +76,11 @@ struct ScanArgs {
     const uint2* rk;        // W <= 13: rank bitmap
     const Entry* dents;     // W <= 13: bucket heads by rank
     const uint2* dents8;    // W <= 13: 8-B heads
-    const uint2* binfo;     // W <= kDenseMaxW: bucket {first entry, records} by key rank
-    const uint4* ents16;    // W <= kDenseMaxW: 16-B entries
+    const uint2* binfo;     // W <= kDenseMaxW: bucket {first padded entry, records} by key rank
+    const uint16_t* dfilt;  // W <= kDenseMaxW: filter word per padded entry
+    const uint4* dgrp;      // W <= kDenseMaxW: per-32-key bucket index
+    const Entry* dents_pad; // W <= kDenseMaxW: Entry per padded entry
+    uint32_t dense_M;       // filter mismatch mask
     const uint32_t* lfilt;
     const Slot* slots;
     uint32_t slot_log2;
@@ -958,36 +961,78 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 }
 
 // Dense seeds (W <= kDenseMaxW, e.g. W=8: ~95% of windows hit one of 62k keys, 3.2 records
-// each).  The exact rank bitmap (4^W / 4 bytes) is staged in LDS; every lane walks its own
-// 32 windows: a seed window's rank gives its bucket {first entry, records} and the lane
-// tests the bucket's records one per iteration from their 8-B form (rec, l1 - W and
-// primer-1 bases W..W+15; the window and its exception bits come from the lane's own
-// registers) -- no seed queue, no shuffles, no head/tail split.  Records whose 8-B form is
-// flagged (seed not at the primer start, IUPAC or long primer) use the full Entry.
-#ifndef MP_DENSE_SLOTS
-#define MP_DENSE_SLOTS 4
-#endif
-__global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
-    constexpr int kDS = MP_DENSE_SLOTS;  // bucket records tested per lane-iteration
-    __shared__ uint2 s_rk[(1u << (2 * kDenseMaxW)) / 32];
+// each).  A per-32-key bucket index {presence bits, escape bits, first oct} (16 B per group,
+// 32 KiB at W=8) is staged in LDS.  Every lane takes its own 32 windows in four static
+// batches of eight: for each seed window of a batch the index gives the bucket's oct (the
+// 16-bit filter words of up to eight records, primer-1 bases W..W+F-1 each), all eight oct
+// loads are issued together, then each word is tested against the window's bases W..W+F-1
+// from the lane's own registers -- two words per 32-bit XOR / mismatch-mask / popcount.
+// Only words that pass (and "always" words) reach the full 32-B Entry test (fp_reject,
+// exact); buckets of more than eight records (escape bit) are walked through binfo.  One
+// L2 request per seed window, no seed queue, no shuffles, no per-seed loop.
+constexpr int kDenseBlock = kBlock;
+constexpr int kDenseWaves = kDenseBlock / 64;
+
+// Full test of filter-passing slots: bit 8t+j of pm (window t of the batch base tb, slot j
+// of its oct oi[t]) -> fp_reject on the Entry, survivors appended.
+__device__ __forceinline__ void dense_full_tests(const ScanArgs& a, uint64_t pm, const uint32_t (&oi)[8],
+                                                 uint32_t tb, uint32_t pb, uint64_t w0, uint64_t w1, uint64_t iv,
+                                                 uint64_t sbase, uint32_t n, bool owned, uint32_t seq, int lane,
+                                                 SurvChunk& C) {
+    const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
+    while (__any(pm != 0)) {
+        bool surv = false, exact = false;
+        uint32_t k = 0, rec = 0;
+        if (pm) {
+            const uint32_t bit = (uint32_t)__builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint32_t t = bit >> 3, j = bit & 7u;
+            uint32_t o = oi[0];
+#pragma unroll
+            for (int q = 1; q < 8; ++q) o = t == (uint32_t)q ? oi[q] : o;
+            const Entry e = a.dents_pad[(uint64_t)o * kDenseOct + j];
+            const uint32_t wi = tb + t;  // window offset in the lane's 32
+            const uint32_t pos = pb + wi;
+            k = pos - e.hash_off;
+            rec = e.rec;
+            bool act = pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
+            if (!owned) act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
+            if (act) {
+                uint64_t Gk = wi ? (w0 << (2 * wi)) | (w1 >> (64 - 2 * wi)) : w0;
+                uint32_t xk = (uint32_t)((iv << wi) >> 32);
+                if (a.has_u || e.hash_off) {  // U in the genome, or a record seeded inside its primer
+                    Gk = ext2(a.g2, sbase + k);
+                    xk = (uint32_t)(ext1(exc, sbase + k) >> 32);
+                }
+                surv = !fp_reject(a, Gk, xk, e.l1, e.code, e.pmask, exact);
+            }
+        }
+        const uint64_t gk = sbase + k;
+        append_chunked(&a.counters[2], a.surv, a.surv_cap, surv,
+                       make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec | (exact ? 0x80000000u : 0u), seq), lane,
+                       C);
+    }
+}
+
+__global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
+    extern __shared__ uint4 s_grp[];
     const uint32_t W = (uint32_t)a.W;
-    const uint32_t nrk = max(1u, (1u << (2 * W)) / 32);
-    for (uint32_t i = threadIdx.x; i < nrk; i += kBlock) s_rk[i] = a.rk[i];
+    const uint32_t ngrp = max(1u, (1u << (2 * W)) / 32);
+    for (uint32_t i = threadIdx.x; i < ngrp; i += kDenseBlock) s_grp[i] = a.dgrp[i];
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+    const uint64_t stride = (uint64_t)gridDim.x * kDenseWaves;
     const uint64_t n_supers = a.spans[a.n_spans].super0;
     const uint32_t shw = 32u - 2u * W;
-    const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
-    // the last X positions of a primer are 3'-protected (engine.py:605-611): the lowest
-    // min(X, 32) 2-bit slots of a right-aligned difference word
-    const uint64_t protx = a.X >= 32 ? ~0ull : ((1ull << (2 * a.X)) - 1ull);
+    const uint32_t fmask = a.dense_M;
+    const uint32_t N = (uint32_t)a.N;
+    const uint4* __restrict__ octs = reinterpret_cast<const uint4*>(a.dfilt);
     uint32_t ncand = 0;
     SurvChunk C{0, 64u, 0u};
 
-    uint64_t ss = (uint64_t)blockIdx.x * kWaves + (uint64_t)w;
+    uint64_t ss = (uint64_t)blockIdx.x * kDenseWaves + (uint64_t)w;
     SeqSpan pf{};
     pf.super0 = 1;
     uint64_t pf_end = 0, pf_sbase = 0;
@@ -1030,125 +1075,104 @@ __global__ __launch_bounds__(kBlock) void dense_kernel(ScanArgs a) {
         const uint32_t d0 = (uint32_t)(w0 >> 32), d1 = (uint32_t)w0, d2 = (uint32_t)(w1 >> 32);
         const uint32_t okm = window_ok_mask(iv, W) &
                              bit_range((int)sp.p_lo - (int)pb, (int)min<int64_t>((int64_t)sp.p_hi - pb, 32));
-        uint32_t seeds = 0;
-        [&]<int... T>(std::integer_sequence<int, T...>) {
-            ((
-                [&] {
-                    const uint32_t h = kmer_top<T>(d0, d1, d2) >> shw;
-                    seeds |= __builtin_amdgcn_ubfe(s_rk[h >> 5].x, h & 31u, 1u) << (31 - T);
-                }()),
-             ...);
-        }(std::make_integer_sequence<int, 32>{});
-        seeds &= okm;
+        // I=1: a window with a non-A/C/G/T/U base among its first 16 sends all its records
+        // to the full test (a genome IUPAC base may match where the 2-bit compare says
+        // otherwise; under I=0 such a base reads as 'A' and can only hide a mismatch, and U
+        // compares as T under I=1)
+        const uint32_t slowm = a.I ? ~window_ok_mask(iv, 16u) : 0u;
         const uint64_t nx = ss + stride;
         if (nx < n_supers) {  // next super-step's words, in flight during this one
             locate(nx);
             words(nx, nw0, nw1, niv);
         }
-        // lane-serial walk over the lane's seed buckets, four records per iteration; the
-        // next seed's bucket info is loaded while the current bucket is tested
-        uint32_t m = seeds;
-        uint32_t ni = 0, cur = 0, end = 0, pos = 0, h = 0, ex = 0;
-        uint2 nbi = make_uint2(0, 0);
-        bool have_n = false, seed_slow = false;
-        uint64_t G = 0, Gt = 0;
-        auto fetch = [&]() {  // rank of the next seed window and its bucket {first, count}
-            ni = (uint32_t)__clz(m);
-            m &= ~(0x80000000u >> ni);
-            const uint64_t Gi = ni ? (w0 << (2 * ni)) | (w1 >> (64 - 2 * ni)) : w0;
-            const uint32_t hi_ = (uint32_t)(Gi >> (64 - 2 * W));
-            const uint2 rw = s_rk[hi_ >> 5];
-            nbi = a.binfo[rw.y + (uint32_t)__popc(rw.x & ((1u << (hi_ & 31u)) - 1u))];
-            have_n = true;
-        };
-        if (m) fetch();
-        while (__any(have_n || cur < end)) {
-            if (cur >= end && have_n) {  // start the next bucket, fetch the one after
-                G = ni ? (w0 << (2 * ni)) | (w1 >> (64 - 2 * ni)) : w0;
-                Gt = G << (2 * W);       // window bases W..31, aligned with the entries' tails
-                h = (uint32_t)(G >> (64 - 2 * W));
-                pos = pb + ni;
-                ex = (uint32_t)((iv << ni) >> 32);
-                if (a.has_u) ex = (uint32_t)(ext1(a.gexc, sbase + pos) >> 32);
-                seed_slow = ex != 0;     // an exception base in the window: full test path
-                cur = nbi.x;
-                end = nbi.x + nbi.y;
-                have_n = false;
-                if (m) fetch();
-            }
-            uint4 c16[kDS];
+        uint32_t escm = 0;
+#pragma unroll 1
+        for (uint32_t TB = 0; TB < 32; TB += 8) {  // four batches of eight windows
+            // window t's 16-base funnel: bases t..t+15 of the lane, from (d0, d1) for t < 16
+            const uint32_t dh = TB < 16 ? d0 : d1, dl = TB < 16 ? d1 : d2;
+            uint32_t oi[8], key[8];
+            uint4 q[8];
+            uint32_t live = 0;
 #pragma unroll
-            for (int j = 0; j < kDS; ++j) {
-#if MP_ABLATE == 11
-                c16[j] = make_uint4(cur * 2654435761u + j, cur ^ 0x5bd1e995u, (cur & 0xFFFFu) | (10u << kHead8RecBits), 0u);
-#else
-                c16[j] = a.ents16[cur + j < end ? cur + j : 0u];
-#endif
+            for (int T = 0; T < 8; ++T) {
+                const uint32_t r = 2u * ((TB + (uint32_t)T) & 15u);
+                key[T] = r ? __builtin_amdgcn_alignbit(dh, dl, 32u - r) : dh;
+                const uint32_t h = key[T] >> shw;
+                const uint4 L = s_grp[h >> 5];
+                const uint32_t bq = h & 31u;
+                const uint32_t below = (1u << bq) - 1u;
+                const uint32_t wb = 31u - (TB + (uint32_t)T);
+                const bool seed = ((L.x >> bq) & 1u) && ((okm >> wb) & 1u);
+                const bool esc = (L.y >> bq) & 1u;
+                escm |= (uint32_t)(seed && esc) << wb;
+                const bool inl = seed && !esc;
+                live |= (uint32_t)inl << T;
+                oi[T] = L.z + (uint32_t)__popc(L.x & ~L.y & below);
+                q[T] = octs[inl ? oi[T] : 0u];
             }
-            // fast tests of the four slots (plain primers seeded at their start; bases [0, W)
-            // matched exactly, mismatches over bases W..l1-1 by one 2-bit XOR/popcount with
-            // the primer's last base in the lowest slot, so the 3'-protected positions are the
-            // lowest X slots), then one branch for any slot needing the full test and one for
-            // any survivor
-            bool slow[kDS], surv[kDS];
-            uint32_t slowm = 0, survm = 0;
+            uint64_t pm = 0;
 #pragma unroll
-            for (int j = 0; j < kDS; ++j) {
-                const bool valid = cur + j < end;
-                const uint32_t y = c16[j].z;
-                slow[j] = valid && ((y & kDense16Full) || seed_slow);
-                const uint32_t L = (y >> kHead8RecBits) & 31u;
-                bool act = valid && !slow[j] && pos + W + L <= n;
-                if (!owned) act = act && sbase + pos >= a.g_lo && sbase + pos < a.g_hi;
-                const uint64_t y2 = ((Gt ^ (((uint64_t)c16[j].y << 32) | c16[j].x)) >> (63 - 2 * L)) >> 1;
-                const uint64_t dm = (y2 | (y2 >> 1)) & kEven;
-                surv[j] = act && !(dm & protx) && __popcll(dm) <= a.N;
-                ncand += act;
-                slowm |= (uint32_t)slow[j] << j;
-                survm |= (uint32_t)surv[j] << j;
+            for (int T = 0; T < 8; ++T) {
+                // window bases W..W+F-1 (F <= 7, W + F <= 16: inside the window's funnel),
+                // in both 16-bit halves
+                const uint32_t gwin = (key[T] << (2 * W)) >> 16;
+                const uint32_t gg = gwin | (gwin << 16);
+                const bool lv = (live >> T) & 1u;
+                const bool sl = (slowm >> (31u - (TB + (uint32_t)T))) & 1u;
+                const uint32_t wv[4] = {q[T].x, q[T].y, q[T].z, q[T].w};
+                uint32_t pbits = 0, pads = 0;
+#pragma unroll
+                for (int h2 = 0; h2 < 4; ++h2) {
+                    const uint32_t x = gg ^ wv[h2];
+                    const uint32_t d = (x | (x >> 1)) & fmask;
+                    const bool p0 = (uint32_t)__popc(d & 0xFFFFu) <= N || (wv[h2] & kDenseAlways);
+                    const bool p1 = (uint32_t)__popc(d >> 16) <= N || ((wv[h2] >> 16) & kDenseAlways);
+                    const uint32_t pad0 = (wv[h2] >> 1) & 1u, pad1 = (wv[h2] >> 17) & 1u;
+                    pbits |= ((uint32_t)((p0 || sl) && !pad0) << (2 * h2)) |
+                             ((uint32_t)((p1 || sl) && !pad1) << (2 * h2 + 1));
+                    pads += pad0 + pad1;
+                }
+                pm |= (uint64_t)(lv ? pbits : 0u) << (8 * T);
+                ncand += lv ? 8u - pads : 0u;
             }
-            uint32_t rec[kDS], kk[kDS];
-            bool exact[kDS];
-#pragma unroll
-            for (int j = 0; j < kDS; ++j) {
-                rec[j] = c16[j].z & ((1u << kHead8RecBits) - 1u);
-                kk[j] = pos;
-                exact[j] = true;
+            if (__any(pm != 0)) dense_full_tests(a, pm, oi, TB, pb, w0, w1, iv, sbase, n, owned, sp.seq, lane, C);
+        }
+        // buckets of more than eight records (rare): walked oct by oct through binfo
+        while (__any(escm != 0)) {
+            uint32_t wi = 0, first = 0, cnt = 0;
+            if (escm) {
+                wi = (uint32_t)__clz(escm);
+                escm &= ~(0x80000000u >> wi);
+                const uint32_t h = (uint32_t)((wi ? (w0 << (2 * wi)) | (w1 >> (64 - 2 * wi)) : w0) >> (64 - 2 * W));
+                const uint2 rw = a.rk[h >> 5];
+                const uint2 bi = a.binfo[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
+                first = bi.x;
+                cnt = bi.y;
             }
-            if (__any(slowm != 0)) {  // rare: full Entry through the general test
+            const bool sl = (slowm >> (31 - wi)) & 1u;
+            const uint32_t tb = wi;  // full tests index windows from tb: one window per pass
+            for (uint32_t c0 = 0; __any(c0 < cnt); c0 += kDenseOct) {
+                uint32_t oi[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                uint64_t pm = 0;
+                if (c0 < cnt) {
+                    oi[0] = (first + c0) / kDenseOct;
+                    const uint4 qq = octs[oi[0]];
+                    const uint32_t gwin = (uint32_t)(((wi ? (w0 << (2 * wi)) | (w1 >> (64 - 2 * wi)) : w0) << (2 * W)) >> 48);
+                    const uint32_t gg = gwin | (gwin << 16);
+                    const uint32_t wv[4] = {qq.x, qq.y, qq.z, qq.w};
 #pragma unroll
-                for (int j = 0; j < kDS; ++j) {
-                    if (!slow[j]) continue;
-                    const Entry e = a.ents[cur + j];
-                    kk[j] = pos - e.hash_off;
-                    rec[j] = e.rec;
-                    bool act2 = pos >= e.hash_off && (uint64_t)kk[j] + e.l1 <= n;
-                    if (!owned) act2 = act2 && sbase + kk[j] >= a.g_lo && sbase + kk[j] < a.g_hi;
-                    surv[j] = false;
-                    if (act2) {
-                        ++ncand;
-                        uint64_t Gk = G;
-                        uint32_t xk = ex;
-                        if (e.hash_off) {  // window of a record seeded inside its primer
-                            Gk = ext2(a.g2, sbase + kk[j]);
-                            xk = (uint32_t)(ext1(exc, sbase + kk[j]) >> 32);
-                        }
-                        surv[j] = !fp_reject(a, Gk, xk, e.l1, e.code, e.pmask, exact[j]);
+                    for (int h2 = 0; h2 < 4; ++h2) {
+                        const uint32_t x = gg ^ wv[h2];
+                        const uint32_t d = (x | (x >> 1)) & fmask;
+                        const bool p0 = (uint32_t)__popc(d & 0xFFFFu) <= N || (wv[h2] & kDenseAlways);
+                        const bool p1 = (uint32_t)__popc(d >> 16) <= N || ((wv[h2] >> 16) & kDenseAlways);
+                        const uint32_t pad0 = (wv[h2] >> 1) & 1u, pad1 = (wv[h2] >> 17) & 1u;
+                        pm |= ((uint64_t)((p0 || sl) && !pad0) << (2 * h2)) | ((uint64_t)((p1 || sl) && !pad1) << (2 * h2 + 1));
+                        ncand += (1u - pad0) + (1u - pad1);
                     }
-                    survm = (survm & ~(1u << j)) | ((uint32_t)surv[j] << j);
                 }
+                if (__any(pm != 0)) dense_full_tests(a, pm, oi, tb, pb, w0, w1, iv, sbase, n, owned, sp.seq, lane, C);
             }
-            if (__any(survm != 0)) {
-#pragma unroll
-                for (int j = 0; j < kDS; ++j) {
-                    const uint64_t gk = sbase + kk[j];
-                    append_chunked(&a.counters[2], a.surv, a.surv_cap, surv[j],
-                                   make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec[j] | (exact[j] ? 0x80000000u : 0u),
-                                              sp.seq),
-                                   lane, C);
-                }
-            }
-            cur = min(cur + (uint32_t)kDS, end);
         }
         ss = nx;
     }
@@ -1467,7 +1491,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.has_u = g->has_u ? 1 : 0;
     a.seq_base = g->d_base; a.seq_len = g->d_len;
     a.spans = s->spans; a.n_spans = n_real_spans;
-    a.binfo = t->binfo; a.ents16 = t->ents16;
+    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
@@ -1503,7 +1527,14 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 48, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
         if (dense) {
-            hipLaunchKernelGGL(dense_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+            const size_t lds = sizeof(uint4) * std::max<size_t>(1, ((size_t)1 << (2 * t->prm.wordsize)) / 32);
+            int per_cu = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_kernel, kDenseBlock, lds) != hipSuccess ||
+                per_cu < 1)
+                per_cu = 1;
+            const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
+                                                                (uint64_t)s->n_cu * (uint64_t)per_cu);
+            hipLaunchKernelGGL(dense_kernel, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
         } else if (inl) {
             if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
             else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true>), dim3(grid), dim3(kBlock), 0, st, a);

@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->binfo); hipFree(t->ents16); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -233,7 +233,9 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         std::vector<uint2> rk;
         std::vector<Entry> dents;
         std::vector<uint2> binfo;
-        std::vector<uint4> ents16;
+        std::vector<uint16_t> dfilt;
+        std::vector<Entry> dents_pad;
+        std::vector<uint4> dgrp;
         std::vector<uint2> dents8;
         std::vector<Slot> slots;
         if (t->filt_direct) {
@@ -247,19 +249,74 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             }
             dents.resize(std::max<uint32_t>(nb, 1));
             dents8.resize(std::max<uint32_t>(nb, 1));
+            std::vector<uint32_t> qfirst;
             if (W <= kDenseMaxW) {
+                // plain run after the seed of every record seeded at its primer start
+                auto plain_run = [&](const Entry& e) -> uint32_t {
+                    if (e.hash_off != 0 || e.l1 < W) return 0;
+                    uint32_t r = 0;
+                    while (W + r < std::min<uint32_t>(e.l1, 32) && r < kDenseMaxF &&
+                           ((e.pmask >> (62 - 2 * (W + r))) & 3ull) == 1ull)
+                        ++r;
+                    return r;
+                };
+                // F: the longest filter that at least 95% of the records can carry
+                std::vector<uint32_t> hist(kDenseMaxF + 1, 0);
+                for (uint32_t i = 0; i < n_rec; ++i) ++hist[plain_run(ents[i])];
+                uint32_t F = 0, atleast = 0;
+                for (int f = (int)kDenseMaxF; f >= 1; --f) {
+                    atleast += hist[f];
+                    if ((uint64_t)atleast * 20 >= (uint64_t)n_rec * 19) { F = (uint32_t)f; break; }
+                }
+                t->dense_F = F;
+                // mismatch mask of the bases, both 16-bit halves of a word pair
+                const uint32_t m16 = F ? (0x5555u & ~(0xFFFFu >> (2 * F))) : 0u;
+                t->dense_M = m16 | (m16 << 16);
                 binfo.resize(std::max<uint32_t>(nb, 1), make_uint2(0, 0));
-                ents16.resize(std::max<uint32_t>(n_rec, 1), make_uint4(0, 0, kDense16Full, 0));
-                for (uint32_t i = 0; i < n_rec; ++i) {
-                    const Entry& e = ents[i];
-                    const uint64_t plain_all = e.l1 >= 32 ? 0x5555555555555555ull
-                                                          : (e.l1 ? (0x5555555555555555ull & (~0ull << (64 - 2 * e.l1))) : 0ull);
-                    const bool fast = e.hash_off == 0 && e.l1 >= W && e.l1 <= 32 && e.pmask == plain_all &&
-                                      e.rec < (1u << kHead8RecBits);
-                    if (!fast) continue;
-                    const uint64_t tail = e.code << (2 * W);  // bases W..31, top-aligned
-                    ents16[i] = make_uint4((uint32_t)tail, (uint32_t)(tail >> 32),
-                                           e.rec | ((uint32_t)(e.l1 - W) << kHead8RecBits), 0u);
+                qfirst.resize(nb);
+                // padded layout in key order, group by group: buckets of up to kDenseOct
+                // records take one oct (16 B of filter words), indexed inside the group by the
+                // popcount of the group's inline keys below; longer buckets are stored after
+                // every group and found through binfo (escape bit)
+                const uint32_t nkeys = 1u << (2 * W);
+                const uint32_t ngrp = std::max<uint32_t>(1, nkeys / 32);
+                std::vector<uint32_t> by_key(nkeys, 0xFFFFFFFFu);
+                for (uint32_t b = 0; b < nb; ++b) by_key[bkey[b]] = b;
+                dgrp.assign(ngrp, make_uint4(0, 0, 0, 0));
+                uint64_t np = 0;  // padded slots
+                for (uint32_t g = 0; g < ngrp; ++g) {
+                    dgrp[g].z = (uint32_t)(np / kDenseOct);
+                    for (uint32_t j = 0; j < 32 && g * 32 + j < nkeys; ++j) {
+                        const uint32_t b = by_key[g * 32 + j];
+                        if (b == 0xFFFFFFFFu) continue;
+                        dgrp[g].x |= 1u << j;
+                        if (bcount[b] > kDenseOct) {
+                            dgrp[g].y |= 1u << j;
+                            continue;
+                        }
+                        qfirst[b] = (uint32_t)np;
+                        np += kDenseOct;
+                    }
+                }
+                for (uint32_t k = 0; k < nkeys; ++k) {
+                    const uint32_t b = by_key[k];
+                    if (b == 0xFFFFFFFFu || bcount[b] <= kDenseOct) continue;
+                    qfirst[b] = (uint32_t)np;
+                    np += (bcount[b] + kDenseOct - 1) / kDenseOct * kDenseOct;
+                }
+                if (np / kDenseOct >= 0xFFFFFFF0ull) { rc = fail(MP_E_ARG, "seed table too large"); break; }
+                dfilt.assign(std::max<uint64_t>(np, kDenseOct), kDensePad);
+                Entry zero{};
+                dents_pad.assign(std::max<uint64_t>(np, kDenseOct), zero);
+                for (uint32_t b = 0; b < nb; ++b) {
+                    for (uint32_t j = 0; j < bcount[b]; ++j) {
+                        const Entry& e = ents[boff[b] + j];
+                        const uint32_t q = qfirst[b] + j;
+                        dents_pad[q] = e;
+                        dfilt[q] = (F && plain_run(e) >= F)
+                                       ? (uint16_t)(((e.code << (2 * W)) >> 48) & ~(0xFFFFu >> (2 * F)))
+                                       : (uint16_t)kDenseAlways;
+                    }
                 }
             }
             for (uint32_t b = 0; b < nb; ++b) {
@@ -268,7 +325,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 const Entry& e = ents[boff[b]];
                 dents[rank] = e;
                 dents8[rank] = e.count == 1 ? entry8(e) : make_uint2(0u, kHead8Full);
-                if (W <= kDenseMaxW) binfo[rank] = make_uint2(boff[b], bcount[b]);
+                if (W <= kDenseMaxW) binfo[rank] = make_uint2(qfirst[b], bcount[b]);
             }
             filt.assign(1, 0);
         } else {
@@ -303,7 +360,9 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->dents, dents.data(), dents.size(), &bytes))) break;
         if ((rc = upload(&t->dents8, dents8.data(), dents8.size(), &bytes))) break;
         if ((rc = upload(&t->binfo, binfo.data(), binfo.size(), &bytes))) break;
-        if ((rc = upload(&t->ents16, ents16.data(), ents16.size(), &bytes))) break;
+        if ((rc = upload(&t->dfilt, dfilt.data(), dfilt.size(), &bytes))) break;
+        if ((rc = upload(&t->dgrp, dgrp.data(), dgrp.size(), &bytes))) break;
+        if ((rc = upload(&t->dents_pad, dents_pad.data(), dents_pad.size(), &bytes))) break;
         if ((rc = upload(&t->ents, ents.data(), ents.size(), &bytes))) break;
         if ((rc = upload(&t->recs, recs.data(), recs.size(), &bytes))) break;
         if ((rc = upload(&t->rank, rank.data(), rank.size(), &bytes))) break;
