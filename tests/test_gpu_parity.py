@@ -252,3 +252,62 @@ def test_dense_tables_vs_c_oracle(tails, W, n_sts, glen, N, I, iupac, monkeypatc
     ref = C.search(table, [g], O.params(**prm), 8)
     assert len(ref) > 100
     assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize("W,I,N,X", [(6, 0, 1, 1), (7, 1, 2, 0), (8, 0, 0, 3), (8, 1, 1, 1), (9, 1, 1, 2)])
+def test_dense_filter_edge_cases(W, I, N, X):
+    """dense_kernel's filter and bucket index against the C oracle: keys shared by up to
+    60 records (escape buckets walked through binfo), records the filter cannot carry
+    (IUPAC bases after the seed, seed inside the primer, primers shorter than W + 7),
+    genome IUPAC characters and U (passed straight to search), protected 3' bases."""
+    from oracle import c_oracle as C
+    rng = np.random.default_rng(100 + W * 10 + I)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+    def rnd(n):
+        return acgt[rng.integers(0, 4, n)].tobytes().decode()
+
+    lines = []
+    prefixes = [rnd(W) for _ in range(6)]
+    for i in range(900):
+        l1, l2 = int(rng.integers(18, 26)), int(rng.integers(18, 26))
+        p1, p2 = rnd(l1), rnd(l2)
+        kind = i % 9
+        if kind in (0, 1):                 # shared seed keys: large buckets
+            p1 = prefixes[i % 6] + p1[W:]
+        elif kind == 2:                    # IUPAC base after the seed
+            j = W + int(rng.integers(0, 7))
+            p1 = p1[:j] + "RYKMSWN"[i % 7] + p1[j + 1:]
+        elif kind == 3:                    # seed inside the primer
+            p1 = "N" + p1[1:]
+        elif kind == 4:                    # too short to carry the filter
+            p1 = p1[:W + int(rng.integers(0, 5))]
+        lines.append(f"S{i}\t{p1}\t{p2}\t{int(rng.integers(80, 300))}\n")
+    sts_text = "".join(lines)
+    table = O.load_sts_lines(sts_text.splitlines(True), W, 240)
+    glen = 600_000
+    g = acgt[rng.integers(0, 4, glen)].copy()
+    # plant amplicons of the STS (both orientations), some with a mismatch
+    for i in range(0, 900, 2):
+        _, p1, p2, size = lines[i].rstrip("\n").split("\t")[:4]
+        a = p1.replace("N", "A")
+        b = O.revcomp(p1)
+        for x, y in ((a, p2), (p2, b)):
+            x = "".join(c if c in "ACGT" else "G" for c in x)
+            y = "".join(c if c in "ACGT" else "C" for c in y)
+            amp = (x + rnd(max(int(size) - len(x) - len(y), 0)) + y).encode()
+            st = int(rng.integers(0, glen - len(amp)))
+            g[st:st + len(amp)] = np.frombuffer(amp, dtype=np.uint8)
+    # genome IUPAC characters and U
+    for c, frac in ((b"N", 0.004), (b"R", 0.002), (b"Y", 0.002), (b"W", 0.001), (b"U", 0.002)):
+        idx = rng.integers(0, glen, int(glen * frac))
+        g[idx] = c[0]
+    prm = dict(wordsize=W, mismatches=N, iupac_mode=I, margin=50, three_prime_match=X)
+    eng = MerPCR(**prm)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    seq = g.tobytes().decode("ascii")
+    hits = eng.find_hits([FASTARecord(defline=">chrE", sequence=seq)])
+    ref = C.search(table, [g], O.params(**prm), 8)
+    assert len(ref) > 50
+    assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes()
