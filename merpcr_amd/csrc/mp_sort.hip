@@ -6,6 +6,8 @@
 // order is the lexicographic order (sequence, k, hash_offset, record, try rank)
 // -- SURVEY 8a-8.  Hits carry it as a 128-bit key (hi = global k coordinate,
 // lo = rank(record) << 32 | try rank) and two stable LSD passes order them.
+#include <algorithm>
+
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "mp_internal.h"
@@ -28,12 +30,48 @@ static int ensure_tmp(void** p, size_t* have, size_t need) {
     return MP_OK;
 }
 
+// (k, record rank, try rank) in one 64-bit key, most significant first.
+__global__ void pack_keys(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
+                          unsigned try_bits, unsigned low_bits, uint64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t l = lo[i];
+    out[i] = (hi[i] << low_bits) | ((l >> 32) << try_bits) | (l & 0xFFFFFFFFull);
+}
+
+__global__ void unpack_keys(const uint64_t* __restrict__ key, uint64_t n, unsigned try_bits, unsigned low_bits,
+                            uint64_t* __restrict__ hi, uint64_t* __restrict__ lo) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = key[i];
+    hi[i] = k >> low_bits;
+    lo[i] = (((k & ((1ull << low_bits) - 1ull)) >> try_bits) << 32) | (k & ((1ull << try_bits) - 1ull));
+}
+
 int sort_hits(Search* s, uint64_t n, hipStream_t st) {
     if (n < 2) return MP_OK;
     uint64_t* hi = s->keys;
     uint64_t* lo = s->keys + s->cap;
     const unsigned lo_bits = 32 + s->table->rank_bits;
     const unsigned hi_bits = bits_for(s->genome->total);
+    // try ranks are <= 2M (engine.py:540-560: d in [-M, M])
+    const unsigned try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
+    const unsigned low_bits = s->table->rank_bits + try_bits;
+    if (hi_bits + low_bits <= 64) {
+        // the whole order key fits 64 bits: one keys-only radix sort
+        const unsigned blocks = (unsigned)((n + 255) / 256);
+        hipLaunchKernelGGL(pack_keys, dim3(blocks), dim3(256), 0, st, hi, lo, n, try_bits, low_bits, s->tmp_lo);
+        MP_HIP_CHECK(hipGetLastError());
+        size_t need = 0;
+        MP_HIP_CHECK(rocprim::radix_sort_keys(nullptr, need, s->tmp_lo, s->tmp_hi, (size_t)n, 0, hi_bits + low_bits, st));
+        int rc = ensure_tmp(&s->sort_tmp, &s->sort_tmp_bytes, need);
+        if (rc) return rc;
+        size_t b = s->sort_tmp_bytes;
+        MP_HIP_CHECK(rocprim::radix_sort_keys(s->sort_tmp, b, s->tmp_lo, s->tmp_hi, (size_t)n, 0, hi_bits + low_bits, st));
+        hipLaunchKernelGGL(unpack_keys, dim3(blocks), dim3(256), 0, st, s->tmp_hi, n, try_bits, low_bits, hi, lo);
+        MP_HIP_CHECK(hipGetLastError());
+        return MP_OK;
+    }
     size_t need1 = 0, need2 = 0;
     MP_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, need1, lo, s->tmp_lo, hi, s->tmp_hi, (size_t)n,
                                            0, lo_bits, st));
