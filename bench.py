@@ -292,7 +292,8 @@ def main():
                      "traffic": int(traffic) if traffic else None,
                      "traffic_source": f"profiles/{traffic_src}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, "
                                        "gfx950-corrected; includes Infinity-Cache hits)" if traffic else None,
-                     "kernel": "mp::scan_kernel", "alg_bytes_per_launch": int(alg_bytes)},
+                     "kernel": "mp::dense_kernel" if cfg["W"] <= 9 else "mp::scan_kernel",
+                     "alg_bytes_per_launch": int(alg_bytes)},
     }
     if args.shard_of > 1:
         out["diagnostic"] = f"rank 0 of a {args.shard_of}-way owned-range split, alone on one GPU (not the metric)"

@@ -7,6 +7,7 @@
 // -- SURVEY 8a-8.  Hits carry it as a 128-bit key (hi = global k coordinate,
 // lo = rank(record) << 32 | try rank) and two stable LSD passes order them.
 #include <algorithm>
+#include <cstdlib>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -57,7 +58,7 @@ int sort_hits(Search* s, uint64_t n, hipStream_t st) {
     // try ranks are <= 2M (engine.py:540-560: d in [-M, M])
     const unsigned try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
     const unsigned low_bits = s->table->rank_bits + try_bits;
-    if (hi_bits + low_bits <= 64) {
+    if (hi_bits + low_bits <= 64 && !std::getenv("MP_SORT2")) {  // MP_SORT2: tests of the two-pass path
         // the whole order key fits 64 bits: one keys-only radix sort
         const unsigned blocks = (unsigned)((n + 255) / 256);
         hipLaunchKernelGGL(pack_keys, dim3(blocks), dim3(256), 0, st, hi, lo, n, try_bits, low_bits, s->tmp_lo);

@@ -1,6 +1,7 @@
 """Copy a round's rocprofv3 summaries from gpurun_out/ into profiles/ and derive traffic.
 
-usage: python scripts/collect_profile.py <tag>   (reads gpurun_out/prof_<tag>)
+usage: python scripts/collect_profile.py <tag> [kernel]   (reads gpurun_out/prof_<tag>; kernel
+default scan_kernel)
 Writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_bench.json (the bench line printed
 under the trace pass) and profiles/<tag>_pmc.json (per-dispatch counter means for the scan
 kernel plus HBM traffic per launch, gfx950-corrected as MI355X_MICROARCH.md prescribes:
@@ -17,6 +18,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
+kern = sys.argv[2] if len(sys.argv) > 2 else "scan_kernel"
 src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
@@ -28,7 +30,7 @@ pmc = {}
 for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv"))):
     per = collections.defaultdict(float)  # (dispatch, counter) -> sum over instances
     for r in csv.DictReader(open(f)):
-        if "scan_kernel" in r["Kernel_Name"]:
+        if kern in r["Kernel_Name"]:
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     agg = collections.defaultdict(list)
     for (_, c), v in per.items():
@@ -37,9 +39,9 @@ for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv")))
         pmc[k] = sum(v) / len(v)
 trace_ns = None
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
-    if "scan_kernel" in r["Name"]:
+    if kern in r["Name"]:
         trace_ns = float(r["AverageNs"])
-out = {"kernel": "mp::scan_kernel", "avg_duration_ns_trace": trace_ns, "counters_mean_per_dispatch": pmc}
+out = {"kernel": "mp::" + kern, "avg_duration_ns_trace": trace_ns, "counters_mean_per_dispatch": pmc}
 if "FETCH_SIZE" in pmc:
     rd = 2 * pmc["FETCH_SIZE"] * 1024
     wr = pmc.get("WRITE_SIZE", 0.0) * 1024
