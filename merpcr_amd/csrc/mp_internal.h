@@ -120,7 +120,8 @@ struct Table {
     uint2* dents8 = nullptr;      // W <= 13: 8-B heads {primer-1 bases W..W+15, rec | (l1-W)<<26 | full<<31}
     uint2* binfo = nullptr;       // W <= kDenseMaxW: per key rank {first padded entry, records}
     uint16_t* dfilt = nullptr;    // W <= kDenseMaxW: 2-B filter word per padded entry (kDenseAlways...)
-    uint4* dgrp = nullptr;        // W <= kDenseMaxW: per 32 keys {bits, escape bits, first oct, 0}
+    uint2* dgrp = nullptr;        // W <= kDenseMaxW: per 32 keys {inline-bucket bits, first oct | any escape << 31}
+    uint32_t* dgesc = nullptr;    // W <= kDenseMaxW: per 32 keys, keys of more than kDenseOct records
     Entry* dents_pad = nullptr;   // W <= kDenseMaxW: ents with every bucket padded to a multiple of 4
     uint32_t dense_F = 0;         // bases after the seed the filter words hold
     uint32_t dense_M = 0;         // their mismatch mask in both halves of a 32-bit word pair

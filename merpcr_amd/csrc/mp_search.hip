@@ -78,7 +78,8 @@ struct ScanArgs {
     const uint2* dents8;    // W <= 13: 8-B heads
     const uint2* binfo;     // W <= kDenseMaxW: bucket {first padded entry, records} by key rank
     const uint16_t* dfilt;  // W <= kDenseMaxW: filter word per padded entry
-    const uint4* dgrp;      // W <= kDenseMaxW: per-32-key bucket index
+    const uint2* dgrp;      // W <= kDenseMaxW: per-32-key bucket index
+    const uint32_t* dgesc;  // W <= kDenseMaxW: per-32-key escape bits
     const Entry* dents_pad; // W <= kDenseMaxW: Entry per padded entry
     uint32_t dense_M;       // filter mismatch mask
     const uint32_t* lfilt;
@@ -961,8 +962,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 }
 
 // Dense seeds (W <= kDenseMaxW, e.g. W=8: ~95% of windows hit one of 62k keys, 3.2 records
-// each).  A per-32-key bucket index {presence bits, escape bits, first oct} (16 B per group,
-// 32 KiB at W=8) is staged in LDS.  Every lane takes its own 32 windows in four static
+// each).  A per-32-key bucket index {inline-bucket bits, first oct | any-escape flag} plus
+// the group's escape bits (12 B per group, 24 KiB at W=8) is staged in LDS.  Every lane takes its own 32 windows in four static
 // batches of eight: for each seed window of a batch the index gives the bucket's oct (the
 // 16-bit filter words of up to eight records, primer-1 bases W..W+F-1 each), all eight oct
 // loads are issued together, then each word is tested against the window's bases W..W+F-1
@@ -971,11 +972,15 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 // exact); buckets of more than eight records (escape bit) are walked through binfo.  One
 // L2 request per seed window, no seed queue, no shuffles, no per-seed loop.
 constexpr int kDenseBlock = kBlock;
+#ifndef MP_DENSE_BATCH
+#define MP_DENSE_BATCH 8
+#endif
+constexpr int kDB = MP_DENSE_BATCH;  // windows whose oct loads are in flight together
 constexpr int kDenseWaves = kDenseBlock / 64;
 
 // Full test of filter-passing slots: bit 8t+j of pm (window t of the batch base tb, slot j
 // of its oct oi[t]) -> fp_reject on the Entry, survivors appended.
-__device__ __forceinline__ void dense_full_tests(const ScanArgs& a, uint64_t pm, const uint32_t (&oi)[8],
+__device__ __forceinline__ void dense_full_tests(const ScanArgs& a, uint64_t pm, const uint2* s_grp, uint32_t ob,
                                                  uint32_t tb, uint32_t pb, uint64_t w0, uint64_t w1, uint64_t iv,
                                                  uint64_t sbase, uint32_t n, bool owned, uint32_t seq, int lane,
                                                  SurvChunk& C) {
@@ -987,11 +992,14 @@ __device__ __forceinline__ void dense_full_tests(const ScanArgs& a, uint64_t pm,
             const uint32_t bit = (uint32_t)__builtin_ctzll(pm);
             pm &= pm - 1;
             const uint32_t t = bit >> 3, j = bit & 7u;
-            uint32_t o = oi[0];
-#pragma unroll
-            for (int q = 1; q < 8; ++q) o = t == (uint32_t)q ? oi[q] : o;
-            const Entry e = a.dents_pad[(uint64_t)o * kDenseOct + j];
             const uint32_t wi = tb + t;  // window offset in the lane's 32
+            uint32_t o = ob;             // escape walk: the oct itself
+            if (s_grp) {                 // batch: the window's oct from the LDS index again
+                const uint32_t h = (uint32_t)((wi ? (w0 << (2 * wi)) | (w1 >> (64 - 2 * wi)) : w0) >> (64 - 2 * a.W));
+                const uint2 L = s_grp[h >> 5];
+                o = (L.y & 0x7FFFFFFFu) + (uint32_t)__popc(L.x & ((1u << (h & 31u)) - 1u));
+            }
+            const Entry e = a.dents_pad[(uint64_t)o * kDenseOct + j];
             const uint32_t pos = pb + wi;
             k = pos - e.hash_off;
             rec = e.rec;
@@ -1015,10 +1023,14 @@ __device__ __forceinline__ void dense_full_tests(const ScanArgs& a, uint64_t pm,
 }
 
 __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
-    extern __shared__ uint4 s_grp[];
+    extern __shared__ uint2 s_grp[];
     const uint32_t W = (uint32_t)a.W;
     const uint32_t ngrp = max(1u, (1u << (2 * W)) / 32);
-    for (uint32_t i = threadIdx.x; i < ngrp; i += kDenseBlock) s_grp[i] = a.dgrp[i];
+    uint32_t* s_esc = reinterpret_cast<uint32_t*>(s_grp + ngrp);
+    for (uint32_t i = threadIdx.x; i < ngrp; i += kDenseBlock) {
+        s_grp[i] = a.dgrp[i];
+        s_esc[i] = a.dgesc[i];
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -1087,35 +1099,33 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         }
         uint32_t escm = 0;
 #pragma unroll 1
-        for (uint32_t TB = 0; TB < 32; TB += 8) {  // four batches of eight windows
+        for (uint32_t TB = 0; TB < 32; TB += kDB) {  // batches of kDB windows
             // window t's 16-base funnel: bases t..t+15 of the lane, from (d0, d1) for t < 16
             const uint32_t dh = TB < 16 ? d0 : d1, dl = TB < 16 ? d1 : d2;
-            uint32_t oi[8], key[8];
-            uint4 q[8];
+            uint4 q[kDB];
             uint32_t live = 0;
 #pragma unroll
-            for (int T = 0; T < 8; ++T) {
+            for (int T = 0; T < kDB; ++T) {
                 const uint32_t r = 2u * ((TB + (uint32_t)T) & 15u);
-                key[T] = r ? __builtin_amdgcn_alignbit(dh, dl, 32u - r) : dh;
-                const uint32_t h = key[T] >> shw;
-                const uint4 L = s_grp[h >> 5];
+                const uint32_t h = (r ? __builtin_amdgcn_alignbit(dh, dl, 32u - r) : dh) >> shw;
+                const uint2 L = s_grp[h >> 5];
                 const uint32_t bq = h & 31u;
-                const uint32_t below = (1u << bq) - 1u;
                 const uint32_t wb = 31u - (TB + (uint32_t)T);
-                const bool seed = ((L.x >> bq) & 1u) && ((okm >> wb) & 1u);
-                const bool esc = (L.y >> bq) & 1u;
-                escm |= (uint32_t)(seed && esc) << wb;
-                const bool inl = seed && !esc;
+                const bool ok = (okm >> wb) & 1u;
+                const bool inl = ok && ((L.x >> bq) & 1u);
+                if ((int32_t)L.y < 0 && ok)  // the group holds a key of more than eight records
+                    escm |= ((s_esc[h >> 5] >> bq) & 1u) << wb;
                 live |= (uint32_t)inl << T;
-                oi[T] = L.z + (uint32_t)__popc(L.x & ~L.y & below);
-                q[T] = octs[inl ? oi[T] : 0u];
+                q[T] = octs[inl ? (L.y & 0x7FFFFFFFu) + (uint32_t)__popc(L.x & ((1u << bq) - 1u)) : 0u];
             }
             uint64_t pm = 0;
 #pragma unroll
-            for (int T = 0; T < 8; ++T) {
+            for (int T = 0; T < kDB; ++T) {
                 // window bases W..W+F-1 (F <= 7, W + F <= 16: inside the window's funnel),
                 // in both 16-bit halves
-                const uint32_t gwin = (key[T] << (2 * W)) >> 16;
+                const uint32_t r = 2u * ((TB + (uint32_t)T) & 15u);
+                const uint32_t key = r ? __builtin_amdgcn_alignbit(dh, dl, 32u - r) : dh;
+                const uint32_t gwin = (key << (2 * W)) >> 16;
                 const uint32_t gg = gwin | (gwin << 16);
                 const bool lv = (live >> T) & 1u;
                 const bool sl = (slowm >> (31u - (TB + (uint32_t)T))) & 1u;
@@ -1135,7 +1145,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
                 pm |= (uint64_t)(lv ? pbits : 0u) << (8 * T);
                 ncand += lv ? 8u - pads : 0u;
             }
-            if (__any(pm != 0)) dense_full_tests(a, pm, oi, TB, pb, w0, w1, iv, sbase, n, owned, sp.seq, lane, C);
+            if (__any(pm != 0)) dense_full_tests(a, pm, s_grp, 0u, TB, pb, w0, w1, iv, sbase, n, owned, sp.seq, lane, C);
         }
         // buckets of more than eight records (rare): walked oct by oct through binfo
         while (__any(escm != 0)) {
@@ -1152,11 +1162,11 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
             const bool sl = (slowm >> (31 - wi)) & 1u;
             const uint32_t tb = wi;  // full tests index windows from tb: one window per pass
             for (uint32_t c0 = 0; __any(c0 < cnt); c0 += kDenseOct) {
-                uint32_t oi[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                uint32_t ob = 0;
                 uint64_t pm = 0;
                 if (c0 < cnt) {
-                    oi[0] = (first + c0) / kDenseOct;
-                    const uint4 qq = octs[oi[0]];
+                    ob = (first + c0) / kDenseOct;
+                    const uint4 qq = octs[ob];
                     const uint32_t gwin = (uint32_t)(((wi ? (w0 << (2 * wi)) | (w1 >> (64 - 2 * wi)) : w0) << (2 * W)) >> 48);
                     const uint32_t gg = gwin | (gwin << 16);
                     const uint32_t wv[4] = {qq.x, qq.y, qq.z, qq.w};
@@ -1171,7 +1181,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
                         ncand += (1u - pad0) + (1u - pad1);
                     }
                 }
-                if (__any(pm != 0)) dense_full_tests(a, pm, oi, tb, pb, w0, w1, iv, sbase, n, owned, sp.seq, lane, C);
+                if (__any(pm != 0)) dense_full_tests(a, pm, nullptr, ob, tb, pb, w0, w1, iv, sbase, n, owned, sp.seq, lane, C);
             }
         }
         ss = nx;
@@ -1491,7 +1501,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.has_u = g->has_u ? 1 : 0;
     a.seq_base = g->d_base; a.seq_len = g->d_len;
     a.spans = s->spans; a.n_spans = n_real_spans;
-    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
+    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
@@ -1527,7 +1537,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 48, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
         if (dense) {
-            const size_t lds = sizeof(uint4) * std::max<size_t>(1, ((size_t)1 << (2 * t->prm.wordsize)) / 32);
+            const size_t lds = (sizeof(uint2) + sizeof(uint32_t)) * std::max<size_t>(1, ((size_t)1 << (2 * t->prm.wordsize)) / 32);
             int per_cu = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_kernel, kDenseBlock, lds) != hipSuccess ||
                 per_cu < 1)

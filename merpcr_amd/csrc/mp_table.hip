@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -235,7 +235,8 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         std::vector<uint2> binfo;
         std::vector<uint16_t> dfilt;
         std::vector<Entry> dents_pad;
-        std::vector<uint4> dgrp;
+        std::vector<uint2> dgrp;
+        std::vector<uint32_t> dgesc;
         std::vector<uint2> dents8;
         std::vector<Slot> slots;
         if (t->filt_direct) {
@@ -282,22 +283,26 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 const uint32_t ngrp = std::max<uint32_t>(1, nkeys / 32);
                 std::vector<uint32_t> by_key(nkeys, 0xFFFFFFFFu);
                 for (uint32_t b = 0; b < nb; ++b) by_key[bkey[b]] = b;
-                dgrp.assign(ngrp, make_uint4(0, 0, 0, 0));
+                dgrp.assign(ngrp, make_uint2(0, 0));
+                dgesc.assign(ngrp, 0u);
                 uint64_t np = 0;  // padded slots
                 for (uint32_t g = 0; g < ngrp; ++g) {
-                    dgrp[g].z = (uint32_t)(np / kDenseOct);
+                    if (np / kDenseOct >= 0x7FFFFFFFull) { rc = fail(MP_E_ARG, "seed table too large"); break; }
+                    dgrp[g].y = (uint32_t)(np / kDenseOct);
                     for (uint32_t j = 0; j < 32 && g * 32 + j < nkeys; ++j) {
                         const uint32_t b = by_key[g * 32 + j];
                         if (b == 0xFFFFFFFFu) continue;
-                        dgrp[g].x |= 1u << j;
                         if (bcount[b] > kDenseOct) {
-                            dgrp[g].y |= 1u << j;
+                            dgesc[g] |= 1u << j;
+                            dgrp[g].y |= 0x80000000u;
                             continue;
                         }
+                        dgrp[g].x |= 1u << j;
                         qfirst[b] = (uint32_t)np;
                         np += kDenseOct;
                     }
                 }
+                if (rc) break;
                 for (uint32_t k = 0; k < nkeys; ++k) {
                     const uint32_t b = by_key[k];
                     if (b == 0xFFFFFFFFu || bcount[b] <= kDenseOct) continue;
@@ -362,6 +367,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->binfo, binfo.data(), binfo.size(), &bytes))) break;
         if ((rc = upload(&t->dfilt, dfilt.data(), dfilt.size(), &bytes))) break;
         if ((rc = upload(&t->dgrp, dgrp.data(), dgrp.size(), &bytes))) break;
+        if ((rc = upload(&t->dgesc, dgesc.data(), dgesc.size(), &bytes))) break;
         if ((rc = upload(&t->dents_pad, dents_pad.data(), dents_pad.size(), &bytes))) break;
         if ((rc = upload(&t->ents, ents.data(), ents.size(), &bytes))) break;
         if ((rc = upload(&t->recs, recs.data(), recs.size(), &bytes))) break;
