@@ -457,9 +457,25 @@ __device__ __forceinline__ void wave_sync() { wave_sync_lds(); }
 // LDS left beside the 128 KiB prefilter (160 KiB per CU) holds 1008 per wave; a denser
 // super-step is drained in rounds.
 constexpr uint32_t kSeedQ = 1008;
+// kMode 1 with MP_RANKQ: the level-2 probe already read each seed's rank word, so the queue
+// carries the key rank beside the offset (6 B per seed) and the drain skips the rank word.
+constexpr uint32_t kSeedQR = 340;
 struct WaveLds {
-    uint16_t q[kSeedQ];
+    union {
+        uint16_t q[kSeedQ];
+        struct {
+            uint16_t q[kSeedQR];
+            uint32_t r[kSeedQR];
+        } rq;
+    };
 };
+static_assert(sizeof(WaveLds) <= 2048, "per-wave LDS beside the 128 KiB prefilter");
+#ifndef MP_RANKQ
+#define MP_RANKQ 1
+#endif
+#ifndef MP_L2SLOTS
+#define MP_L2SLOTS 12
+#endif
 
 // The current super-step as the wave holds it: lane L owns bases [base + 32L,
 // base + 32L + 64) as two 2-bit words and one ambiguity word.
@@ -729,6 +745,40 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
     }
 }
 
+// drain_seeds for the ranked queue (kMode 1, MP_RANKQ): the head comes straight from the
+// queued key rank -- one dependent load (the 8-B head) per seed instead of two.
+template <bool kInline>
+__device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
+                                             uint32_t qn, int lane, uint32_t& ncand, WaveLds& L,
+                                             SurvChunk& C, SurvChunk& TC) {
+    const uint32_t shw = 64u - 2u * (uint32_t)a.W;
+    for (uint32_t b = 0; b < qn; b += 128) {
+        const uint32_t ea = b + (uint32_t)lane, eb = ea + 64;
+        const bool la = ea < qn, lb = eb < qn;
+        const uint32_t pa = R.base + (la ? (uint32_t)L.rq.q[ea] : 0u);
+        const uint32_t pb = R.base + (lb ? (uint32_t)L.rq.q[eb] : 0u);
+        const uint32_t qa = la ? L.rq.r[ea] : 0u, qb = lb ? L.rq.r[eb] : 0u;
+        const uint2 ca = a.dents8[qa];
+        const uint2 cb = a.dents8[qb];
+        uint64_t Ga, Gb;
+        uint32_t xa, xb;
+        window_from_regs(a, R, sbase, pa, true, Ga, xa);
+        window_from_regs(a, R, sbase, pb, true, Gb, xb);
+        const uint32_t ha = (uint32_t)(Ga >> shw), hb = (uint32_t)(Gb >> shw);
+        Entry e0a{}, e0b{};
+        if (la) {
+            if (ca.y & kHead8Full) e0a = a.dents[qa];  // full entry: IUPAC/long primer or bucket tail
+            else e0a = head8_entry(ca, ha, (uint32_t)a.W);
+        }
+        if (lb) {
+            if (cb.y & kHead8Full) e0b = a.dents[qb];
+            else e0b = head8_entry(cb, hb, (uint32_t)a.W);
+        }
+        heads_and_tails<1, kInline>(a, R, sbase, n, la, pa, e0a, Ga, xa, lane, ncand, C, TC);
+        if (b + 64 < qn) heads_and_tails<1, kInline>(a, R, sbase, n, lb, pb, e0b, Gb, xb, lane, ncand, C, TC);
+    }
+}
+
 // Bit 31-i set iff window i (bases [i, i+W) of the lane's 64-base ambiguity window,
 // bit 63-j = base j is not A/C/G/T/U) is clean: every bad base is smeared over the W
 // windows that contain it (OR of bad << t, t < W, by binary decomposition of W).
@@ -840,6 +890,28 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
     }
 }
 
+// Level 1 only: the LDS prefilter bits of the lane's 32 windows (bit 31-T), kMode != 0.
+__device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds, uint32_t d0, uint32_t d1, uint32_t d2) {
+    uint32_t lmask = 0;
+    [&]<int... T>(std::integer_sequence<int, T...>) {
+        ((
+            [&] {
+                const uint32_t x = kmer_top<T>(d0, d1, d2);
+                lmask |= __builtin_amdgcn_ubfe(lds[x >> (37 - kLdsFilterLog2)], (x >> (32 - kLdsFilterLog2)) & 31u, 1u)
+                         << (31 - T);
+            }()),
+         ...);
+    }(std::make_integer_sequence<int, 32>{});
+    return lmask;
+}
+
+// 32-bit funnel of window i (0..31, run-time) of the lane: bases i..i+15, left-aligned.
+__device__ __forceinline__ uint32_t kmer_dyn(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t i) {
+    const uint32_t hi = i < 16 ? d0 : d1, lo = i < 16 ? d1 : d2;
+    const uint32_t r = 2u * (i & 15u);
+    return r ? __builtin_amdgcn_alignbit(hi, lo, 32u - r) : hi;
+}
+
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
 // ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
 // The next super-step's plane words are loaded before the current one is processed.
@@ -921,6 +993,65 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint32_t okm = window_ok_mask(R.iv, W) &
                              bit_range((int)sp.p_lo - (int)pb, (int)min<int64_t>((int64_t)sp.p_hi - pb, 32));
         const uint64_t nx = ss + stride;
+#if MP_RANKQ
+        if constexpr (kMode == 1) {
+            // level 2 compacted: the LDS-positive windows, MP_L2SLOTS per lane per pass, each
+            // one rank-word load; a seed's rank goes into the queue beside its offset
+            constexpr int K = MP_L2SLOTS;
+            uint32_t rem = lds_probe32(s_lf, d0, d1, d2) & okm;
+            bool first = true;
+            do {
+                uint32_t sb[K];
+                uint2 rw[K];
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    const bool on = rem != 0;
+                    const uint32_t i = on ? (uint32_t)__clz(rem) : 0u;
+                    rem = on ? rem & ~(0x80000000u >> i) : rem;
+                    const uint32_t h = kmer_dyn(d0, d1, d2, i) >> shw;
+                    sb[q] = on ? (i << 5) | (h & 31u) : 0xFFFFFFFFu;
+                    rw[q] = a.rk[on ? (h >> 5) : 0u];
+                }
+                if (first) {  // the next super-step's words, issued after this step's probes
+                    first = false;
+                    if (nx < n_supers) {
+                        locate(nx);
+                        words(nx, nw0, nw1, niv);
+                    }
+                }
+                uint32_t hs = 0;
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    hs |= (uint32_t)(sb[q] != 0xFFFFFFFFu && ((rw[q].x >> (sb[q] & 31u)) & 1u)) << q;
+                const uint32_t c = (uint32_t)__popc(hs);
+                const uint32_t incl = wave_incl_scan(c, lane);
+                const uint32_t total = rl32(incl, 63);
+#if MP_ABLATE == 1 || MP_ABLATE == 3
+                ncand += total;
+#else
+                for (uint32_t rb = 0; rb < total; rb += kSeedQR) {
+                    uint32_t qi = incl - c;
+#pragma unroll
+                    for (int q = 0; q < K; ++q) {
+                        if ((hs >> q) & 1u) {
+                            if (qi - rb < kSeedQR) {
+                                const uint32_t bq = sb[q] & 31u;
+                                L.rq.q[qi - rb] = (uint16_t)((uint32_t)lane * kLanePos + (sb[q] >> 5));
+                                L.rq.r[qi - rb] = rw[q].y + (uint32_t)__popc(rw[q].x & ((1u << bq) - 1u));
+                            }
+                            ++qi;
+                        }
+                    }
+                    wave_sync();
+                    drain_ranked<kInline>(a, R, sbase, n, min(total - rb, kSeedQR), lane, ncand, L, C, TC);
+                    wave_sync();
+                }
+#endif
+            } while (__any(rem != 0));
+            ss = nx;
+            continue;
+        }
+#endif
         uint32_t hits = probe32<kMode>(a, s_lf, d0, d1, d2, shw, okm, [&] {
             // prefetch the next super-step's words (issued after this step's probes)
             if (nx < n_supers) {

@@ -312,3 +312,29 @@ def test_dense_filter_edge_cases(W, I, N, X):
     ref = C.search(table, [g], O.params(**prm), 8)
     assert len(ref) > 50
     assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize("W", [11, 12])
+def test_seed_queue_rounds(W):
+    """Every window a seed (a periodic genome whose 11/12-mers are all keys): the scan
+    kernel's per-wave seed queue overflows and drains in rounds; against the C oracle."""
+    from oracle import c_oracle as C
+    rng = np.random.default_rng(W)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    unit = acgt[rng.integers(0, 4, 97)].tobytes().decode()
+    g = (unit * 260)[:25_000]
+    lines = []
+    for i in range(97):
+        s = (unit * 3)[i:]
+        p1, p2 = s[:20], s[150:170]
+        lines.append(f"P{i}\t{p1}\t{p2}\t{150 + 20 + int(rng.integers(-3, 4))}\n")
+    sts_text = "".join(lines)
+    prm = dict(wordsize=W, mismatches=1, margin=5)
+    eng = MerPCR(**prm)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    hits = eng.find_hits([FASTARecord(defline=">chrP", sequence=g)])
+    table = O.load_sts_lines(sts_text.splitlines(True), W, 240)
+    ref = C.search(table, [np.frombuffer(g.encode(), dtype=np.uint8)], O.params(**prm), 8)
+    assert len(ref) > 1000
+    assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes()
