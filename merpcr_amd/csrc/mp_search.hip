@@ -477,6 +477,7 @@ static_assert(sizeof(WaveLds) <= 2048, "per-wave LDS beside the 128 KiB prefilte
 #define MP_L2SLOTS 12
 #endif
 
+
 // The current super-step as the wave holds it: lane L owns bases [base + 32L,
 // base + 32L + 64) as two 2-bit words and one ambiguity word.
 struct SuperRegs {
@@ -997,9 +998,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         if constexpr (kMode == 1) {
             // level 2 compacted: the LDS-positive windows, MP_L2SLOTS per lane per pass, each
             // one rank-word load; a seed's rank goes into the queue beside its offset
+            // a lane with more than K positives takes further passes; their seeds join the
+            // same queue, drained once (in rounds only when it fills)
             constexpr int K = MP_L2SLOTS;
             uint32_t rem = lds_probe32(s_lf, d0, d1, d2) & okm;
             bool first = true;
+            uint32_t qfill = 0;  // queued seeds not yet drained (wave-uniform)
             do {
                 uint32_t sb[K];
                 uint2 rw[K];
@@ -1029,23 +1033,36 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 #if MP_ABLATE == 1 || MP_ABLATE == 3
                 ncand += total;
 #else
-                for (uint32_t rb = 0; rb < total; rb += kSeedQR) {
-                    uint32_t qi = incl - c;
+                // queue this pass's seeds; drain when the queue is full or after the last pass
+                const bool last = !__any(rem != 0);
+                uint32_t done = 0;  // this pass's seeds already queued
+                for (;;) {
+                    const uint32_t wr = min(kSeedQR - qfill, total - done);
+                    if (wr) {
+                        uint32_t qi = incl - c;  // this lane's first seed in the pass
 #pragma unroll
-                    for (int q = 0; q < K; ++q) {
-                        if ((hs >> q) & 1u) {
-                            if (qi - rb < kSeedQR) {
-                                const uint32_t bq = sb[q] & 31u;
-                                L.rq.q[qi - rb] = (uint16_t)((uint32_t)lane * kLanePos + (sb[q] >> 5));
-                                L.rq.r[qi - rb] = rw[q].y + (uint32_t)__popc(rw[q].x & ((1u << bq) - 1u));
+                        for (int q = 0; q < K; ++q) {
+                            if ((hs >> q) & 1u) {
+                                if (qi - done < wr) {
+                                    const uint32_t bq = sb[q] & 31u;
+                                    L.rq.q[qfill + qi - done] = (uint16_t)((uint32_t)lane * kLanePos + (sb[q] >> 5));
+                                    L.rq.r[qfill + qi - done] = rw[q].y + (uint32_t)__popc(rw[q].x & ((1u << bq) - 1u));
+                                }
+                                ++qi;
                             }
-                            ++qi;
                         }
+                        done += wr;
+                        qfill += wr;
                     }
-                    wave_sync();
-                    drain_ranked<kInline>(a, R, sbase, n, min(total - rb, kSeedQR), lane, ncand, L, C, TC);
-                    wave_sync();
+                    if (qfill == kSeedQR || (last && done == total && qfill)) {
+                        wave_sync();
+                        drain_ranked<kInline>(a, R, sbase, n, qfill, lane, ncand, L, C, TC);
+                        wave_sync();
+                        qfill = 0;
+                    }
+                    if (done == total) break;
                 }
+                rem = last ? 0u : rem;
 #endif
             } while (__any(rem != 0));
             ss = nx;
