@@ -103,6 +103,13 @@ struct ScanArgs {
     uint64_t tails_cap;
 };
 
+// 64-bit min/max as plain compares (HIP's templated min/max on 64-bit integers went
+// through f64 conversions in the scan kernel's loop header).
+__device__ __forceinline__ int64_t smin64(int64_t x, int64_t y) { return x < y ? x : y; }
+__device__ __forceinline__ int64_t smax64(int64_t x, int64_t y) { return x > y ? x : y; }
+__device__ __forceinline__ uint64_t umin64(uint64_t x, uint64_t y) { return x < y ? x : y; }
+__device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x > y ? x : y; }
+
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -114,7 +121,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 __device__ __forceinline__ uint64_t exc_run(const ScanArgs& a, uint64_t j) {
     const uint64_t b = j >> kDirShift;
     uint64_t lo = a.xr_dir[b];
-    uint64_t hi = min<uint64_t>((uint64_t)a.xr_dir[b + 1] + 1, a.n_xr);
+    uint64_t hi = umin64((uint64_t)a.xr_dir[b + 1] + 1, a.n_xr);
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
         if (a.xr_start[mid] <= j) lo = mid;
@@ -177,10 +184,10 @@ __device__ __forceinline__ bool chunk_ok(const ScanArgs& a, uint64_t G, uint32_t
     uint64_t prot;
     if (plus) {
         const int64_t a0 = (int64_t)L - a.X - (int64_t)c;  // first protected local position
-        prot = inside & ~sp_lt((int)max<int64_t>(min<int64_t>(a0, 32), 0));
+        prot = inside & ~sp_lt((int)smax64(smin64(a0, 32), 0));
     } else {
         const int64_t b0 = (int64_t)a.X - (int64_t)c;  // protected local positions < b0
-        prot = sp_lt((int)max<int64_t>(min<int64_t>(b0, len), 0));
+        prot = sp_lt((int)smax64(smin64(b0, len), 0));
     }
     if (mmv & prot) return false;
     mm += __popcll(mmv);
@@ -237,7 +244,7 @@ __device__ __forceinline__ bool fp_reject(const ScanArgs& a, uint64_t G, uint32_
         if (!a.I) d |= es & plain;
     }
     const int64_t a0 = (int64_t)l1 - a.X;  // '+' strand: positions >= l1 - X are protected
-    const uint64_t prot = inside & ~sp_lt((int)max<int64_t>(min<int64_t>(a0, 32), 0));
+    const uint64_t prot = inside & ~sp_lt((int)smax64(smin64(a0, 32), 0));
     if (d & prot) return true;
     return __popcll(d) > a.N;
 }
@@ -323,7 +330,7 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         e = r.size;
         hi = (int)min<uint32_t>((uint32_t)a.M, n - k - e);
     }
-    const int lo = (int)max<int64_t>(0, min<int64_t>(a.M, (int64_t)e - r.l1 - r.l2));
+    const int lo = (int)smax64(0, smin64(a.M, (int64_t)e - r.l1 - r.l2));
     uint64_t todo = __ballot(keep);
     while (todo) {
         const int j = (int)__builtin_ctzll(todo);
@@ -992,7 +999,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint32_t pb = R.base + (uint32_t)lane * kLanePos;
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
         const uint32_t okm = window_ok_mask(R.iv, W) &
-                             bit_range((int)sp.p_lo - (int)pb, (int)min<int64_t>((int64_t)sp.p_hi - pb, 32));
+                             bit_range((int)sp.p_lo - (int)pb, (int)smin64((int64_t)sp.p_hi - pb, 32));
         const uint64_t nx = ss + stride;
 #if MP_RANKQ
         if constexpr (kMode == 1) {
@@ -1234,7 +1241,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         const uint32_t pb = base + (uint32_t)lane * kLanePos;
         const uint32_t d0 = (uint32_t)(w0 >> 32), d1 = (uint32_t)w0, d2 = (uint32_t)(w1 >> 32);
         const uint32_t okm = window_ok_mask(iv, W) &
-                             bit_range((int)sp.p_lo - (int)pb, (int)min<int64_t>((int64_t)sp.p_hi - pb, 32));
+                             bit_range((int)sp.p_lo - (int)pb, (int)smin64((int64_t)sp.p_hi - pb, 32));
         // I=1: a window with a non-A/C/G/T/U base among its first 16 sends all its records
         // to the full test (a genome IUPAC base may match where the 2-bit compare says
         // otherwise; under I=0 such a base reads as 'A' and can only hide a mismatch, and U
@@ -1370,7 +1377,7 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const uint64_t n_refs = min<uint64_t>(a.counters[4], a.tails_cap);
+    const uint64_t n_refs = umin64(a.counters[4], a.tails_cap);
     const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
     uint32_t ncand = 0, nsurv = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 256;
@@ -1433,7 +1440,7 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
 // Persistent: each wave strides over the survivor list (empty slots skipped) and stages
 // its hits in LDS.
 __global__ __launch_bounds__(256) void pair_kernel(ScanArgs a) {
-    const uint64_t n_surv = min<uint64_t>(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
+    const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
     __shared__ HitStage s_st[4];
     const int lane = threadIdx.x & 63;
     HitStage& S = s_st[threadIdx.x >> 6];
@@ -1442,7 +1449,7 @@ __global__ __launch_bounds__(256) void pair_kernel(ScanArgs a) {
     // survivors per wave batch: up to MP_PBATCH, fewer when the list is short, so that
     // every resident wave gets work (a batch is checked one survivor at a time)
     const uint64_t waves = (uint64_t)gridDim.x * 4;
-    const uint32_t batch = (uint32_t)max<uint64_t>(4, min<uint64_t>(MP_PBATCH, (n_surv + waves - 1) / waves));
+    const uint32_t batch = (uint32_t)umax64(4, umin64(MP_PBATCH, (n_surv + waves - 1) / waves));
     const uint64_t stride = waves * batch;
     for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * batch; b < n_surv; b += stride)
         pair_check_batch(a, b, n_surv, batch, lane, S);
