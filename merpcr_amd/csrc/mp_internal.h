@@ -266,6 +266,23 @@ __host__ __device__ __forceinline__ uint32_t lds_bit(uint32_t key, uint32_t W, b
     return exact ? key : (key << (32u - 2u * W)) >> (32 - kLdsFilterLog2);
 }
 
+// W 11..13 (the rank-bitmap tables): a blocked filter -- the word is the key's top 15 bits
+// (as above) and kLdsK bits inside it are set: the next 5 bits, the last 5 bits and (k=3)
+// the 5 bits above those.  One LDS read per window either way; more bits per key cut the
+// windows that reach the global rank-word probe, which is bound by the CU's outstanding L1
+// misses.
+#ifndef MP_LDS_K
+#define MP_LDS_K 2
+#endif
+constexpr int kLdsK = MP_LDS_K;
+__host__ __device__ __forceinline__ uint32_t lds_block_mask(uint32_t x, uint32_t shw) {
+    // x: the key left-aligned in 32 bits (x >> shw = key)
+    uint32_t m = 1u << ((x >> (32 - kLdsFilterLog2)) & 31u);
+    if (kLdsK >= 2) m |= 1u << ((x >> shw) & 31u);
+    if (kLdsK >= 3) m |= 1u << ((x >> (shw + 5u)) & 31u);
+    return m;
+}
+
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {
     return d == 0 ? 0u : (d < 0 ? (uint32_t)(-2 * d - 1) : (uint32_t)(2 * d));
 }

@@ -36,6 +36,7 @@
 //   6: pair kernel stops after loading the record   7: pair kernel skips the primer-2 compares
 //   8: pair kernel skips its final hit flush          9: pair kernel never writes hits
 //  10: pair kernel stages synthetic words instead of loading the genome
+//  12: ranked scan (W 11-13): LDS prefilter only (no level-2 probes, no drain)
 #ifndef MP_ABLATE
 #define MP_ABLATE 0
 #endif
@@ -898,15 +899,20 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
     }
 }
 
-// Level 1 only: the LDS prefilter bits of the lane's 32 windows (bit 31-T), kMode != 0.
-__device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds, uint32_t d0, uint32_t d1, uint32_t d2) {
+// Level 1 only, kMode 1: the blocked LDS filter bits of the lane's 32 windows (bit 31-T):
+// every bit of lds_block_mask set in the key's word.
+__device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds, uint32_t d0, uint32_t d1, uint32_t d2,
+                                                uint32_t shw) {
     uint32_t lmask = 0;
     [&]<int... T>(std::integer_sequence<int, T...>) {
         ((
             [&] {
                 const uint32_t x = kmer_top<T>(d0, d1, d2);
-                lmask |= __builtin_amdgcn_ubfe(lds[x >> (37 - kLdsFilterLog2)], (x >> (32 - kLdsFilterLog2)) & 31u, 1u)
-                         << (31 - T);
+                const uint32_t wv = lds[x >> (37 - kLdsFilterLog2)];
+                uint32_t on = __builtin_amdgcn_ubfe(wv, (x >> (32 - kLdsFilterLog2)) & 31u, 1u);
+                if constexpr (kLdsK >= 2) on &= __builtin_amdgcn_ubfe(wv, (x >> shw) & 31u, 1u);
+                if constexpr (kLdsK >= 3) on &= __builtin_amdgcn_ubfe(wv, (x >> (shw + 5u)) & 31u, 1u);
+                lmask |= on << (31 - T);
             }()),
          ...);
     }(std::make_integer_sequence<int, 32>{});
@@ -1008,7 +1014,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // a lane with more than K positives takes further passes; their seeds join the
             // same queue, drained once (in rounds only when it fills)
             constexpr int K = MP_L2SLOTS;
-            uint32_t rem = lds_probe32(s_lf, d0, d1, d2) & okm;
+            uint32_t rem = lds_probe32(s_lf, d0, d1, d2, shw) & okm;
+#if MP_ABLATE == 12
+            ncand += (uint32_t)__popc(rem);  // level 1 only
+            rem = 0;
+            if (nx < n_supers) {
+                locate(nx);
+                words(nx, nw0, nw1, niv);
+            }
+            ss = nx;
+            continue;
+#endif
             bool first = true;
             uint32_t qfill = 0;  // queued seeds not yet drained (wave-uniform)
             do {
