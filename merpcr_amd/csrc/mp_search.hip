@@ -900,7 +900,8 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
 }
 
 // Level 1 only, kMode 1: the blocked LDS filter bits of the lane's 32 windows (bit 31-T):
-// every bit of lds_block_mask set in the key's word.
+// all kK bits of lds_block_mask set in the key's word.
+template <int kK>
 __device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds, uint32_t d0, uint32_t d1, uint32_t d2,
                                                 uint32_t shw) {
     uint32_t lmask = 0;
@@ -910,8 +911,7 @@ __device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds
                 const uint32_t x = kmer_top<T>(d0, d1, d2);
                 const uint32_t wv = lds[x >> (37 - kLdsFilterLog2)];
                 uint32_t on = __builtin_amdgcn_ubfe(wv, (x >> (32 - kLdsFilterLog2)) & 31u, 1u);
-                if constexpr (kLdsK >= 2) on &= __builtin_amdgcn_ubfe(wv, (x >> shw) & 31u, 1u);
-                if constexpr (kLdsK >= 3) on &= __builtin_amdgcn_ubfe(wv, (x >> (shw + 5u)) & 31u, 1u);
+                if constexpr (kK >= 2) on &= __builtin_amdgcn_ubfe(wv, (x >> shw) & 31u, 1u);
                 lmask |= on << (31 - T);
             }()),
          ...);
@@ -929,7 +929,7 @@ __device__ __forceinline__ uint32_t kmer_dyn(uint32_t d0, uint32_t d1, uint32_t 
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
 // ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
 // The next super-step's plane words are loaded before the current one is processed.
-template <int kMode, bool kInline>
+template <int kMode, bool kInline, int kK = 1>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // a lane with more than K positives takes further passes; their seeds join the
             // same queue, drained once (in rounds only when it fills)
             constexpr int K = MP_L2SLOTS;
-            uint32_t rem = lds_probe32(s_lf, d0, d1, d2, shw) & okm;
+            uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
 #if MP_ABLATE == 12
             ncand += (uint32_t)__popc(rem);  // level 1 only
             rem = 0;
@@ -1718,11 +1718,13 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             hipLaunchKernelGGL(dense_kernel, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
         } else if (inl) {
             if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
-            else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true>), dim3(grid), dim3(kBlock), 0, st, a);
+            else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+            else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
             else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
         } else {
             if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
-            else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, false>), dim3(grid), dim3(kBlock), 0, st, a);
+            else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+            else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, false, 1>), dim3(grid), dim3(kBlock), 0, st, a);
             else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
         }
         MP_HIP_CHECK(hipGetLastError());

@@ -149,11 +149,12 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         t->lds_exact = (2 * W <= (uint32_t)kLdsFilterLog2);
         std::vector<uint32_t> lfilt(kLdsFilterWords, 0);
         const bool blocked = !t->lds_exact && t->filt_direct;  // W 11..13: lds_block_mask
+        t->lds_k = blocked && nb > kLdsK2Keys ? 2 : 1;
         for (uint32_t b = 0; b < nb; ++b) {
             const uint32_t idx = lds_bit(bkey[b], W, t->lds_exact);
             if (blocked) {
                 const uint32_t x = bkey[b] << (32u - 2u * W);
-                lfilt[idx >> 5] |= lds_block_mask(x, 32u - 2u * W);
+                lfilt[idx >> 5] |= lds_block_mask(x, 32u - 2u * W, t->lds_k);
             } else {
                 lfilt[idx >> 5] |= 1u << (idx & 31);
             }
