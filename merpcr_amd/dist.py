@@ -86,9 +86,9 @@ def gather_hits(local, n_local: int, group=None, dst: int = 0, seq_base: int = 0
     rank = dist.get_rank(group)
     dev = local.device
     cnt = torch.tensor([n_local], dtype=torch.int64, device=dev)
-    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
+    counts = torch.zeros(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(counts, cnt, group=group)
+    counts = [int(c) for c in counts.cpu().tolist()]  # one device-to-host read
     if rank == dst:
         total = sum(counts)
         out = torch.empty(max(total, 1) * HIT_BYTES, dtype=torch.uint8, device=dev)
