@@ -252,9 +252,11 @@ constexpr uint32_t kDenseMaxW = 9;
 // plain primer position is a real one; a genome exception base there reads as 'A' and can
 // only hide mismatches under I=0, and windows with exception bases take the full test
 // under I=1), so only the words that pass reach the 32-B Entry.  Buckets of up to eight
-// records take one 16-B oct of filter words: one load per seed window.
+// records, all carrying the filter, take one 16-B oct of filter words: one load per seed
+// window, and the hot loop tests no flags (spare slots repeat slot 0's bases); other buckets
+// (longer, or holding a record the filter cannot carry) are walked through binfo.
 constexpr uint32_t kDenseAlways = 1u;   // entry not filterable (seed inside the primer, short or IUPAC primer)
-constexpr uint32_t kDensePad = 2u;      // padding slot of an oct
+constexpr uint32_t kDensePad = 2u;      // spare slot of an oct
 constexpr uint32_t kDenseMaxF = 7;
 constexpr uint32_t kDenseOct = 8;
 

@@ -1170,11 +1170,11 @@ __device__ __forceinline__ void dense_full_tests(const ScanArgs& a, uint64_t pm,
                 const uint2 L = s_grp[h >> 5];
                 o = (L.y & 0x7FFFFFFFu) + (uint32_t)__popc(L.x & ((1u << (h & 31u)) - 1u));
             }
-            const Entry e = a.dents_pad[(uint64_t)o * kDenseOct + j];
+            const Entry e = a.dents_pad[(uint64_t)o * kDenseOct + j];  // l1 = 0: a spare slot
             const uint32_t pos = pb + wi;
             k = pos - e.hash_off;
             rec = e.rec;
-            bool act = pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
+            bool act = e.l1 != 0 && pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
             if (!owned) act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
             if (act) {
                 uint64_t Gk = wi ? (w0 << (2 * wi)) | (w1 >> (64 - 2 * wi)) : w0;
@@ -1301,20 +1301,19 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
                 const bool lv = (live >> T) & 1u;
                 const bool sl = (slowm >> (31u - (TB + (uint32_t)T))) & 1u;
                 const uint32_t wv[4] = {q[T].x, q[T].y, q[T].z, q[T].w};
-                uint32_t pbits = 0, pads = 0;
+                uint32_t pbits = 0;
 #pragma unroll
                 for (int h2 = 0; h2 < 4; ++h2) {
                     const uint32_t x = gg ^ wv[h2];
                     const uint32_t d = (x | (x >> 1)) & fmask;
-                    const bool p0 = (uint32_t)__popc(d & 0xFFFFu) <= N || (wv[h2] & kDenseAlways);
-                    const bool p1 = (uint32_t)__popc(d >> 16) <= N || ((wv[h2] >> 16) & kDenseAlways);
-                    const uint32_t pad0 = (wv[h2] >> 1) & 1u, pad1 = (wv[h2] >> 17) & 1u;
-                    pbits |= ((uint32_t)((p0 || sl) && !pad0) << (2 * h2)) |
-                             ((uint32_t)((p1 || sl) && !pad1) << (2 * h2 + 1));
-                    pads += pad0 + pad1;
+                    pbits |= ((uint32_t)((uint32_t)__popc(d & 0xFFFFu) <= N) << (2 * h2)) |
+                             ((uint32_t)((uint32_t)__popc(d >> 16) <= N) << (2 * h2 + 1));
                 }
-                pm |= (uint64_t)(lv ? pbits : 0u) << (8 * T);
-                ncand += lv ? 8u - pads : 0u;
+                // spare slots (pad bit) pass with slot 0 and are skipped by the full test
+                const uint32_t spare = (wv[0] & 0x20002u) | ((wv[1] & 0x20002u) >> 1) |
+                                       ((wv[2] & 0x20002u) << 1) | ((wv[3] & 0x20002u) << 2);
+                pm |= (uint64_t)(lv ? (sl ? 0xFFu : pbits) : 0u) << (8 * T);
+                ncand += lv ? 8u - (uint32_t)__popc(spare) : 0u;
             }
             if (__any(pm != 0)) dense_full_tests(a, pm, s_grp, 0u, TB, pb, w0, w1, iv, sbase, n, owned, sp.seq, lane, C);
         }

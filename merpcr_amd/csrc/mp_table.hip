@@ -290,6 +290,14 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 const uint32_t ngrp = std::max<uint32_t>(1, nkeys / 32);
                 std::vector<uint32_t> by_key(nkeys, 0xFFFFFFFFu);
                 for (uint32_t b = 0; b < nb; ++b) by_key[bkey[b]] = b;
+                // inline: at most one oct of records, every one carrying the filter (the hot
+                // loop then tests no flags); other buckets take the escape walk
+                auto inline_ok = [&](uint32_t b) {
+                    if (bcount[b] > kDenseOct || !F) return false;
+                    for (uint32_t j = 0; j < bcount[b]; ++j)
+                        if (plain_run(ents[boff[b] + j]) < F) return false;
+                    return true;
+                };
                 dgrp.assign(ngrp, make_uint2(0, 0));
                 dgesc.assign(ngrp, 0u);
                 uint64_t np = 0;  // padded slots
@@ -299,7 +307,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                     for (uint32_t j = 0; j < 32 && g * 32 + j < nkeys; ++j) {
                         const uint32_t b = by_key[g * 32 + j];
                         if (b == 0xFFFFFFFFu) continue;
-                        if (bcount[b] > kDenseOct) {
+                        if (!inline_ok(b)) {
                             dgesc[g] |= 1u << j;
                             dgrp[g].y |= 0x80000000u;
                             continue;
@@ -312,7 +320,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 if (rc) break;
                 for (uint32_t k = 0; k < nkeys; ++k) {
                     const uint32_t b = by_key[k];
-                    if (b == 0xFFFFFFFFu || bcount[b] <= kDenseOct) continue;
+                    if (b == 0xFFFFFFFFu || inline_ok(b)) continue;
                     qfirst[b] = (uint32_t)np;
                     np += (bcount[b] + kDenseOct - 1) / kDenseOct * kDenseOct;
                 }
@@ -329,6 +337,11 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                                        ? (uint16_t)(((e.code << (2 * W)) >> 48) & ~(0xFFFFu >> (2 * F)))
                                        : (uint16_t)kDenseAlways;
                     }
+                    // inline oct: the spare slots repeat slot 0's bases (so they pass exactly
+                    // when it does) with the pad bit set; their Entry has l1 = 0 (skipped)
+                    if (inline_ok(b))
+                        for (uint32_t j = bcount[b]; j < kDenseOct; ++j)
+                            dfilt[qfirst[b] + j] = (uint16_t)(dfilt[qfirst[b]] | kDensePad);
                 }
             }
             for (uint32_t b = 0; b < nb; ++b) {
