@@ -113,6 +113,7 @@ struct Table {
     uint32_t filt_log2 = 0;   // log2(filter bits)
     int lds_exact = 0;        // LDS prefilter is the exact 4^W bitmap (W <= 10)
     int lds_k = 1;            // bits per key in the blocked LDS filter (W 11..13)
+    int defer_full = 0;       // < 5% full heads: the ranked drain defers them to tail_kernel
     uint32_t* lfilt = nullptr;  // kLdsFilterWords words
     uint32_t slot_log2 = 0;
     uint32_t* filt = nullptr;     // W >= 14: hashed presence filter

@@ -83,6 +83,7 @@ struct ScanArgs {
     const uint32_t* dgesc;  // W <= kDenseMaxW: per-32-key escape bits
     const Entry* dents_pad; // W <= kDenseMaxW: Entry per padded entry
     uint32_t dense_M;       // filter mismatch mask
+    int defer_full;         // ranked drain: full-head buckets go whole to tail_kernel
     const uint32_t* lfilt;
     const Slot* slots;
     uint32_t slot_log2;
@@ -754,9 +755,53 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
     }
 }
 
+// One seed of the ranked drain when full heads are rare (Table::defer_full): a compact
+// head (single record seeded at its primer start, plain, l1 <= W + 16) is tested right here
+// by one 32-bit XOR/popcount over bases W..l1-1 (the seed matched bases [0, W) exactly); a
+// full head sends its whole bucket to tail_kernel (its first entry is in the head's low
+// word), so the drain never reads a 32-B Entry.  Compact heads whose primer span holds a
+// genome exception base take the general candidate test (rare: all lanes must call).
+__device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
+                                              bool l, uint32_t p, const uint2 c, uint64_t G, uint32_t x, int lane,
+                                              uint32_t& ncand, SurvChunk& C, SurvChunk& TC) {
+    const uint32_t W = (uint32_t)a.W;
+    const bool full = l && (c.y & kHead8Full);
+    const uint32_t L = (c.y >> kHead8RecBits) & 31u;  // l1 - W
+    const uint32_t l1 = W + L;
+    const uint32_t exl = l1 >= 32u ? x : x & ~(0xFFFFFFFFu >> l1);
+    const bool compact = l && !full;
+    const bool general = compact && exl != 0u;
+    bool act = compact && !general && (uint64_t)p + l1 <= n;
+    if (!R.owned) act = act && sbase + p >= a.g_lo && sbase + p < a.g_hi;
+    const uint32_t g = (uint32_t)((G << (2u * W)) >> 32);
+    const uint32_t xx = g ^ c.x;
+    const uint32_t inm = L >= 16u ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (2u * L));
+    const uint32_t d = (xx | (xx >> 1)) & 0x55555555u & inm;
+    const int32_t p0 = (int32_t)L - a.X;  // protected: relative positions >= L - X
+    const uint32_t prot = p0 <= 0 ? inm : (p0 >= 16 ? 0u : inm & (0xFFFFFFFFu >> (2 * p0)));
+    bool surv = act && !(d & prot) && __popc(d) <= a.N;
+    bool exact = true;
+    ncand += act;
+    if (__any(general)) {
+        const Entry e = head8_entry(c, (uint32_t)(G >> (64u - 2u * W)), W);
+        uint32_t k2 = 0;
+        bool ex2 = false;
+        const bool s2 = candidate(a, R, sbase, n, general, p, e, ncand, k2, G, x, true, ex2);
+        if (general) {
+            surv = s2;
+            exact = ex2;
+        }
+    }
+    flush_survivors(a, R, sbase, surv, p, c.y & ((1u << kHead8RecBits) - 1u), exact, lane, C);
+    const uint64_t gp = sbase + p;
+    append_chunked<2>(&a.counters[4], a.tails, a.tails_cap, full,
+                      make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), c.x, R.seq), lane, TC,
+                      make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
+}
+
 // drain_seeds for the ranked queue (kMode 1, MP_RANKQ): the head comes straight from the
 // queued key rank -- one dependent load (the 8-B head) per seed instead of two.
-template <bool kInline>
+template <bool kInline, bool kDefer>
 __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
                                              uint32_t qn, int lane, uint32_t& ncand, WaveLds& L,
                                              SurvChunk& C, SurvChunk& TC) {
@@ -773,6 +818,13 @@ __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs&
         uint32_t xa, xb;
         window_from_regs(a, R, sbase, pa, true, Ga, xa);
         window_from_regs(a, R, sbase, pb, true, Gb, xb);
+#if MP_ABLATE != 4
+        if constexpr (kDefer) {  // compact heads tested here, full-head buckets to tail_kernel
+            drain_compact(a, R, sbase, n, la, pa, ca, Ga, xa, lane, ncand, C, TC);
+            if (b + 64 < qn) drain_compact(a, R, sbase, n, lb, pb, cb, Gb, xb, lane, ncand, C, TC);
+            continue;
+        }
+#endif
         const uint32_t ha = (uint32_t)(Ga >> shw), hb = (uint32_t)(Gb >> shw);
         Entry e0a{}, e0b{};
         if (la) {
@@ -783,6 +835,11 @@ __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs&
             if (cb.y & kHead8Full) e0b = a.dents[qb];
             else e0b = head8_entry(cb, hb, (uint32_t)a.W);
         }
+#if MP_ABLATE == 4
+        ncand += (la && e0a.rec == 0xFFFFFFFFu) + (lb && e0b.rec == 0xFFFFFFFFu) + (uint32_t)(Ga == 1) + (uint32_t)(Gb == 1) +
+                 (uint32_t)(xa == 3) + (uint32_t)(xb == 3);
+        continue;
+#endif
         heads_and_tails<1, kInline>(a, R, sbase, n, la, pa, e0a, Ga, xa, lane, ncand, C, TC);
         if (b + 64 < qn) heads_and_tails<1, kInline>(a, R, sbase, n, lb, pb, e0b, Gb, xb, lane, ncand, C, TC);
     }
@@ -929,7 +986,7 @@ __device__ __forceinline__ uint32_t kmer_dyn(uint32_t d0, uint32_t d1, uint32_t 
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
 // ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
 // The next super-step's plane words are loaded before the current one is processed.
-template <int kMode, bool kInline, int kK = 1>
+template <int kMode, bool kInline, int kK = 1, bool kDefer = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
@@ -1079,7 +1136,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     }
                     if (qfill == kSeedQR || (last && done == total && qfill)) {
                         wave_sync();
-                        drain_ranked<kInline>(a, R, sbase, n, qfill, lane, ncand, L, C, TC);
+                        drain_ranked<kInline, kDefer>(a, R, sbase, n, qfill, lane, ncand, L, C, TC);
                         wave_sync();
                         qfill = 0;
                     }
@@ -1671,7 +1728,8 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.has_u = g->has_u ? 1 : 0;
     a.seq_base = g->d_base; a.seq_len = g->d_len;
     a.spans = s->spans; a.n_spans = n_real_spans;
-    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
+    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M; a.defer_full = t->defer_full;
+    if (const char* f = std::getenv("MP_DEFER")) a.defer_full = a.defer_full && f[0] != '0';  // tests: old drain
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
@@ -1722,13 +1780,17 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
         } else {
             if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
+            else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
+                hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
             else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+            else if (t->filt_direct && a.defer_full)
+                hipLaunchKernelGGL((scan_kernel<1, false, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);
             else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, false, 1>), dim3(grid), dim3(kBlock), 0, st, a);
             else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
         }
         MP_HIP_CHECK(hipGetLastError());
         MP_HIP_CHECK(hipEventRecord(s->evt, st));
-        if (!dense && !inl && t->max_bucket > 1) {
+        if (!dense && !inl && (t->max_bucket > 1 || a.defer_full)) {  // defer_full: single-record full heads too
             hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }

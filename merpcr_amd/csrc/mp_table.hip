@@ -344,14 +344,24 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                             dfilt[qfirst[b] + j] = (uint16_t)(dfilt[qfirst[b]] | kDensePad);
                 }
             }
+            uint64_t n_full = 0;
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint32_t k = bkey[b];
                 const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
                 const Entry& e = ents[boff[b]];
                 dents[rank] = e;
-                dents8[rank] = e.count == 1 ? entry8(e) : make_uint2(0u, kHead8Full);
+                // a full head names its bucket's first entry: the ranked drain can hand the whole
+                // bucket to tail_kernel without reading the 32-B head
+                dents8[rank] = e.count == 1 ? entry8(e) : make_uint2(boff[b], kHead8Full);
+                if (dents8[rank].y & kHead8Full) {
+                    dents8[rank].x = boff[b];
+                    ++n_full;
+                }
                 if (W <= kDenseMaxW) binfo[rank] = make_uint2(qfirst[b], bcount[b]);
             }
+            // few full heads (multi-record buckets, IUPAC/long/inner-seed primers): the ranked
+            // drain tests only compact heads and defers every full-head bucket to tail_kernel
+            t->defer_full = n_full * 20 < (uint64_t)nb;
             filt.assign(1, 0);
         } else {
             uint32_t lg = 6;

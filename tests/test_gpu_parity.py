@@ -88,11 +88,13 @@ def test_dense_repeat_order():
 def test_golden_corpus(name, tails, monkeypatch):
     """Every recorded reference case through the default kernels (dense_kernel for W <= 9),
     and again through scan_kernel with the multi-record bucket tails forced to each of its
-    two paths (MP_DENSE=0, MP_TAILS), with the two-pass hit ordering (MP_SORT2)."""
+    two paths (MP_DENSE=0, MP_TAILS), with the two-pass hit ordering (MP_SORT2) and without
+    deferring full-head buckets to tail_kernel (MP_DEFER=0)."""
     if tails != "auto":
         monkeypatch.setenv("MP_TAILS", tails)
         monkeypatch.setenv("MP_DENSE", "0")
         monkeypatch.setenv("MP_SORT2", "1")  # and the two-pass 128-bit hit ordering
+        monkeypatch.setenv("MP_DEFER", "0")  # and the drain that tests full heads itself
     cases = load_golden(name)["cases"]
     bad = []
     for i, case in enumerate(cases):
