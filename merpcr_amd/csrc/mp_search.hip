@@ -485,6 +485,11 @@ static_assert(sizeof(WaveLds) <= 2048, "per-wave LDS beside the 128 KiB prefilte
 #ifndef MP_L2SLOTS
 #define MP_L2SLOTS 12
 #endif
+// level 2 through a wave-wide LDS list of the positives (full-lane probes) instead of
+// per-lane slots
+#ifndef MP_L2WAVE
+#define MP_L2WAVE 1
+#endif
 
 
 // The current super-step as the wave holds it: lane L owns bases [base + 32L,
@@ -1066,6 +1071,85 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint64_t nx = ss + stride;
 #if MP_RANKQ
         if constexpr (kMode == 1) {
+#if MP_L2WAVE
+            // level 2, wave-compacted: the wave's LDS-positive windows go into the LDS list
+            // {key, offset} (the queue's arrays), then every lane probes one list entry per
+            // pass -- full lanes, all passes' rank-word loads in flight together -- and the
+            // seeds are compacted back into the same arrays as {offset, rank}
+            const uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
+            const uint32_t c = (uint32_t)__popc(rem);
+            const uint32_t incl = wave_incl_scan(c, lane);
+            const uint32_t tot = rl32(incl, 63);
+            bool first = true;
+            uint32_t r0 = 0;
+            do {  // rounds of kSeedQR positives (one round unless the super-step is dense)
+                {
+                    uint32_t m = rem, qi = incl - c;
+                    while (m) {
+                        const uint32_t i = (uint32_t)__clz(m);
+                        m &= ~(0x80000000u >> i);
+                        if (qi - r0 < kSeedQR) {
+                            L.rq.r[qi - r0] = kmer_dyn(d0, d1, d2, i) >> shw;
+                            L.rq.q[qi - r0] = (uint16_t)((uint32_t)lane * kLanePos + i);
+                        }
+                        ++qi;
+                    }
+                }
+                wave_sync();
+                const uint32_t nr = min(tot - r0, kSeedQR);
+                constexpr int kP = (kSeedQR + 63) / 64;
+                uint32_t pk[kP], po[kP];
+                uint2 rw[kP];
+#pragma unroll
+                for (int q = 0; q < kP; ++q) {
+                    const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
+                    pk[q] = 0;
+                    po[q] = 0;
+                    rw[q] = make_uint2(0u, 0u);
+                    if ((uint32_t)q * 64u < nr) {
+                        const bool v = e < nr;
+                        pk[q] = v ? L.rq.r[e] : 0u;
+                        po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
+                        rw[q] = a.rk[v ? (pk[q] >> 5) : 0u];
+                    }
+                }
+                if (first) {  // the next super-step's words, issued after this step's probes
+                    first = false;
+                    if (nx < n_supers) {
+                        locate(nx);
+                        words(nx, nw0, nw1, niv);
+                    }
+                }
+                wave_sync();  // every list entry is in registers before the seeds overwrite it
+                uint32_t qn = 0;
+#pragma unroll
+                for (int q = 0; q < kP; ++q) {
+                    if ((uint32_t)q * 64u < nr) {
+                        const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
+                        const uint32_t bq = pk[q] & 31u;
+                        const bool hit = e < nr && ((rw[q].x >> bq) & 1u);
+                        const uint64_t hm = __ballot(hit);
+                        if (hit) {
+                            const uint32_t at = qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
+                            L.rq.q[at] = (uint16_t)po[q];
+                            L.rq.r[at] = rw[q].y + (uint32_t)__popc(rw[q].x & ((1u << bq) - 1u));
+                        }
+                        qn += (uint32_t)__popcll(hm);
+                    }
+                }
+#if MP_ABLATE == 1 || MP_ABLATE == 3
+                ncand += qn;
+#else
+                wave_sync();
+                if (qn) drain_ranked<kInline, kDefer>(a, R, sbase, n, qn, lane, ncand, L, C, TC);
+#endif
+                wave_sync();
+                r0 += kSeedQR;
+            } while (r0 < tot);
+            (void)first;
+            ss = nx;
+            continue;
+#else
             // level 2 compacted: the LDS-positive windows, MP_L2SLOTS per lane per pass, each
             // one rank-word load; a seed's rank goes into the queue beside its offset
             // a lane with more than K positives takes further passes; their seeds join the
@@ -1147,6 +1231,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             } while (__any(rem != 0));
             ss = nx;
             continue;
+#endif
         }
 #endif
         uint32_t hits = probe32<kMode>(a, s_lf, d0, d1, d2, shw, okm, [&] {
