@@ -1077,6 +1077,15 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // pass -- full lanes, all passes' rank-word loads in flight together -- and the
             // seeds are compacted back into the same arrays as {offset, rank}
             const uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
+#if MP_ABLATE == 12
+            ncand += (uint32_t)__popc(rem);  // level 1 only
+            if (nx < n_supers) {
+                locate(nx);
+                words(nx, nw0, nw1, niv);
+            }
+            ss = nx;
+            continue;
+#endif
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
