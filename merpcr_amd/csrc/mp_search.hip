@@ -37,6 +37,9 @@
 //   8: pair kernel skips its final hit flush          9: pair kernel never writes hits
 //  10: pair kernel stages synthetic words instead of loading the genome
 //  12: ranked scan (W 11-13): LDS prefilter only (no level-2 probes, no drain)
+//  15: exception bases count as mismatches without a character lookup
+//  13/14: pair kernel reports its longest / summed wave time (wall-clock ticks) as the
+//      survivor count
 #ifndef MP_ABLATE
 #define MP_ABLATE 0
 #endif
@@ -169,6 +172,28 @@ __device__ __forceinline__ uint64_t exception_mismatches(const ScanArgs& a, uint
     return mmv;
 }
 
+// 32-bit per-base mask (bit 31-i) -> spaced form (bit 62-2i).
+__device__ __forceinline__ uint64_t spread32(uint32_t v) {
+    uint64_t x = v;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & kEven;
+    return x;
+}
+
+// Spaced form (bit 62-2i) -> 32-bit per-base mask (bit 31-i); inverse of spread32.
+__device__ __forceinline__ uint32_t compress_even(uint64_t x) {
+    x &= kEven;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+    return (uint32_t)x;
+}
+
 // One chunk (bases c .. c+len-1, len <= 32) of _compare_seqs (engine.py:599-642):
 // genome window G (2-bit, base c on top) and its exception bits ex (bit 31-i) against
 // the primer's accept planes P.  Adds the chunk's mismatches to mm; false on a
@@ -182,7 +207,19 @@ __device__ __forceinline__ bool chunk_ok(const ScanArgs& a, uint64_t G, uint32_t
     const uint64_t inside = sp_lt(len);
     uint64_t mmv = ~match & inside;
     if (len < 32) ex &= ~(0xFFFFFFFFu >> len);
+#if MP_ABLATE == 15  // timing only: exception bases count as mismatches, no lookups
+    if (ex) mmv |= spread32(ex) & inside;
+#else
+    if (ex && !a.I) {
+        // literal compare (I=0): where the primer base is one of A/C/G/T (a plane bit set),
+        // a genome exception character (never exactly A/C/G/T) cannot equal it -- a
+        // mismatch without looking the character up; only the other positions need it
+        const uint64_t acgt = (P0 | P1 | P2 | P3) & kEven;
+        mmv |= spread32(ex) & acgt & inside;
+        ex &= ~compress_even(acgt);
+    }
     if (ex) mmv = exception_mismatches(a, ex, gpos_c, ch_c, mmv);
+#endif
     uint64_t prot;
     if (plus) {
         const int64_t a0 = (int64_t)L - a.X - (int64_t)c;  // first protected local position
@@ -210,17 +247,6 @@ __device__ __forceinline__ bool primer_ok(const ScanArgs& a, uint64_t gpos, uint
         if (!chunk_ok(a, G, ex, P[0], P[1], P[2], P[3], gpos + c, ch + c, len, c, L, plus, mm)) return false;
     }
     return true;
-}
-
-// 32-bit per-base mask (bit 31-i) -> spaced form (bit 62-2i).
-__device__ __forceinline__ uint64_t spread32(uint32_t v) {
-    uint64_t x = v;
-    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    x = (x | (x << 1)) & kEven;
-    return x;
 }
 
 // Lower bound on primer-1 mismatches from the fingerprint, over the first min(l1, 32)
@@ -284,6 +310,41 @@ __device__ __forceinline__ void stage_flush(const ScanArgs& a, HitStage& S, int 
     wave_sync_lds();
 }
 
+// One block of tries: the lanes whose try hit append (order key: k, record rank, try
+// rank) to the wave's stage, which leaves once it holds 64 or more.
+__device__ __forceinline__ void stage_try_hit(const ScanArgs& a, HitStage& S, int lane, bool hit, uint64_t jgk,
+                                              uint32_t jrk, int d) {
+    const uint64_t m = __ballot(hit);
+    if (!m) return;
+    const uint32_t at = S.n;
+    if (hit) {
+        const uint32_t idx = at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        S.hi[idx] = jgk;
+        S.lo[idx] = ((uint64_t)jrk << 32) | try_rank(d);
+    }
+    wave_sync_lds();
+    if (lane == 0) S.n = at + (uint32_t)__popcll(m);
+    wave_sync_lds();
+#if MP_ABLATE == 9
+    if (S.n >= 64) {
+        wave_sync_lds();
+        if (lane == 0) S.n = 0;
+        wave_sync_lds();
+    }
+#else
+    if (S.n >= 64) stage_flush(a, S, lane);
+#endif
+}
+
+// Pair-check staging per survivor (MP_PSTAGE2): kPW 2-bit words, kPE exception words and
+// the four primer-2 accept planes, [slot][survivor] in the wave's LDS.  At M=50 and
+// primers of <= 25 bases every survivor fits (the tries span <= 125 bases).
+#ifndef MP_PSTAGE2
+#define MP_PSTAGE2 1
+#endif
+constexpr int kPW = 6, kPE = 4, kPSlots = kPW + kPE + 4;
+static_assert(MP_PBATCH <= 64, "pair-check batch is one survivor per lane");
+
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
     return ((uint64_t)rl32((uint32_t)(v >> 32), j) << 32) | rl32((uint32_t)v, j);
@@ -301,7 +362,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
 // the windows, else through the accept planes.  The reference's try order 0, -1, +1,
 // ... is restored by the device sort through try_rank(d).
 __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_surv, uint32_t batch, int lane,
-                                 HitStage& S) {
+                                 HitStage& S, uint64_t* __restrict__ pst) {
     const uint64_t i = base + (uint64_t)lane;
     uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
     if ((uint32_t)lane < batch && i < n_surv) v = a.surv[i];
@@ -323,7 +384,6 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
 #if MP_ABLATE == 6
     keep = keep && r.l1 == 0xFFFFFFFFu;
 #endif
-    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);
     uint32_t e = 0;
     int hi = 0;
     if (r.size > n - k) {
@@ -333,6 +393,32 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         hi = (int)min<uint32_t>((uint32_t)a.M, n - k - e);
     }
     const int lo = (int)smax64(0, smin64(a.M, (int64_t)e - r.l1 - r.l2));
+#if MP_PSTAGE2
+    // Staged survivors: primer 2 within 32 bases and every try inside kPW 2-bit words and
+    // kPE exception words.  The lane loads its survivor's words and primer-2 planes now,
+    // in parallel with the primer-1 compare, into the wave's LDS stage ([slot][lane], so
+    // the writes are conflict-free), and phase 2 reads them from LDS instead of issuing
+    // one dependent global round trip per survivor.
+    bool fast = false;
+    {
+        const uint64_t P0l = gk + e - r.l2 - (uint32_t)lo;
+        const uint64_t lastl = P0l + (uint64_t)(lo + hi) + r.l2 - 1;
+        const uint64_t w0 = P0l >> 5, e0 = P0l >> 6;
+        const uint64_t wl = (lastl >> 5) + 1, el = (lastl >> 6) + 1;  // last words any try reads
+        fast = keep && r.l2 <= 32u && wl - w0 < (uint64_t)kPW && el - e0 < (uint64_t)kPE;
+        if (fast) {
+#pragma unroll
+            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[w0 + t] : 0ull;
+#pragma unroll
+            for (int t = 0; t < kPE; ++t) pst[(kPW + t) * MP_PBATCH + lane] = e0 + t <= el ? a.gexc[e0 + t] : 0ull;
+            const uint64_t* pp = a.planes + (uint64_t)r.p2_pl * 4;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) pst[(kPW + kPE + t) * MP_PBATCH + lane] = pp[t];
+        }
+    }
+    wave_sync_lds();
+#endif
+    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);
     uint64_t todo = __ballot(keep);
     while (todo) {
         const int j = (int)__builtin_ctzll(todo);
@@ -344,6 +430,48 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         const int jlo = (int)rl32((uint32_t)lo, j), jhi = (int)rl32((uint32_t)hi, j);
         const int ntry = jlo + jhi + 1;
         const uint64_t P0 = jgk + je - jl2 - (uint32_t)jlo;            // global start of the first try
+#if MP_PSTAGE2
+        if (rl32((uint32_t)fast, j)) {
+            const uint64_t* sj = pst + j;
+            const uint64_t Q0 = sj[(kPW + kPE) * MP_PBATCH], Q1 = sj[(kPW + kPE + 1) * MP_PBATCH];
+            const uint64_t Q2 = sj[(kPW + kPE + 2) * MP_PBATCH], Q3 = sj[(kPW + kPE + 3) * MP_PBATCH];
+            const uint64_t in2 = sp_lt((int)jl2);
+            const uint64_t two = (Q0 & Q1) | (Q0 & Q2) | (Q0 & Q3) | (Q1 & Q2) | (Q1 & Q3) | (Q2 & Q3);
+            const bool plain2 = two == 0 && ((Q0 | Q1 | Q2 | Q3) & in2) == in2;
+            const uint64_t code2 = ((Q1 | Q3) & kEven) | (((Q2 | Q3) & kEven) << 1);
+            const uint64_t prot2 = sp_lt(min(a.X, (int)jl2));  // '-' strand: positions < X
+            const uint32_t a5 = (uint32_t)(P0 & 31), a6 = (uint32_t)(P0 & 63);
+            for (int b = 0; b < ntry; b += 64) {
+                const int d = -jlo + b + lane;
+                const int64_t p2 = (int64_t)jk + je - jl2 + d;
+                const bool inb = b + lane < ntry && !(d <= 0 && (int64_t)jk + jl1 > p2) && p2 + jl2 <= (int64_t)jn;
+                const uint64_t q = P0 + (uint64_t)(b + lane);
+                // lanes past the last try clamp their word index (their result is unused)
+                const uint32_t rw = a5 + (uint32_t)(b + lane), re = a6 + (uint32_t)(b + lane);
+                const uint32_t wi = min(rw >> 5, (uint32_t)kPW - 2), ei = min(re >> 6, (uint32_t)kPE - 2);
+                const int rs = (int)(rw & 31), es = (int)(re & 63);
+                const uint64_t x0 = sj[wi * MP_PBATCH], x1 = sj[(wi + 1) * MP_PBATCH];
+                const uint64_t y0 = sj[(kPW + ei) * MP_PBATCH], y1 = sj[(kPW + ei + 1) * MP_PBATCH];
+                const uint64_t G = rs ? (x0 << (2 * rs)) | (x1 >> (64 - 2 * rs)) : x0;
+                const uint32_t ex = (uint32_t)((es ? (y0 << es) | (y1 >> (64 - es)) : y0) >> 32);
+                const int len = (int)jl2;
+                const uint32_t exl = len >= 32 ? ex : ex & ~(0xFFFFFFFFu >> len);
+                bool ok = true;
+                int mm = 0;
+                // plain primer 2: one XOR/popcount; a genome exception base is a certain
+                // mismatch under the literal rule (I=0), else the lanes need the lookup
+                if (plain2 && (!a.I || __all(!inb || exl == 0))) {
+                    const uint64_t x = G ^ code2;
+                    const uint64_t dm = ((x | (x >> 1)) | (exl ? spread32(exl) : 0ull)) & in2;
+                    ok = !(dm & prot2) && __popcll(dm) <= a.N;
+                } else if (inb) {
+                    ok = chunk_ok(a, G, ex, Q0, Q1, Q2, Q3, q, jch, len, 0, jl2, false, mm);
+                }
+                stage_try_hit(a, S, lane, inb && ok, jgk, jrk, d);
+            }
+            continue;
+        }
+#endif
         const uint64_t last = P0 + (uint64_t)(ntry - 1) + jl2 - 1;     // last base any try reads
         const uint64_t wlast = (last >> 5) + 1, elast = (last >> 6) + 1;
         uint64_t sw = ~0ull, se = ~0ull;  // staged word bases (wave-uniform)
@@ -399,37 +527,18 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
 #if MP_ABLATE == 7
                 ok = ok && (G != ex || q == 0);
 #else
-                if (plain2 && __all(!inb || exl == 0)) {
+                // plain primer 2: one XOR/popcount; a genome exception base is a certain
+                // mismatch under the literal rule (I=0), else the lanes need the lookup
+                if (plain2 && (!a.I || __all(!inb || exl == 0))) {
                     const uint64_t x = G ^ code2;
-                    const uint64_t dm = (x | (x >> 1)) & in2;
+                    const uint64_t dm = ((x | (x >> 1)) | (exl ? spread32(exl) : 0ull)) & in2;
                     ok = !(dm & prot2) && __popcll(dm) <= a.N;
                 } else if (inb && ok) {
                     ok = chunk_ok(a, G, ex, Q0, Q1, Q2, Q3, q, jch + c, len, c, jl2, false, mm);
                 }
 #endif
             }
-            const bool hit = inb && ok;
-            const uint64_t m = __ballot(hit);
-            if (m) {
-                const uint32_t at = S.n;
-                if (hit) {
-                    const uint32_t idx = at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                    S.hi[idx] = jgk;
-                    S.lo[idx] = ((uint64_t)jrk << 32) | try_rank(d);
-                }
-                wave_sync_lds();
-                if (lane == 0) S.n = at + (uint32_t)__popcll(m);
-                wave_sync_lds();
-#if MP_ABLATE == 9
-                if (S.n >= 64) {
-                    wave_sync_lds();
-                    if (lane == 0) S.n = 0;
-                    wave_sync_lds();
-                }
-#else
-                if (S.n >= 64) stage_flush(a, S, lane);
-#endif
-            }
+            stage_try_hit(a, S, lane, inb && ok, jgk, jrk, d);
         }
     }
 }
@@ -1611,6 +1720,7 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
 __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
     __shared__ HitStage s_st[4];
+    __shared__ uint64_t s_pst[4][kPSlots * MP_PBATCH];
     const int lane = threadIdx.x & 63;
     HitStage& S = s_st[threadIdx.x >> 6];
     if (lane == 0) S.n = 0;
@@ -1618,10 +1728,22 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
     // survivors per wave batch: up to MP_PBATCH, fewer when the list is short, so that
     // every resident wave gets work (a batch is checked one survivor at a time)
     const uint64_t waves = (uint64_t)gridDim.x * 4;
-    const uint32_t batch = (uint32_t)umax64(4, umin64(MP_PBATCH, (n_surv + waves - 1) / waves));
+    // equal rounds for every wave: the fewest rounds of at most MP_PBATCH, then the batch
+    // that spreads n_surv evenly over them (32 per batch would leave 1/3 of the waves
+    // one round short on c3 while the kernel waits for the rest)
+    const uint64_t rounds = umax64(1, (n_surv + waves * MP_PBATCH - 1) / (waves * MP_PBATCH));
+    const uint32_t batch = (uint32_t)umax64(4, umin64(MP_PBATCH, (n_surv + waves * rounds - 1) / (waves * rounds)));
     const uint64_t stride = waves * batch;
+#if MP_ABLATE == 13 || MP_ABLATE == 14
+    const uint64_t t_start = wall_clock64();
+#endif
     for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * batch; b < n_surv; b += stride)
-        pair_check_batch(a, b, n_surv, batch, lane, S);
+        pair_check_batch(a, b, n_surv, batch, lane, S, s_pst[threadIdx.x >> 6]);
+#if MP_ABLATE == 13  // survivors stat = longest wave (wall-clock ticks)
+    if (lane == 0) atomicMax(&a.counters[5], (unsigned long long)(wall_clock64() - t_start));
+#elif MP_ABLATE == 14  // survivors stat = sum over waves
+    if (lane == 0) atomicAdd(&a.counters[5], (unsigned long long)(wall_clock64() - t_start));
+#endif
 #if MP_ABLATE != 8 && MP_ABLATE != 9
     // the block's four stages leave with one returning atomic: one per wave at the end of
     // the kernel would serialise ~5k atomics on the hit counter (~88 per microsecond)
@@ -1915,7 +2037,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
     MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     s->n_candidates = cnt[1];
-    s->n_survivors = cnt[3];
+    s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14) ? cnt[5] : cnt[3];
     const uint64_t nh = cnt[0];
     int rc = sort_hits(s, nh, st);
     if (rc) return rc;
