@@ -244,6 +244,13 @@ __host__ __device__ __forceinline__ uint32_t filter_index(uint32_t key, uint32_t
 // head sets kHead8Full and the lookup reads the full Entry.
 constexpr uint32_t kHead8Full = 0x80000000u;
 constexpr uint32_t kHead8RecBits = 26;
+// A full head of a bucket of 1-3 records that are all seeded at primer 1's first base and
+// plain over bases W..W+F-1 (F = 14 / records) may carry kHead8Filt: bits 28-29 hold
+// records - 1 and bits [2F j, 2F j + 2F) record j's 2-bit bases W..W+F-1 (base W on
+// top).  The ranked drain hands such a bucket to tail_kernel only when some record's F
+// bases are within N mismatches of the genome (a lower bound on primer-1 mismatches).
+constexpr uint32_t kHead8Filt = 0x40000000u;
+__host__ __device__ __forceinline__ uint32_t head8_filt_bases(uint32_t records) { return 14u / records; }
 // Tables with W <= 9 run dense_kernel: the rank bitmap (4^W / 4 bytes <= 64 KiB) lives in
 // LDS and each lane walks its own seeds' buckets.
 constexpr uint32_t kDenseMaxW = 9;

@@ -37,6 +37,7 @@
 //   8: pair kernel skips its final hit flush          9: pair kernel never writes hits
 //  10: pair kernel stages synthetic words instead of loading the genome
 //  12: ranked scan (W 11-13): LDS prefilter only (no level-2 probes, no drain)
+//  16: the survivor count reports the bucket-tail reference slots instead
 //  15: exception bases count as mismatches without a character lookup
 //  13/14: pair kernel reports its longest / summed wave time (wall-clock ticks) as the
 //      survivor count
@@ -114,6 +115,25 @@ __device__ __forceinline__ int64_t smin64(int64_t x, int64_t y) { return x < y ?
 __device__ __forceinline__ int64_t smax64(int64_t x, int64_t y) { return x > y ? x : y; }
 __device__ __forceinline__ uint64_t umin64(uint64_t x, uint64_t y) { return x < y ? x : y; }
 __device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x > y ? x : y; }
+
+// Candidate / survivor statistics (counters[1], counters[3]) are summed from 64 slots
+// 256 B apart: thousands of waves ending together serialise on one address (~11 ns per
+// atomic, MI355X_MICROARCH.md) -- measured ~0.1 ms on tail_kernel's exit.  pair_kernel
+// folds the slots into counters[1] and counters[3] before the host reads them.
+constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
+constexpr size_t kCounterBytes = (size_t)(kStatBase + kStatSlots * kStatStride) * 8;
+
+__device__ __forceinline__ void add_stats(const ScanArgs& a, uint32_t cand, uint32_t surv, int lane) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cand += __shfl_xor(cand, o, 64);
+        surv += __shfl_xor(surv, o, 64);
+    }
+    const uint32_t slot = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kStatSlots - 1);
+    unsigned long long* c = a.counters + kStatBase + slot * kStatStride;
+    if (lane == 0 && cand) atomicAdd(&c[0], (unsigned long long)cand);
+    if (lane == 0 && surv) atomicAdd(&c[1], (unsigned long long)surv);
+}
 
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -907,8 +927,24 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
         }
     }
     flush_survivors(a, R, sbase, surv, p, c.y & ((1u << kHead8RecBits) - 1u), exact, lane, C);
+    bool defer = full;
+    if (full && (c.y & kHead8Filt)) {
+        // bucket prefilter (kHead8Filt): every record's bases W..W+F-1 against the genome;
+        // a window with an exception base among them is deferred untested
+        const uint32_t cnt = ((c.y >> 28) & 3u) + 1u;
+        const uint32_t F = head8_filt_bases(cnt);
+        const uint32_t fm = (1u << (2u * F)) - 1u;
+        const uint32_t gf = g >> (32u - 2u * F);
+        const uint32_t xf = x & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
+        bool any = xf != 0u;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t xj = gf ^ ((c.y >> (2u * F * j)) & fm);
+            any = any || __popc((xj | (xj >> 1)) & 0x55555555u) <= a.N;
+        }
+        defer = any;
+    }
     const uint64_t gp = sbase + p;
-    append_chunked<2>(&a.counters[4], a.tails, a.tails_cap, full,
+    append_chunked<2>(&a.counters[4], a.tails, a.tails_cap, defer,
                       make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), c.x, R.seq), lane, TC,
                       make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
 }
@@ -1384,12 +1420,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     }
     close_chunked(a.surv, a.surv_cap, lane, C);
     close_chunked<2>(a.tails, a.tails_cap, lane, TC);
-    // candidate statistics, one atomic per wave
-    uint32_t tot = ncand;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-    if (lane == 0 && tot) atomicAdd(&a.counters[1], (unsigned long long)tot);
-    if (lane == 0 && C.total) atomicAdd(&a.counters[3], (unsigned long long)C.total);
+    // candidate statistics
+    add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);
 }
 
 // Dense seeds (W <= kDenseMaxW, e.g. W=8: ~95% of windows hit one of 62k keys, 3.2 records
@@ -1617,11 +1649,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         ss = nx;
     }
     close_chunked(a.surv, a.surv_cap, lane, C);
-    uint32_t tot = ncand;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-    if (lane == 0 && tot) atomicAdd(&a.counters[1], (unsigned long long)tot);
-    if (lane == 0 && C.total) atomicAdd(&a.counters[3], (unsigned long long)C.total);
+    add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);
 }
 
 // Bucket tails: one lane per reference left by the scan (a seed whose key names more
@@ -1700,14 +1728,7 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
         __syncthreads();
     }
     tail_flush(a, s_buf, s_n, s_base);
-    uint32_t t1 = ncand, t2 = nsurv;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        t1 += __shfl_xor(t1, o, 64);
-        t2 += __shfl_xor(t2, o, 64);
-    }
-    if (lane == 0 && t1) atomicAdd(&a.counters[1], (unsigned long long)t1);
-    if (lane == 0 && t2) atomicAdd(&a.counters[3], (unsigned long long)t2);
+    add_stats(a, ncand, nsurv, lane);
 }
 
 // One wave per fingerprint survivor: exact primer-1 compare unless the fingerprint was
@@ -1719,6 +1740,20 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
 #endif
 __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
+    if (blockIdx.x == 0 && threadIdx.x < 64) {  // statistics of the scan / tail kernels (add_stats)
+        unsigned long long c = a.counters[kStatBase + threadIdx.x * kStatStride];
+        unsigned long long v = a.counters[kStatBase + threadIdx.x * kStatStride + 1];
+        static_assert(kStatSlots == 64, "one stat slot per lane");
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            c += __shfl_xor(c, o, 64);
+            v += __shfl_xor(v, o, 64);
+        }
+        if (threadIdx.x == 0) {
+            a.counters[1] = c;
+            a.counters[3] = v;
+        }
+    }
     __shared__ HitStage s_st[4];
     __shared__ uint64_t s_pst[4][kPSlots * MP_PBATCH];
     const int lane = threadIdx.x & 63;
@@ -1855,7 +1890,7 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
     int rc = MP_OK;
     do {
         if (hipSetDevice(g->device) != hipSuccess) { rc = fail(MP_E_HIP, "hipSetDevice failed"); break; }
-        if (hipMalloc(&s->counters, 64) != hipSuccess) { rc = fail(MP_E_NOMEM, "counter allocation failed"); break; }
+        if (hipMalloc(&s->counters, kCounterBytes) != hipSuccess) { rc = fail(MP_E_NOMEM, "counter allocation failed"); break; }
         if (hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess ||
             s->n_cu <= 0)
             s->n_cu = 256;
@@ -1981,7 +2016,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         a.surv_cap = s->surv_cap;
         a.tails = s->tails;
         a.tails_cap = s->tails_cap;
-        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, 48, st));
+        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
         MP_HIP_CHECK(hipEventRecord(s->ev0, st));
         if (dense) {
             const size_t lds = (sizeof(uint2) + sizeof(uint32_t)) * std::max<size_t>(1, ((size_t)1 << (2 * t->prm.wordsize)) / 32);
@@ -2037,7 +2072,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
     MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     s->n_candidates = cnt[1];
-    s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14) ? cnt[5] : cnt[3];
+    s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14) ? cnt[5] : MP_ABLATE == 16 ? cnt[4] : cnt[3];
     const uint64_t nh = cnt[0];
     int rc = sort_hits(s, nh, st);
     if (rc) return rc;

@@ -237,6 +237,22 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             c.y = fast ? (e.rec | ((uint32_t)(e.l1 - W) << kHead8RecBits)) : kHead8Full;
             return c;
         };
+        // kHead8Filt bits of a full head (0 when some record does not qualify)
+        auto head8_filter = [&](uint32_t b) -> uint32_t {
+            const uint32_t cnt = bcount[b];
+            if (cnt < 1 || cnt > 3) return 0u;
+            const uint32_t F = head8_filt_bases(cnt);
+            const uint64_t fmask = 0x5555555555555555ull & ~(~0ull >> (2 * F));  // bases 0..F-1, spaced
+            uint32_t bits = kHead8Filt | ((cnt - 1u) << 28);
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const Entry& e = ents[boff[b] + j];
+                if (e.hash_off != 0 || e.l1 < W + F || W + F > 32) return 0u;
+                const uint64_t pm = e.pmask << (2 * W);
+                if ((pm & fmask) != fmask || ((pm >> 1) & fmask) != 0) return 0u;  // plain, never "never"
+                bits |= (uint32_t)((e.code << (2 * W)) >> (64 - 2 * F)) << (2 * F * j);
+            }
+            return bits;
+        };
         std::vector<uint2> rk;
         std::vector<Entry> dents;
         std::vector<uint2> binfo;
@@ -355,6 +371,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 dents8[rank] = e.count == 1 ? entry8(e) : make_uint2(boff[b], kHead8Full);
                 if (dents8[rank].y & kHead8Full) {
                     dents8[rank].x = boff[b];
+                    dents8[rank].y = kHead8Full | head8_filter(b);
                     ++n_full;
                 }
                 if (W <= kDenseMaxW) binfo[rank] = make_uint2(qfirst[b], bcount[b]);
