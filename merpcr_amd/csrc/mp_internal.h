@@ -183,6 +183,7 @@ struct Search {
     uint64_t n_windows = 0, n_candidates = 0, n_survivors = 0;
     float scan_ms = 0.f, tail_ms = 0.f, pair_ms = 0.f, order_ms = 0.f;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, evt = nullptr;
+    uint32_t* bucket = nullptr;  // device sort: bucket counts, offsets, cursors
 };
 
 // ---------------------------------------------------------------- device helpers
@@ -303,6 +304,9 @@ inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
 // internal entry points shared across TUs
 int sort_hits(Search* s, uint64_t n, hipStream_t st);
+bool sort_hits_device_ok(const Search* s);
+int sort_hits_device(Search* s, hipStream_t st);  // hit count read on the device, writes s->out
+constexpr int kSortOverflow = 6;                  // counters[6]: a device-sort bucket overflowed
 int sort_runs(Genome* g, hipStream_t st);
 
 }  // namespace mp

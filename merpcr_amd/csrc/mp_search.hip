@@ -1832,7 +1832,7 @@ __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* _
 static void free_search(Search* s) {
     if (!s) return;
     hipFree(s->keys); hipFree(s->tmp_hi); hipFree(s->tmp_lo); hipFree(s->out); hipFree(s->sort_tmp);
-    hipFree(s->counters); hipFree(s->spans);
+    hipFree(s->counters); hipFree(s->spans); hipFree(s->bucket);
     hipFree(s->surv);
     hipFree(s->tails);
     if (s->ev0) hipEventDestroy(s->ev0);
@@ -1992,7 +1992,8 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
     a.g_lo = g_lo; a.g_hi = g_hi;
 
-    unsigned long long cnt[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool dev_sort = sort_hits_device_ok(s);
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
                                                        (uint64_t)s->n_cu * kBlocksPerCU);
     // scan -> fingerprint survivors (+ bucket-tail references -> tail survivors) -> pair
@@ -2056,7 +2057,12 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * (uint32_t)pair_per_cu), dim3(256), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
         MP_HIP_CHECK(hipEventRecord(s->ev2, st));
-        MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, 48, hipMemcpyDeviceToHost, st));
+        if (dev_sort) {  // hit order on the device count: no host round trip before the sort
+            const int src = sort_hits_device(s, st);
+            if (src) return src;
+            MP_HIP_CHECK(hipEventRecord(s->ev3, st));
+        }
+        MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, sizeof(cnt), hipMemcpyDeviceToHost, st));
         MP_HIP_CHECK(hipStreamSynchronize(st));
         if (cnt[2] <= s->surv_cap && cnt[4] <= s->tails_cap && cnt[0] <= s->cap) break;
         int rc = MP_OK;
@@ -2074,16 +2080,18 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     s->n_candidates = cnt[1];
     s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14) ? cnt[5] : MP_ABLATE == 16 ? cnt[4] : cnt[3];
     const uint64_t nh = cnt[0];
-    int rc = sort_hits(s, nh, st);
-    if (rc) return rc;
-    if (nh) {
-        const uint32_t blocks = (uint32_t)((nh + 255) / 256);
-        hipLaunchKernelGGL(decode_kernel, dim3(blocks), dim3(256), 0, st, s->keys, s->keys + s->cap, nh,
-                           g->d_base, g->d_len, g->n_seq, t->inv_rank, t->recs, s->out);
-        MP_HIP_CHECK(hipGetLastError());
+    if (!dev_sort || cnt[kSortOverflow]) {  // 128-bit order key, or a crowded bucket: rocPRIM
+        int rc = sort_hits(s, nh, st);
+        if (rc) return rc;
+        if (nh) {
+            const uint32_t blocks = (uint32_t)((nh + 255) / 256);
+            hipLaunchKernelGGL(decode_kernel, dim3(blocks), dim3(256), 0, st, s->keys, s->keys + s->cap, nh,
+                               g->d_base, g->d_len, g->n_seq, t->inv_rank, t->recs, s->out);
+            MP_HIP_CHECK(hipGetLastError());
+        }
+        MP_HIP_CHECK(hipEventRecord(s->ev3, st));
+        MP_HIP_CHECK(hipStreamSynchronize(st));
     }
-    MP_HIP_CHECK(hipEventRecord(s->ev3, st));
-    MP_HIP_CHECK(hipStreamSynchronize(st));
     MP_HIP_CHECK(hipEventElapsedTime(&s->order_ms, s->ev2, s->ev3));
     s->n_hits = nh;
     if (n_hits) *n_hits = nh;

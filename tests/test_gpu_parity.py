@@ -72,7 +72,13 @@ def test_bundled_search_to_file():
     assert text == "L78833\t75823..76023\tAFM248yg9\t(D17S932)  Chr.17, 63.7 cM\t(-)\n"
 
 
-def test_dense_repeat_order():
+@pytest.mark.parametrize("bits", [None, "1", "4"])
+def test_dense_repeat_order(bits, monkeypatch):
+    """15,936 hits on an 8 kbp repeat; with 2 forced device-sort buckets they overflow the
+    per-bucket capacity and the rocPRIM fallback orders them, with 16 each bucket holds
+    ~1,000 keys ranked in LDS."""
+    if bits:
+        monkeypatch.setenv("MP_SORT_BUCKET_BITS", bits)
     case = load_golden("repeat.json.gz")
     eng = _engine(case["params"])
     with tempfile.TemporaryDirectory() as td:
@@ -109,6 +115,25 @@ def test_golden_corpus(name, tails, monkeypatch):
         if lines != case["output"].splitlines():
             bad.append((i, case["params"], lines[:5], case["output"].splitlines()[:5]))
     assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("bits", ["1", "4"])
+def test_device_sort_crowded_buckets(bits, monkeypatch):
+    """The device-count bucket sort with forced coarse buckets: 2 buckets overflow the
+    per-bucket LDS capacity on the larger cases (rocPRIM fallback), 16 buckets rank
+    hundreds of keys per workgroup.  Every golden case must still match byte for byte."""
+    monkeypatch.setenv("MP_SORT_BUCKET_BITS", bits)
+    bad = []
+    for name in ("special_cases.json.gz", "random_cases.json.gz"):
+        for i, case in enumerate(load_golden(name)["cases"][:200]):
+            eng = _engine(case["params"])
+            with tempfile.TemporaryDirectory() as td:
+                if not _load_sts(eng, case["sts_text"], td):
+                    continue
+                recs = _records(case, eng, td)
+            if _device_lines(eng, recs) != case["output"].splitlines():
+                bad.append((name, i))
+    assert not bad, bad[:5]
 
 
 def _synthetic(seed, n_sts, glen, W, N, I, M=50, iupac_primers=False, nrun=False):
