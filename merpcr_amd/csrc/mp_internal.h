@@ -133,6 +133,7 @@ struct Table {
     uint32_t* rank = nullptr;      // rec -> position in (hash_off, rec) order
     uint32_t* inv_rank = nullptr;  // position -> rec
     uint64_t* planes = nullptr;    // 4 u64 per 32-base primer chunk
+    uint64_t planes_words = 0;
     uint8_t* pchars = nullptr;
     uint32_t rank_bits = 1;
 };

@@ -37,6 +37,9 @@
 //   8: pair kernel skips its final hit flush          9: pair kernel never writes hits
 //  10: pair kernel stages synthetic words instead of loading the genome
 //  12: ranked scan (W 11-13): LDS prefilter only (no level-2 probes, no drain)
+//  17: pair kernel reports its slowest batch (ticks, phase-1 ticks, staged, kept survivors)
+//  18: pair kernel launched twice (the second runs with warm caches)
+//  19: recs, rank and planes streamed once before the pair kernel (warm caches/TLB)
 //  16: the survivor count reports the bucket-tail reference slots instead
 //  15: exception bases count as mismatches without a character lookup
 //  13/14: pair kernel reports its longest / summed wave time (wall-clock ticks) as the
@@ -121,7 +124,14 @@ __device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x > 
 // atomic, MI355X_MICROARCH.md) -- measured ~0.1 ms on tail_kernel's exit.  pair_kernel
 // folds the slots into counters[1] and counters[3] before the host reads them.
 constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
-constexpr size_t kCounterBytes = (size_t)(kStatBase + kStatSlots * kStatStride) * 8;
+constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;  // pair_kernel batch counters, 8 x 256 B
+constexpr size_t kCounterBytes = (size_t)(kPairQBase + 8 * kStatStride) * 8;
+#ifndef MP_PDYN
+#define MP_PDYN 1
+#endif
+#ifndef MP_PDYN_BATCH
+#define MP_PDYN_BATCH 16
+#endif
 
 __device__ __forceinline__ void add_stats(const ScanArgs& a, uint32_t cand, uint32_t surv, int lane) {
 #pragma unroll
@@ -362,6 +372,12 @@ __device__ __forceinline__ void stage_try_hit(const ScanArgs& a, HitStage& S, in
 #ifndef MP_PSTAGE2
 #define MP_PSTAGE2 1
 #endif
+#ifndef MP_PPRIO  // wave priority during the pair-check prologue (0 = off)
+#define MP_PPRIO 0
+#endif
+#ifndef MP_P1X  // timing only: 1 = staging loads read a fixed word instead of the genome
+#define MP_P1X 0
+#endif
 constexpr int kPW = 6, kPE = 4, kPSlots = kPW + kPE + 4;
 static_assert(MP_PBATCH <= 64, "pair-check batch is one survivor per lane");
 
@@ -382,7 +398,10 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
 // the windows, else through the accept planes.  The reference's try order 0, -1, +1,
 // ... is restored by the device sort through try_rank(d).
 __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_surv, uint32_t batch, int lane,
-                                 HitStage& S, uint64_t* __restrict__ pst) {
+                                 HitStage& S, uint64_t* __restrict__ pst, uint64_t* dbg = nullptr) {
+#if MP_PPRIO
+    __builtin_amdgcn_s_setprio(MP_PPRIO);  // prologue: a short dependent load chain
+#endif
     const uint64_t i = base + (uint64_t)lane;
     uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
     if ((uint32_t)lane < batch && i < n_surv) v = a.surv[i];
@@ -428,9 +447,9 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         fast = keep && r.l2 <= 32u && wl - w0 < (uint64_t)kPW && el - e0 < (uint64_t)kPE;
         if (fast) {
 #pragma unroll
-            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[w0 + t] : 0ull;
+            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[MP_P1X == 1 ? (t & 1) : w0 + t] : 0ull;
 #pragma unroll
-            for (int t = 0; t < kPE; ++t) pst[(kPW + t) * MP_PBATCH + lane] = e0 + t <= el ? a.gexc[e0 + t] : 0ull;
+            for (int t = 0; t < kPE; ++t) pst[(kPW + t) * MP_PBATCH + lane] = e0 + t <= el ? a.gexc[MP_P1X == 1 ? (t & 1) : e0 + t] : 0ull;
             const uint64_t* pp = a.planes + (uint64_t)r.p2_pl * 4;
 #pragma unroll
             for (int t = 0; t < 4; ++t) pst[(kPW + kPE + t) * MP_PBATCH + lane] = pp[t];
@@ -440,6 +459,15 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
 #endif
     if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);
     uint64_t todo = __ballot(keep);
+#if MP_PPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+#if MP_ABLATE == 17
+    dbg[0] = wall_clock64();
+    dbg[1] = (uint64_t)__popcll(todo) | ((uint64_t)__popcll(__ballot(fast)) << 8);
+#else
+    (void)dbg;
+#endif
     while (todo) {
         const int j = (int)__builtin_ctzll(todo);
         todo &= todo - 1;
@@ -1740,6 +1768,9 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
 #endif
 __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
+#if MP_ABLATE == 17
+    const uint64_t t_k0 = wall_clock64();
+#endif
     if (blockIdx.x == 0 && threadIdx.x < 64) {  // statistics of the scan / tail kernels (add_stats)
         unsigned long long c = a.counters[kStatBase + threadIdx.x * kStatStride];
         unsigned long long v = a.counters[kStatBase + threadIdx.x * kStatStride + 1];
@@ -1772,8 +1803,51 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
 #if MP_ABLATE == 13 || MP_ABLATE == 14
     const uint64_t t_start = wall_clock64();
 #endif
+#if MP_PDYN
+    // Dynamic batches: survivors cost very different amounts (primer-1 failures leave in
+    // the prologue), so a static split left the slowest wave ~1.7x the mean.  Each XCD
+    // (blocks x, x+8, ...) owns 1/8 of the batches: its waves take one batch each, then
+    // pull the rest from the XCD's own counter (8 counters 256 B apart, ~1.3k atomics each).
+    {
+        const uint32_t db = (uint32_t)umax64(4, umin64(MP_PDYN_BATCH, (n_surv + waves - 1) / waves));
+        const uint64_t nbat = (n_surv + db - 1) / db;
+        const uint32_t x = blockIdx.x & 7u;
+        const uint64_t lo_b = nbat * x / 8, hi_b = nbat * (x + 1) / 8;
+        const uint64_t nw_x = (uint64_t)((gridDim.x - x + 7u) / 8u) * 4u;  // waves of this XCD
+#if MP_PDYN == 2  // every batch claimed from the counter, the first too
+        uint64_t bi;
+        {
+            unsigned long long t = 0;
+            if (lane == 0) t = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
+            bi = lo_b + (uint64_t)__shfl((long long)t, 0, 64);
+        }
+        const uint64_t nw_d = 0;
+#else
+        uint64_t bi = lo_b + (uint64_t)(blockIdx.x >> 3) * 4u + (threadIdx.x >> 6);
+        const uint64_t nw_d = nw_x;
+#endif
+        while (bi < hi_b) {
+#if MP_ABLATE == 17  // survivors stat = slowest batch: ticks << 40 | phase-1 ticks << 16 | fast << 8 | kept
+            uint64_t dbg[2] = {0, 0};
+            const uint64_t t0 = wall_clock64();
+            pair_check_batch(a, bi * db, n_surv, db, lane, S, s_pst[threadIdx.x >> 6], dbg);
+            const uint64_t t1 = wall_clock64();
+            if (lane == 0)
+                atomicMax(&a.counters[5], (unsigned long long)(((t1 - t0) << 40) | (umin64(dbg[0] - t0, 0xFFFFFF) << 16) |
+                                                               umin64((t0 - t_k0) >> 4, 0xFFFF)));
+#else
+            pair_check_batch(a, bi * db, n_surv, db, lane, S, s_pst[threadIdx.x >> 6]);
+#endif
+            unsigned long long t = 0;
+            if (lane == 0) t = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
+            bi = lo_b + nw_d + (uint64_t)__shfl((long long)t, 0, 64);
+        }
+    }
+    (void)stride;
+#else
     for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * batch; b < n_surv; b += stride)
         pair_check_batch(a, b, n_surv, batch, lane, S, s_pst[threadIdx.x >> 6]);
+#endif
 #if MP_ABLATE == 13  // survivors stat = longest wave (wall-clock ticks)
     if (lane == 0) atomicMax(&a.counters[5], (unsigned long long)(wall_clock64() - t_start));
 #elif MP_ABLATE == 14  // survivors stat = sum over waves
@@ -1799,6 +1873,16 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
         }
     }
 #endif
+}
+
+// Timing experiment (MP_ABLATE 19): stream a table once so its pages and lines are warm.
+__global__ void warm_kernel(const uint4* __restrict__ p, uint64_t n16, unsigned long long* sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 v = p[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u) atomicAdd(sink, 1ull);
 }
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
@@ -2049,6 +2133,11 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }
+#if MP_ABLATE == 19
+        hipLaunchKernelGGL(warm_kernel, dim3(512), dim3(256), 0, st, (const uint4*)t->recs, (uint64_t)t->n_rec * 2, s->counters + 7);
+        hipLaunchKernelGGL(warm_kernel, dim3(512), dim3(256), 0, st, (const uint4*)t->rank, (uint64_t)t->n_rec / 4, s->counters + 7);
+        hipLaunchKernelGGL(warm_kernel, dim3(512), dim3(256), 0, st, (const uint4*)t->planes, t->planes_words / 2, s->counters + 7);
+#endif
         MP_HIP_CHECK(hipEventRecord(s->ev1, st));
         int pair_per_cu = 0;  // persistent: every resident block slot once
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pair_per_cu, pair_kernel, 256, 0) != hipSuccess ||
@@ -2056,6 +2145,9 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             pair_per_cu = 5;
         hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * (uint32_t)pair_per_cu), dim3(256), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
+#if MP_ABLATE == 18  // timing only: the pair kernel twice (warm second launch; hits doubled)
+        hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * (uint32_t)pair_per_cu), dim3(256), 0, st, a);
+#endif
         MP_HIP_CHECK(hipEventRecord(s->ev2, st));
         if (dev_sort) {  // hit order on the device count: no host round trip before the sort
             const int src = sort_hits_device(s, st);
@@ -2078,7 +2170,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
     MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     s->n_candidates = cnt[1];
-    s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14) ? cnt[5] : MP_ABLATE == 16 ? cnt[4] : cnt[3];
+    s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14 || MP_ABLATE == 17) ? cnt[5] : MP_ABLATE == 16 ? cnt[4] : cnt[3];
     const uint64_t nh = cnt[0];
     if (!dev_sort || cnt[kSortOverflow]) {  // 128-bit order key, or a crowded bucket: rocPRIM
         int rc = sort_hits(s, nh, st);

@@ -422,6 +422,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->inv_rank, order.data(), order.size(), &bytes))) break;
         planes.push_back(0); planes.push_back(0); planes.push_back(0); planes.push_back(0);
         if ((rc = upload(&t->planes, planes.data(), planes.size(), &bytes))) break;
+        t->planes_words = planes.size();
         pchars.resize(pchars.size() + 40, 0);  // chunk_ok reads 36 bytes from a 4-aligned offset
         if ((rc = upload(&t->pchars, pchars.data(), pchars.size(), &bytes))) break;
         t->dev_bytes = bytes;
