@@ -185,6 +185,7 @@ struct Search {
     float scan_ms = 0.f, tail_ms = 0.f, pair_ms = 0.f, order_ms = 0.f;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, evt = nullptr;
     uint32_t* bucket = nullptr;  // device sort: bucket counts, offsets, cursors
+    bool sort_crowded = false;   // a device-sort bucket overflowed: later runs go to rocPRIM
 };
 
 // ---------------------------------------------------------------- device helpers

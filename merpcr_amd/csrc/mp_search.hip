@@ -2077,7 +2077,9 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.g_lo = g_lo; a.g_hi = g_hi;
 
     unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const bool dev_sort = sort_hits_device_ok(s);
+    // crowded hit positions (IUPAC primers over N runs, repeats) overflow the buckets and
+    // pay both sorts; once seen, this search orders with rocPRIM directly
+    const bool dev_sort = sort_hits_device_ok(s) && !s->sort_crowded;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
                                                        (uint64_t)s->n_cu * kBlocksPerCU);
     // scan -> fingerprint survivors (+ bucket-tail references -> tail survivors) -> pair
@@ -2172,6 +2174,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     s->n_candidates = cnt[1];
     s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14 || MP_ABLATE == 17) ? cnt[5] : MP_ABLATE == 16 ? cnt[4] : cnt[3];
     const uint64_t nh = cnt[0];
+    if (dev_sort && cnt[kSortOverflow]) s->sort_crowded = true;
     if (!dev_sort || cnt[kSortOverflow]) {  // 128-bit order key, or a crowded bucket: rocPRIM
         int rc = sort_hits(s, nh, st);
         if (rc) return rc;

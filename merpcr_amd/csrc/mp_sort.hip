@@ -60,39 +60,73 @@ __global__ void unpack_keys(const uint64_t* __restrict__ key, uint64_t n, unsign
 constexpr uint32_t kSortCap = 2048;
 constexpr unsigned kMaxBucketBits = 16;
 
+// Raw hits arrive in runs of one bucket (a survivor's tries, a wave's batch of nearby
+// survivors; IUPAC primers over N runs pile thousands on a few positions).  Same-address
+// atomics serialise at the L2, so each wave collapses its runs of equal buckets: the run
+// head adds the run length once and hands the base to the run's other lanes.
+__device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint32_t& head, uint32_t& len) {
+    const uint32_t prev = (uint32_t)__shfl_up((int)b, 1, 64);
+    const uint64_t heads = __ballot(on && (lane == 0 || prev != b));
+    const uint64_t upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+    head = upto ? 63u - (uint32_t)__clzll(upto) : 0u;  // this lane's run head
+    const uint64_t above = heads & ~((2ull << lane) - 1ull);
+    const uint64_t onm = __ballot(on);
+    const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1u : 64u - (uint32_t)__clzll(onm);
+    len = end - (uint32_t)lane;  // meaningful on heads only
+}
+
 __global__ void bucket_hist(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
                             const unsigned long long* __restrict__ counters, uint64_t cap, unsigned try_bits,
                             unsigned low_bits, unsigned shift, uint64_t* __restrict__ keys, uint32_t* __restrict__ cnt) {
     const uint64_t n = counters[0] < cap ? counters[0] : cap;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t l = lo[i];
-        const uint64_t key = (hi[i] << low_bits) | ((l >> 32) << try_bits) | (l & 0xFFFFFFFFull);
-        keys[i] = key;
-        atomicAdd(&cnt[key >> shift], 1u);
+    const int lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
+        const uint64_t i = base + (uint64_t)lane;  // wave-uniform loop: the ballots see every lane
+        const bool on = i < n;
+        uint32_t b = 0xFFFFFFFFu;
+        if (on) {
+            const uint64_t l = lo[i];
+            const uint64_t key = (hi[i] << low_bits) | ((l >> 32) << try_bits) | (l & 0xFFFFFFFFull);
+            keys[i] = key;
+            b = (uint32_t)(key >> shift);
+        }
+        uint32_t head, len;
+        bucket_runs(b, on, lane, head, len);
+        if (on && head == (uint32_t)lane) atomicAdd(&cnt[b], len);
     }
 }
 
-// exclusive scan of the bucket counts (one 1024-thread workgroup); cursor = offset
+// exclusive scan of the bucket counts (one 1024-thread workgroup, <= 64 buckets per
+// thread held in registers: one load round trip); cursor = offset
 __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restrict__ cnt, uint32_t nb,
                                                        uint32_t* __restrict__ off, uint32_t* __restrict__ cursor) {
     __shared__ uint32_t s_part[1024];
-    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t per = (nb + 1023) / 1024;  // <= 64 (nb <= 2^16)
     const uint32_t b0 = threadIdx.x * per;
+    uint32_t v[64];
     uint32_t sum = 0;
-    for (uint32_t j = 0; j < per && b0 + j < nb; ++j) sum += cnt[b0 + j];
+#pragma unroll
+    for (uint32_t j = 0; j < 64; ++j) {
+        v[j] = j < per && b0 + j < nb ? cnt[b0 + j] : 0u;
+        sum += v[j];
+    }
     s_part[threadIdx.x] = sum;
     __syncthreads();
     for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t v = threadIdx.x >= o ? s_part[threadIdx.x - o] : 0u;
+        const uint32_t x = threadIdx.x >= o ? s_part[threadIdx.x - o] : 0u;
         __syncthreads();
-        s_part[threadIdx.x] += v;
+        s_part[threadIdx.x] += x;
         __syncthreads();
     }
     uint32_t run = s_part[threadIdx.x] - sum;
-    for (uint32_t j = 0; j < per && b0 + j < nb; ++j) {
-        off[b0 + j] = run;
-        cursor[b0 + j] = run;
-        run += cnt[b0 + j];
+#pragma unroll
+    for (uint32_t j = 0; j < 64; ++j) {
+        if (j < per && b0 + j < nb) {
+            off[b0 + j] = run;
+            cursor[b0 + j] = run;
+        }
+        run += v[j];
     }
     if (threadIdx.x == 1023) off[nb] = s_part[1023];
 }
@@ -100,9 +134,19 @@ __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restric
 __global__ void bucket_scatter(const uint64_t* __restrict__ keys, const unsigned long long* __restrict__ counters,
                                uint64_t cap, unsigned shift, uint32_t* __restrict__ cursor, uint64_t* __restrict__ out) {
     const uint64_t n = counters[0] < cap ? counters[0] : cap;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t key = keys[i];
-        out[atomicAdd(&cursor[key >> shift], 1u)] = key;
+    const int lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
+        const uint64_t i = base + (uint64_t)lane;
+        const bool on = i < n;
+        const uint64_t key = on ? keys[i] : 0ull;
+        const uint32_t b = on ? (uint32_t)(key >> shift) : 0xFFFFFFFFu;
+        uint32_t head, len;
+        bucket_runs(b, on, lane, head, len);
+        uint32_t pos = 0;
+        if (on && head == (uint32_t)lane) pos = atomicAdd(&cursor[b], len);
+        pos = (uint32_t)__shfl((int)pos, (int)head, 64) + ((uint32_t)lane - head);
+        if (on) out[pos] = key;
     }
 }
 
@@ -121,11 +165,36 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
         return;
     }
     for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
+    const bool small = m <= 256;  // rank by counting; larger buckets: bitonic sort in LDS
+    if (!small) {
+        uint32_t P = 512;
+        while (P < m) P <<= 1;
+        for (uint32_t i = m + threadIdx.x; i < P; i += blockDim.x) s_k[i] = ~0ull;
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+                    const uint32_t ij = i ^ j;
+                    if (ij > i) {
+                        const uint64_t x = s_k[i], y = s_k[ij];
+                        if ((x > y) == ((i & k) == 0)) {
+                            s_k[i] = y;
+                            s_k[ij] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
         const uint64_t key = s_k[i];
-        uint32_t r = 0;
-        for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
+        uint32_t r = i;
+        if (small) {
+            r = 0;
+            for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
+        }
         const uint64_t gk = key >> low_bits;
         const uint32_t rank = (uint32_t)((key & ((1ull << low_bits) - 1ull)) >> try_bits);
         const uint32_t tr = (uint32_t)(key & ((1ull << try_bits) - 1ull));
