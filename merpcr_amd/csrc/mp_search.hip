@@ -165,13 +165,6 @@ __device__ __forceinline__ uint64_t exc_run(const ScanArgs& a, uint64_t j) {
     return lo;
 }
 
-// Byte i (0..31) of the 36 primer bytes held as nine 32-bit words.
-__device__ __forceinline__ uint8_t byte_of(const uint32_t (&w)[9], uint32_t i) {
-    uint32_t v = w[0];
-#pragma unroll
-    for (int q = 1; q < 9; ++q) v = (i >> 2) == (uint32_t)q ? w[q] : v;
-    return (uint8_t)(v >> (8 * (i & 3)));
-}
 
 // Exception bases of a window (bit 31-i of ex): their characters come from the run
 // index, walked forward once from the first one; each is compared with the primer
@@ -179,10 +172,6 @@ __device__ __forceinline__ uint8_t byte_of(const uint32_t (&w)[9], uint32_t i) {
 // cleared.  Rare (windows touching non-ACGT bases), so kept out of line.
 __device__ __forceinline__ uint64_t exception_mismatches(const ScanArgs& a, uint32_t ex, uint64_t gpos_c, uint32_t ch_c,
                                                      uint64_t mmv) {
-    const uint32_t c0 = ch_c & ~3u, sh = ch_c & 3u;
-    uint32_t pw[9];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) pw[q] = *reinterpret_cast<const uint32_t*>(a.pchars + c0 + 4u * q);
     uint64_t j = exc_run(a, gpos_c + (uint32_t)__clz(ex));
     uint8_t gch = a.xr_char[j];
     uint64_t nxt = j + 1 < a.n_xr ? a.xr_start[j + 1] : ~0ull;
@@ -195,7 +184,9 @@ __device__ __forceinline__ uint64_t exception_mismatches(const ScanArgs& a, uint
             gch = a.xr_char[j];
             nxt = j + 1 < a.n_xr ? a.xr_start[j + 1] : ~0ull;
         }
-        const bool ok = char_match(gch, byte_of(pw, sh + (uint32_t)i), a.I);
+        // the primer character straight from memory (a register array indexed by i went
+        // to scratch, which every wave of the kernel then paid for)
+        const bool ok = char_match(gch, a.pchars[ch_c + (uint32_t)i], a.I);
         const uint64_t bit = 1ull << (62 - 2 * i);
         mmv = ok ? (mmv & ~bit) : (mmv | bit);
     }
