@@ -410,6 +410,10 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         rk = a.rank[rec];
     }
     const uint32_t k = (uint32_t)(gk - sbase);
+#if MP_ABLATE == 17
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t t_rec = wall_clock64();
+#endif
     keep = keep && n - k - r.l1 >= r.l2;
 #if MP_ABLATE == 6
     keep = keep && r.l1 == 0xFFFFFFFFu;
@@ -438,15 +442,23 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         fast = keep && r.l2 <= 32u && wl - w0 < (uint64_t)kPW && el - e0 < (uint64_t)kPE;
         if (fast) {
 #pragma unroll
+#if MP_P1X == 3  // timing only: nothing loaded
+            for (int t = 0; t < kPSlots; ++t) pst[t * MP_PBATCH + lane] = w0 + t;
+#else
             for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[MP_P1X == 1 ? (t & 1) : w0 + t] : 0ull;
 #pragma unroll
             for (int t = 0; t < kPE; ++t) pst[(kPW + t) * MP_PBATCH + lane] = e0 + t <= el ? a.gexc[MP_P1X == 1 ? (t & 1) : e0 + t] : 0ull;
-            const uint64_t* pp = a.planes + (uint64_t)r.p2_pl * 4;
+            const uint64_t* pp = a.planes + (MP_P1X == 2 ? 0ull : (uint64_t)r.p2_pl * 4);
 #pragma unroll
             for (int t = 0; t < 4; ++t) pst[(kPW + kPE + t) * MP_PBATCH + lane] = pp[t];
+#endif
         }
     }
     wave_sync_lds();
+#endif
+#if MP_ABLATE == 17
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t t_stage = wall_clock64();
 #endif
     if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);
     uint64_t todo = __ballot(keep);
@@ -455,7 +467,8 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
 #endif
 #if MP_ABLATE == 17
     dbg[0] = wall_clock64();
-    dbg[1] = (uint64_t)__popcll(todo) | ((uint64_t)__popcll(__ballot(fast)) << 8);
+    dbg[1] = t_rec;
+    dbg[2] = t_stage;
 #else
     (void)dbg;
 #endif
@@ -1819,13 +1832,15 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
 #endif
         while (bi < hi_b) {
 #if MP_ABLATE == 17  // survivors stat = slowest batch: ticks << 40 | phase-1 ticks << 16 | fast << 8 | kept
-            uint64_t dbg[2] = {0, 0};
+            uint64_t dbg[3] = {0, 0, 0};
             const uint64_t t0 = wall_clock64();
             pair_check_batch(a, bi * db, n_surv, db, lane, S, s_pst[threadIdx.x >> 6], dbg);
             const uint64_t t1 = wall_clock64();
             if (lane == 0)
-                atomicMax(&a.counters[5], (unsigned long long)(((t1 - t0) << 40) | (umin64(dbg[0] - t0, 0xFFFFFF) << 16) |
-                                                               umin64((t0 - t_k0) >> 4, 0xFFFF)));
+                atomicMax(&a.counters[5], (unsigned long long)(((t1 - t0) << 40) | (umin64((dbg[1] - t0) >> 4, 0x1FFF) << 27) |
+                                                               (umin64((dbg[2] - t0) >> 4, 0x1FFF) << 14) |
+                                                               umin64((dbg[0] - t0) >> 4, 0x3FFF)));
+            (void)t_k0;
 #else
             pair_check_batch(a, bi * db, n_surv, db, lane, S, s_pst[threadIdx.x >> 6]);
 #endif
