@@ -2151,6 +2151,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pair_per_cu, pair_kernel, 256, 0) != hipSuccess ||
             pair_per_cu < 1)
             pair_per_cu = 5;
+        if (const char* f = std::getenv("MP_PAIR_PER_CU")) pair_per_cu = std::max(1, std::min(pair_per_cu, std::atoi(f)));  // timing
         hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * (uint32_t)pair_per_cu), dim3(256), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
 #if MP_ABLATE == 18  // timing only: the pair kernel twice (warm second launch; hits doubled)
