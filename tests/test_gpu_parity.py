@@ -366,3 +366,41 @@ def test_seed_queue_rounds(W):
     ref = C.search(table, [np.frombuffer(g.encode(), dtype=np.uint8)], O.params(**prm), 8)
     assert len(ref) > 1000
     assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize("N,X", [(0, 0), (1, 1), (2, 0)])
+def test_full_head_prefilter_buckets(N, X, monkeypatch):
+    """Buckets of 2-4 records that share a primer-1 seed (kHead8Filt prefilter on the full
+    8-B head for 1-3 records, plain deferral for 4), some also sharing the filter bases,
+    with planted amplicons of every record: the deferring drain against the C oracle."""
+    from merpcr_amd import synth
+    from oracle import c_oracle as C
+    W = 11
+    sts = synth.make_sts(6000, seed=11, W=W)
+    rng = np.random.default_rng(5)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    # ~1.5% of the buckets shared, so the drain defers full heads (under 5% of them)
+    for i in range(0, 450, 3):  # groups: record i's first W (or W + 4) bases copied to i+1, i+2
+        for j in (1, 2):
+            keep = W + (4 if rng.random() < 0.3 else 0)
+            tail = acgt[rng.integers(0, 4, len(sts.p1[i + j]) - keep)].tobytes()
+            sts.p1[i + j] = sts.p1[i][:keep] + tail
+    for i in range(3000, 3040, 4):  # a few 4-record buckets
+        for j in (1, 2, 3):
+            sts.p1[i + j] = sts.p1[i][:W] + sts.p1[i + j][W:]
+    glen = 5_000_000
+    g = acgt[rng.integers(0, 4, glen)].copy()
+    amps, starts = synth.amplicons(sts, glen, 13, N, 50, W)
+    for amp, st in zip(amps, starts):
+        if st + len(amp) <= glen:
+            g[st:st + len(amp)] = np.frombuffer(amp, dtype=np.uint8)
+    seq = g.tobytes().decode("ascii")
+    prm = dict(wordsize=W, mismatches=N, three_prime_match=X, margin=50)
+    eng = MerPCR(**prm)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts.text(), td)
+    hits = eng.find_hits([FASTARecord(defline=">chrH", sequence=seq)])
+    table = O.load_sts_lines(sts.text().splitlines(True), W, 240)
+    ref = C.search(table, [g], O.params(**prm), 8)
+    assert len(ref) > 1000
+    assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes()
