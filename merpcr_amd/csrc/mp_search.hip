@@ -40,6 +40,7 @@
 //  17: pair kernel reports its slowest batch (ticks, phase-1 ticks, staged, kept survivors)
 //  18: pair kernel launched twice (the second runs with warm caches)
 //  19: recs, rank and planes streamed once before the pair kernel (warm caches/TLB)
+//  20/21: scan kernel reports its longest / summed wave time (ticks) as the survivor count
 //  16: the survivor count reports the bucket-tail reference slots instead
 //  15: exception bases count as mismatches without a character lookup
 //  13/14: pair kernel reports its longest / summed wave time (wall-clock ticks) as the
@@ -125,7 +126,8 @@ __device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x > 
 // folds the slots into counters[1] and counters[3] before the host reads them.
 constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
 constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;  // pair_kernel batch counters, 8 x 256 B
-constexpr size_t kCounterBytes = (size_t)(kPairQBase + 8 * kStatStride) * 8;
+constexpr int kSchedBase = kPairQBase + 8 * kStatStride;  // scan super-step chunk counters, 8 x 256 B
+constexpr size_t kCounterBytes = (size_t)(kSchedBase + 8 * kStatStride) * 8;
 #ifndef MP_PDYN
 #define MP_PDYN 1
 #endif
@@ -1168,10 +1170,56 @@ __device__ __forceinline__ uint32_t kmer_dyn(uint32_t d0, uint32_t d1, uint32_t 
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
 // ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
 // The next super-step's plane words are loaded before the current one is processed.
+// Dynamic super-step order (MP_SDYN): with a static round-robin the last wave of the scan
+// ended 15% after the mean (c3: 2.76 vs 2.36 ms; MP_ABLATE 20/21) -- super-steps differ in
+// cost and a CU's younger waves get fewer issue slots.  Each XCD (blocks x, x+8, ...) owns
+// a contiguous 1/8 of the super-steps in chunks of kSChunk; its waves take one chunk each,
+// then claim further chunks from the XCD's counter one chunk ahead (the claim's latency
+// hides behind the chunk's work; ~9 atomics per microsecond per counter on c3).
+#ifndef MP_SDYN
+#define MP_SDYN 1
+#endif
+constexpr uint64_t kSChunk = 8;
+struct SuperSched {
+    uint64_t lo, hi, nw, end;  // XCD range, waves of the XCD, end of the current chunk
+    uint64_t pending;          // lane 0: counter value claimed for the next chunk
+    unsigned long long* ctr;
+    __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint64_t n_supers, int w, int kW, int lane) {
+        const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
+        const uint32_t x = blockIdx.x % g;
+        ctr = counters + kSchedBase + x * kStatStride;
+        lo = n_supers * x / g;
+        hi = n_supers * (x + 1) / g;
+        nw = (uint64_t)((gridDim.x - x + g - 1u) / g) * (uint64_t)kW;
+        const uint64_t st = lo + ((uint64_t)(blockIdx.x / g) * (uint64_t)kW + (uint64_t)w) * kSChunk;
+        end = umin64(st + kSChunk, hi);
+        claim(lane);
+        return st < hi ? st : n_supers;
+    }
+    __device__ __forceinline__ void claim(int lane) {
+        pending = 0;
+        if (lane == 0) pending = atomicAdd(ctr, 1ull);
+    }
+    __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane) {
+        if (ss + 1 < end) return ss + 1;
+        const uint64_t st = lo + (nw + (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pending)) * kSChunk;
+        if (st >= hi) {
+            end = 0;
+            return n_supers;
+        }
+        end = umin64(st + kSChunk, hi);
+        claim(lane);
+        return st;
+    }
+};
+
 template <int kMode, bool kInline, int kK = 1, bool kDefer = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
+#if MP_ABLATE == 20 || MP_ABLATE == 21
+    const uint64_t t_k0 = wall_clock64();
+#endif
 
     // stage the seed prefilter in LDS (once per persistent workgroup)
     for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)
@@ -1189,7 +1237,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     SurvChunk C{0, 64u, 0u};
     SurvChunk TC{0, 64u, 0u};
 
+#if MP_SDYN
+    SuperSched sch;
+    uint64_t ss = sch.first(a.counters, n_supers, w, kWaves, lane);
+#else
     uint64_t ss = (uint64_t)blockIdx.x * kWaves + (uint64_t)w;
+#endif
     // span of the super-step being prefetched, cached in registers (wave-uniform): the
     // common path of the prefetch issues only the four plane loads, no waits
     SeqSpan pf{};
@@ -1245,7 +1298,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
         const uint32_t okm = window_ok_mask(R.iv, W) &
                              bit_range((int)sp.p_lo - (int)pb, (int)smin64((int64_t)sp.p_hi - pb, 32));
+#if MP_SDYN
+        const uint64_t nx = sch.next(ss, n_supers, lane);
+        (void)stride;
+#else
         const uint64_t nx = ss + stride;
+#endif
 #if MP_RANKQ
         if constexpr (kMode == 1) {
 #if MP_L2WAVE
@@ -1454,6 +1512,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     close_chunked<2>(a.tails, a.tails_cap, lane, TC);
     // candidate statistics
     add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);
+#if MP_ABLATE == 20  // survivors stat = latest wave end (ticks after its block started)
+    if (lane == 0) atomicMax(&a.counters[5], (unsigned long long)(wall_clock64() - t_k0));
+#elif MP_ABLATE == 21  // survivors stat = sum over waves
+    if (lane == 0) atomicAdd(&a.counters[5], (unsigned long long)(wall_clock64() - t_k0));
+#endif
 }
 
 // Dense seeds (W <= kDenseMaxW, e.g. W=8: ~95% of windows hit one of 62k keys, 3.2 records
@@ -2179,7 +2242,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
     MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     s->n_candidates = cnt[1];
-    s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14 || MP_ABLATE == 17) ? cnt[5] : MP_ABLATE == 16 ? cnt[4] : cnt[3];
+    s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14 || MP_ABLATE == 17 || MP_ABLATE == 20 || MP_ABLATE == 21) ? cnt[5] : MP_ABLATE == 16 ? cnt[4] : cnt[3];
     const uint64_t nh = cnt[0];
     if (dev_sort && cnt[kSortOverflow]) s->sort_crowded = true;
     if (!dev_sort || cnt[kSortOverflow]) {  // 128-bit order key, or a crowded bucket: rocPRIM
