@@ -1602,7 +1602,12 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     uint32_t ncand = 0;
     SurvChunk C{0, 64u, 0u};
 
+#if MP_SDYN
+    SuperSched sch;
+    uint64_t ss = sch.first(a.counters, n_supers, w, kDenseWaves, lane);
+#else
     uint64_t ss = (uint64_t)blockIdx.x * kDenseWaves + (uint64_t)w;
+#endif
     SeqSpan pf{};
     pf.super0 = 1;
     uint64_t pf_end = 0, pf_sbase = 0;
@@ -1650,7 +1655,12 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         // otherwise; under I=0 such a base reads as 'A' and can only hide a mismatch, and U
         // compares as T under I=1)
         const uint32_t slowm = a.I ? ~window_ok_mask(iv, 16u) : 0u;
+#if MP_SDYN
+        const uint64_t nx = sch.next(ss, n_supers, lane);
+        (void)stride;
+#else
         const uint64_t nx = ss + stride;
+#endif
         if (nx < n_supers) {  // next super-step's words, in flight during this one
             locate(nx);
             words(nx, nw0, nw1, niv);
