@@ -1179,7 +1179,10 @@ __device__ __forceinline__ uint32_t kmer_dyn(uint32_t d0, uint32_t d1, uint32_t 
 #ifndef MP_SDYN
 #define MP_SDYN 1
 #endif
-constexpr uint64_t kSChunk = 8;
+#ifndef MP_SCHUNK
+#define MP_SCHUNK 8
+#endif
+constexpr uint64_t kSChunk = MP_SCHUNK;
 struct SuperSched {
     uint64_t lo, hi, nw, end;  // XCD range, waves of the XCD, end of the current chunk
     uint64_t pending;          // lane 0: counter value claimed for the next chunk
