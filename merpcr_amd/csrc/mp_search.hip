@@ -1187,7 +1187,16 @@ struct SuperSched {
     uint64_t lo, hi, nw, end;  // XCD range, waves of the XCD, end of the current chunk
     uint64_t pending;          // lane 0: counter value claimed for the next chunk
     unsigned long long* ctr;
+    uint64_t stride;  // 0: dynamic; else the static round-robin stride
     __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint64_t n_supers, int w, int kW, int lane) {
+        // short scans (under 64 super-steps per wave, e.g. c2) keep the static order: their
+        // per-wave totals average out and the claims would only add latency
+        const uint64_t waves = (uint64_t)gridDim.x * (uint64_t)kW;
+        if (n_supers < waves * 64u) {
+            stride = waves;
+            return (uint64_t)blockIdx.x * (uint64_t)kW + (uint64_t)w;
+        }
+        stride = 0;
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
         ctr = counters + kSchedBase + x * kStatStride;
@@ -1204,6 +1213,7 @@ struct SuperSched {
         if (lane == 0) pending = atomicAdd(ctr, 1ull);
     }
     __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane) {
+        if (stride) return ss + stride;
         if (ss + 1 < end) return ss + 1;
         const uint64_t st = lo + (nw + (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pending)) * kSChunk;
         if (st >= hi) {
