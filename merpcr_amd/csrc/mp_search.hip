@@ -1183,44 +1183,44 @@ __device__ __forceinline__ uint32_t kmer_dyn(uint32_t d0, uint32_t d1, uint32_t 
 #define MP_SCHUNK 8
 #endif
 constexpr uint64_t kSChunk = MP_SCHUNK;
-struct SuperSched {
-    uint64_t lo, hi, nw, end;  // XCD range, waves of the XCD, end of the current chunk
-    uint64_t pending;          // lane 0: counter value claimed for the next chunk
-    unsigned long long* ctr;
-    uint64_t stride;  // 0: dynamic; else the static round-robin stride
+struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives beside the scan's registers
+    uint32_t lo, hi, nw, end;  // XCD group range, waves of the group, end of the current chunk
+    uint32_t pending;          // lane 0: counter value claimed for the next chunk
+    uint32_t stride;           // 0: dynamic; else the static round-robin stride
+    unsigned int* ctr;
     __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint64_t n_supers, int w, int kW, int lane) {
         // short scans (under 64 super-steps per wave, e.g. c2) keep the static order: their
         // per-wave totals average out and the claims would only add latency
-        const uint64_t waves = (uint64_t)gridDim.x * (uint64_t)kW;
-        if (n_supers < waves * 64u) {
+        const uint32_t waves = gridDim.x * (uint32_t)kW;
+        if (n_supers < (uint64_t)waves * 64u) {
             stride = waves;
             return (uint64_t)blockIdx.x * (uint64_t)kW + (uint64_t)w;
         }
         stride = 0;
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
-        ctr = counters + kSchedBase + x * kStatStride;
-        lo = n_supers * x / g;
-        hi = n_supers * (x + 1) / g;
-        nw = (uint64_t)((gridDim.x - x + g - 1u) / g) * (uint64_t)kW;
-        const uint64_t st = lo + ((uint64_t)(blockIdx.x / g) * (uint64_t)kW + (uint64_t)w) * kSChunk;
-        end = umin64(st + kSChunk, hi);
+        ctr = reinterpret_cast<unsigned int*>(counters + kSchedBase + x * kStatStride);
+        lo = (uint32_t)(n_supers * x / g);
+        hi = (uint32_t)(n_supers * (x + 1) / g);
+        nw = ((gridDim.x - x + g - 1u) / g) * (uint32_t)kW;
+        const uint32_t st = lo + ((blockIdx.x / g) * (uint32_t)kW + (uint32_t)w) * (uint32_t)kSChunk;
+        end = min(st + (uint32_t)kSChunk, hi);
         claim(lane);
         return st < hi ? st : n_supers;
     }
     __device__ __forceinline__ void claim(int lane) {
         pending = 0;
-        if (lane == 0) pending = atomicAdd(ctr, 1ull);
+        if (lane == 0) pending = atomicAdd(ctr, 1u);
     }
     __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane) {
         if (stride) return ss + stride;
         if (ss + 1 < end) return ss + 1;
-        const uint64_t st = lo + (nw + (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pending)) * kSChunk;
+        const uint32_t st = lo + (nw + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending)) * (uint32_t)kSChunk;
         if (st >= hi) {
             end = 0;
             return n_supers;
         }
-        end = umin64(st + kSChunk, hi);
+        end = min(st + (uint32_t)kSChunk, hi);
         claim(lane);
         return st;
     }
