@@ -1901,9 +1901,10 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
     {
         const uint32_t db = (uint32_t)umax64(4, umin64(MP_PDYN_BATCH, (n_surv + waves - 1) / waves));
         const uint64_t nbat = (n_surv + db - 1) / db;
-        const uint32_t x = blockIdx.x & 7u;
-        const uint64_t lo_b = nbat * x / 8, hi_b = nbat * (x + 1) / 8;
-        const uint64_t nw_x = (uint64_t)((gridDim.x - x + 7u) / 8u) * 4u;  // waves of this XCD
+        const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
+        const uint32_t x = blockIdx.x % g;
+        const uint64_t lo_b = nbat * x / g, hi_b = nbat * (x + 1) / g;
+        const uint64_t nw_x = (uint64_t)((gridDim.x - x + g - 1u) / g) * 4u;  // waves of this group
 #if MP_PDYN == 2  // every batch claimed from the counter, the first too
         uint64_t bi;
         {
@@ -1913,7 +1914,7 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
         }
         const uint64_t nw_d = 0;
 #else
-        uint64_t bi = lo_b + (uint64_t)(blockIdx.x >> 3) * 4u + (threadIdx.x >> 6);
+        uint64_t bi = lo_b + (uint64_t)(blockIdx.x / g) * 4u + (threadIdx.x >> 6);
         const uint64_t nw_d = nw_x;
 #endif
         while (bi < hi_b) {
