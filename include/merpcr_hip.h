@@ -104,12 +104,39 @@ int mp_genome_put_device(void* genome, uint32_t seq, uint64_t offset, const uint
 /* Build the exception-run index; required once after the last put. */
 int mp_genome_seal(void* genome, void* stream);
 int mp_genome_stats(void* genome, uint64_t* total_bases, uint64_t* n_exc_runs, uint64_t* dev_bytes);
+/* Re-lay the handle out for a new set of sequences (the next search() call of the
+ * engine): device planes are reused when the new layout fits them, else regrown.  The
+ * handle is unsealed and empty afterwards; searches created on it stay valid. */
+int mp_genome_reset(void* genome, uint32_t n_seq, const uint64_t* seq_len);
 void mp_genome_destroy(void* genome);
 
 /* ---- search (replaces _process_thread/_match_sts/_compare_seqs and the
  * sort of engine.py:434; T=1 semantics) ---------------------------------------
  * A search handle owns the hit buffers for one (table, genome) pair. */
 int mp_search_create(void* table, void* genome, void** search_out);
+
+/* Kernel-path selection and initial list capacities of a search handle.  Every field
+ * zero (the state after mp_search_create) = the library's own choice; the other values
+ * exist so that tests can drive each path of the hot loop and its overflow recovery. */
+#define MP_TAILS_AUTO 0    /* bucket tails: chosen from the table's key sharing */
+#define MP_TAILS_INLINE 1  /* expanded by the scanning wave itself */
+#define MP_TAILS_KERNEL 2  /* left as references for tail_kernel */
+#define MP_SORT_AUTO 0     /* device bucket sort when the order key fits 64 bits */
+#define MP_SORT_RADIX64 1  /* rocPRIM radix sort of the packed 64-bit key */
+#define MP_SORT_RADIX128 2 /* two stable rocPRIM passes over the 128-bit key */
+typedef struct mp_search_options {
+    int32_t tails;              /* MP_TAILS_* */
+    int32_t no_defer;           /* 1: the ranked drain tests full-head buckets itself */
+    int32_t no_dense;           /* 1: W <= 9 tables run scan_kernel, not dense_kernel */
+    int32_t sort;               /* MP_SORT_* */
+    int32_t sort_bucket_bits;   /* device bucket sort: log2(buckets); 0 = from the capacity */
+    int32_t pair_blocks_per_cu; /* pair_kernel residency; 0 = every resident slot */
+    uint64_t hit_cap;           /* initial raw-hit list capacity (entries); 0 = default */
+    uint64_t surv_cap;          /* initial fingerprint-survivor list capacity; 0 = default */
+    uint64_t tail_cap;          /* initial bucket-tail reference list capacity; 0 = default */
+} mp_search_options;
+/* Replace the handle's options (reallocating the lists to the given capacities). */
+int mp_search_set_options(void* search, const mp_search_options* opt);
 /* Scan, verify, pair-check and sort.  *n_hits receives the number of hits of
  * the owned range (range NULL = whole genome).  Synchronises `stream`. */
 int mp_search_run(void* search, const mp_range* range, void* stream, uint64_t* n_hits);
@@ -123,6 +150,9 @@ int mp_search_device_hits(void* search, const mp_hit** dev_hits);
 /* Duration of the last run's scan kernel alone (HIP events on the run's stream), the
  * number of candidate seeds it verified and the windows it scanned. */
 int mp_search_last_stats(void* search, float* scan_ms, uint64_t* n_windows, uint64_t* n_candidates);
+/* List regrowths (a run whose survivor, tail or hit list overflowed and was rerun)
+ * over the handle's life. */
+int mp_search_regrowths(void* search, uint64_t* n_regrowths);
 /* Seeds whose primer-1 fingerprint could not reject them (pair-checked). */
 int mp_search_survivors(void* search, uint64_t* n_survivors);
 /* Last run's stage times (HIP events on the run's stream): seed scan kernel alone,
@@ -138,6 +168,9 @@ void mp_search_destroy(void* search);
  * before the first header dropped.  The caller handles the reference's empty-file
  * case (fasta.py:31-33) before calling.  Records stay owned by the handle. */
 int mp_fasta_load(const char* path, void** fasta_out);
+/* Same, reading the file in chunks of `chunk_bytes` (0 = 64 MiB): tests use small chunks
+ * to put read seams inside lines, UTF-8 sequences and CR/LF pairs. */
+int mp_fasta_load_chunked(const char* path, uint64_t chunk_bytes, void** fasta_out);
 /* Number of records and total filtered sequence bytes. */
 int mp_fasta_info(void* fasta, uint64_t* n_records, uint64_t* total_bytes);
 /* Borrowed pointers to record i's defline (UTF-8, with '>') and filtered sequence. */

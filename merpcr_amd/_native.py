@@ -30,10 +30,10 @@ EXPORTS = (
     "mp_abi_version", "mp_last_error", "mp_device_count",
     "mp_table_create", "mp_table_stats", "mp_table_destroy",
     "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
-    "mp_genome_stats", "mp_genome_destroy",
-    "mp_search_create", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
-    "mp_search_last_stats", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
-    "mp_fasta_load", "mp_fasta_info", "mp_fasta_record", "mp_fasta_destroy",
+    "mp_genome_stats", "mp_genome_reset", "mp_genome_destroy",
+    "mp_search_create", "mp_search_set_options", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
+    "mp_search_last_stats", "mp_search_regrowths", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
+    "mp_fasta_load", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record", "mp_fasta_destroy",
     "mp_format_hits",
     "mp_sts_parse", "mp_sts_info", "mp_sts_arrays", "mp_sts_destroy",
 )
@@ -47,6 +47,16 @@ class MPParams(ctypes.Structure):
 class MPRange(ctypes.Structure):
     _fields_ = [("seq_begin", c_uint32), ("seq_end", c_uint32),
                 ("k_begin", c_uint64), ("k_end", c_uint64)]
+
+
+MP_TAILS = {"auto": 0, "inline": 1, "kernel": 2}
+MP_SORT = {"auto": 0, "radix64": 1, "radix128": 2}
+
+
+class MPSearchOptions(ctypes.Structure):
+    _fields_ = [("tails", c_int32), ("no_defer", c_int32), ("no_dense", c_int32), ("sort", c_int32),
+                ("sort_bucket_bits", c_int32), ("pair_blocks_per_cu", c_int32),
+                ("hit_cap", c_uint64), ("surv_cap", c_uint64), ("tail_cap", c_uint64)]
 
 
 HIT_DTYPE = np.dtype([("pos1", "<u8"), ("pos2", "<u8"), ("seq", "<u4"), ("rec", "<u4")])
@@ -77,10 +87,13 @@ def _sig(lib):
     lib.mp_genome_put_device.argtypes = [P, c_uint32, c_uint64, P, c_uint64, P]
     lib.mp_genome_seal.argtypes = [P, P]
     lib.mp_genome_stats.argtypes = [P, u64p, u64p, u64p]
+    lib.mp_genome_reset.argtypes = [P, c_uint32, P]
     lib.mp_genome_destroy.argtypes = [P]
     lib.mp_genome_destroy.restype = None
     lib.mp_search_create.argtypes = [P, P, POINTER(c_void_p)]
+    lib.mp_search_set_options.argtypes = [P, POINTER(MPSearchOptions)]
     lib.mp_search_run.argtypes = [P, POINTER(MPRange), P, u64p]
+    lib.mp_search_regrowths.argtypes = [P, u64p]
     lib.mp_search_fetch.argtypes = [P, P, c_uint64, P]
     lib.mp_search_fetch_device.argtypes = [P, P, c_uint64, P]
     lib.mp_search_device_hits.argtypes = [P, POINTER(c_void_p)]
@@ -90,6 +103,7 @@ def _sig(lib):
     lib.mp_search_destroy.argtypes = [P]
     lib.mp_search_destroy.restype = None
     lib.mp_fasta_load.argtypes = [c_char_p, POINTER(c_void_p)]
+    lib.mp_fasta_load_chunked.argtypes = [c_char_p, c_uint64, POINTER(c_void_p)]
     lib.mp_fasta_info.argtypes = [P, u64p, u64p]
     lib.mp_fasta_record.argtypes = [P, c_uint64, POINTER(c_void_p), u64p, POINTER(c_void_p), u64p]
     lib.mp_fasta_destroy.argtypes = [P]
@@ -181,6 +195,11 @@ class Genome:
         self.lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
         check(lib().mp_genome_create(device, len(self.lengths), ptr(self.lengths), ctypes.byref(self._h)))
 
+    def reset(self, lengths):
+        """New sequence set on the same device buffers (grown only when needed)."""
+        self.lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        check(lib().mp_genome_reset(self._h, len(self.lengths), ptr(self.lengths)))
+
     def put(self, seq: int, data: bytes, offset: int = 0, stream=None):
         buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
@@ -215,6 +234,19 @@ class Search:
         self.table = table
         self.genome = genome
         check(lib().mp_search_create(table._h, genome._h, ctypes.byref(self._h)))
+
+    def set_options(self, tails="auto", defer=True, dense=True, sort="auto", sort_bucket_bits=0,
+                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0):
+        """Kernel-path selection and initial list capacities (mp_search_set_options);
+        the defaults are the library's automatic choices."""
+        o = MPSearchOptions(MP_TAILS[tails], 0 if defer else 1, 0 if dense else 1, MP_SORT[sort],
+                            sort_bucket_bits, pair_blocks_per_cu, hit_cap, surv_cap, tail_cap)
+        check(lib().mp_search_set_options(self._h, ctypes.byref(o)))
+
+    def regrowths(self) -> int:
+        n = c_uint64()
+        check(lib().mp_search_regrowths(self._h, ctypes.byref(n)))
+        return n.value
 
     def run(self, rng=None, stream=None) -> int:
         n = c_uint64(0)
@@ -300,13 +332,14 @@ def sts_parse(path: str, wordsize: int, default_pcr_size: int):
         lib().mp_sts_destroy(h)
 
 
-def fasta_read(path: str):
-    """Read a FASTA file natively (mp_fasta_load); returns [(defline, sequence bytes)].
+def fasta_read(path: str, chunk_bytes: int = 0):
+    """Read a FASTA file natively (mp_fasta_load_chunked); returns [(defline, sequence bytes)].
 
     Raises UnicodeDecodeError for invalid UTF-8, as the reference's text-mode read does.
+    chunk_bytes (tests) sets the read size; 0 = the library default.
     """
     h = c_void_p()
-    rc = lib().mp_fasta_load(os.fsencode(path), ctypes.byref(h))
+    rc = lib().mp_fasta_load_chunked(os.fsencode(path), chunk_bytes, ctypes.byref(h))
     _decode_error(rc)
     check(rc)
     try:

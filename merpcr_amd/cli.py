@@ -33,7 +33,7 @@ def convert_mepcr_arguments(args: List[str]) -> List[str]:
 
 def setup_logging(quiet: int, debug: bool) -> None:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
-    logger = logging.getLogger("merpcr_amd")
+    logger = logging.getLogger("merpcr")
     if debug:
         logger.setLevel(logging.DEBUG)
     elif quiet == 0:
@@ -98,7 +98,7 @@ def create_parser() -> argparse.ArgumentParser:
 def main(argv: List[str] = None) -> int:
     args = create_parser().parse_args(convert_mepcr_arguments(sys.argv[1:] if argv is None else argv))
     setup_logging(args.quiet, args.debug)
-    logger = logging.getLogger("merpcr_amd")
+    logger = logging.getLogger("merpcr")
     try:
         eng = MerPCR(wordsize=args.wordsize, margin=args.margin, mismatches=args.mismatches,
                      three_prime_match=args.three_prime_match, iupac_mode=args.iupac,

@@ -47,7 +47,9 @@ MIN_THREE_PRIME_MATCH = 0
 MIN_PCR_SIZE = 1
 MAX_PCR_SIZE = 10000
 
-logger = logging.getLogger(__name__)
+# the reference's module logger name (src/merpcr/core/engine.py: getLogger(__name__)), so
+# that code configuring the "merpcr" logger hierarchy sees this engine's messages too
+logger = logging.getLogger("merpcr.core.engine")
 
 _CODE2 = {"A": 0, "C": 1, "G": 2, "T": 3, "U": 3}
 _COMPL_BASE = {"A": "T", "C": "G", "G": "C", "T": "A", "U": "A", "B": "V", "D": "H",
@@ -89,6 +91,13 @@ class MerPCR:
         self._dev_table_sig = None
         self._codes = CharCodes()
         self.last_search_stats: dict = {}
+        # kernel-path selection of the device search (tests; _native.Search.set_options
+        # keywords), and the genome/search handles kept across search() calls
+        self.search_options: dict = {}
+        self._dev_genome = None
+        self._dev_search = None
+        self._dev_search_key = None
+        self._dev_genome_dev = None
 
         self._init_lookup_tables()
         self._validate_parameters()
@@ -263,17 +272,27 @@ class MerPCR:
         self._sts_keys.append(hash_value)
 
     def _hash_value(self, primer: str) -> Tuple[int, int]:
-        """(offset, value) of the first all-ACGTU W-mer (engine.py:331-355)."""
+        """(offset, value) of the first all-ACGTU W-mer (engine.py:331-355).
+
+        The reference looks every character it reaches up in its 256-entry scode list, so a
+        character whose upper case is beyond U+00FF raises IndexError when the scan reaches
+        it: every position up to the end of the first valid window, or, when there is none,
+        up to the first ambiguous character at or after len - W (the last offset tried)."""
         p = primer.upper()
         W = self.wordsize
-        if len(p) < W:
+        n = len(p)
+        if n < W:
             return -1, 0
         run = 0
         v = 0
         mask = (1 << (2 * W)) - 1
         for i, ch in enumerate(p):
+            if ord(ch) > 0xFF:
+                raise IndexError("list index out of range")
             c = _CODE2.get(ch)
             if c is None:
+                if i >= n - W:
+                    return -1, 0
                 run = 0
                 v = 0
                 continue
@@ -355,7 +374,20 @@ class MerPCR:
         return self._dev_table
 
     def encode_sequences(self, sequences: Sequence[str]) -> List[np.ndarray]:
-        return [self._codes.sequence_bytes(s) for s in sequences]
+        """Device bytes of each sequence, in the coordinates of ``seq.upper()``.
+
+        Raises IndexError as the reference's scan does (engine.py:455-503 looks every base
+        up in the 256-entry scode list): a sequence longer than W holding a character whose
+        upper case is beyond U+00FF."""
+        out = []
+        W = self.wordsize
+        for s in sequences:
+            if not s.isascii():
+                up = s.upper()
+                if len(up) > W and max(map(ord, up)) > 0xFF:
+                    raise IndexError("list index out of range")
+            out.append(self._codes.sequence_bytes(s))
+        return out
 
     def chunk_plan(self, seq_len: int) -> List[Tuple[int, int]]:
         """(offset, length) of each chunk the reference's search scans for a record of
@@ -382,7 +414,10 @@ class MerPCR:
         chunk lists are concatenated in chunk order and stably sorted on pos1
         (engine.py:412-434) -- overlap hits then appear once per chunk, as in the
         reference's multi-process output."""
-        data = self.encode_sequences([r.sequence for r in fasta_records])
+        self.device_table()  # registers the primers' non-ASCII codes before the genome is encoded
+        return self._hits_of(self.encode_sequences([r.sequence for r in fasta_records]))
+
+    def _hits_of(self, data: List[np.ndarray]) -> np.ndarray:
         if not (self.emulate_chunks and self.threads > 1):
             return self._search_device(data)
         pieces, owner, base = [], [], []
@@ -403,21 +438,39 @@ class MerPCR:
             hits = hits[np.argsort(hits["seq"], kind="stable")]
         return hits
 
-    def _search_device(self, data: Sequence[np.ndarray]) -> np.ndarray:
+    def _device_search(self, lengths):
+        """Genome and search handles of this engine, kept across calls: the genome is
+        re-laid out on its existing device buffers (mp_genome_reset) and the search keeps
+        its grown hit lists and sort buffers."""
         from .. import _native
         table = self.device_table()
-        genome = _native.Genome(self.device, [len(d) for d in data])
+        if self._dev_genome is None or self._dev_genome_dev != self.device:
+            self._dev_search = None
+            self._dev_genome = _native.Genome(self.device, lengths)
+            self._dev_genome_dev = self.device
+        else:
+            self._dev_genome.reset(lengths)
+        key = tuple(sorted(self.search_options.items()))
+        if self._dev_search is None or self._dev_search.table is not table or self._dev_search_key != key:
+            if self._dev_search is not None:
+                self._dev_search.close()
+            self._dev_search = _native.Search(table, self._dev_genome)
+            if self.search_options:
+                self._dev_search.set_options(**self.search_options)
+            self._dev_search_key = key
+        return self._dev_genome, self._dev_search
+
+    def _search_device(self, data: Sequence[np.ndarray]) -> np.ndarray:
+        genome, search = self._device_search([len(d) for d in data])
         for i, d in enumerate(data):
             if len(d):
                 genome.put(i, d)
         genome.seal()
-        search = _native.Search(table, genome)
         t0 = time.time()
         n = search.run()
         hits = search.fetch(n)
-        self.last_search_stats = dict(search.last_stats(), wall_s=time.time() - t0, hits=n)
-        search.close()
-        genome.close()
+        self.last_search_stats = dict(search.last_stats(), wall_s=time.time() - t0, hits=n,
+                                      regrowths=search.regrowths())
         return hits
 
     # ------------------------------------------------------------------ search
@@ -449,19 +502,51 @@ class MerPCR:
         return [STSHit(pos1=int(h["pos1"]), pos2=int(h["pos2"]), sts=recs[int(h["rec"])]) for h in hits]
 
     def search(self, fasta_records: List[FASTARecord], output_file: str = None) -> int:
-        """Search every record; print one line per hit (engine.py:365-451)."""
+        """Search every record; print one line per hit (engine.py:365-451).
+
+        One device pass covers all records; the per-record log lines and output then follow
+        in the reference's order (record i's lines before record i+1's log).  A record the
+        reference's scan would fail on (IndexError, see encode_sequences) ends the call
+        after the output of the records before it, as in the reference."""
         to_file = bool(output_file) and output_file.lower() != "stdout"
         output = open(output_file, "w") if to_file else sys.stdout
+        total = 0
         try:
-            for rec in fasta_records:
+            recs = list(fasta_records)
+            self.device_table()
+            data, err = [], None
+            for r in recs:
+                try:
+                    data.extend(self.encode_sequences([r.sequence]))
+                except IndexError as e:
+                    err = e
+                    break
+            n_ok = len(data)
+            if self.threads > 1 and not self.emulate_chunks and any(
+                    len(self.chunk_plan(len(r.sequence))) > 1 for r in recs[:n_ok]):
+                logger.warning("threads > 1: hits are reported once, as with -T 1 (the reference's "
+                               "multi-process chunking repeats hits inside chunk overlaps; "
+                               "emulate_chunks=True reproduces that output)")
+            hits = self._hits_of(data) if n_ok else np.zeros(0, dtype=_hit_dtype())
+            text = self.format_bytes(recs[:n_ok], hits) if len(hits) else b""
+            # byte range of each record's lines: hits are ordered by record
+            per = np.bincount(hits["seq"].astype(np.int64), minlength=n_ok) if len(hits) else np.zeros(n_ok, np.int64)
+            ends = np.flatnonzero(np.frombuffer(text, dtype=np.uint8) == 10) + 1 if text else np.zeros(0, np.int64)
+            line_end = np.cumsum(per)
+            pos = 0
+            for i, rec in enumerate(recs[:n_ok]):
                 logger.info(f"Processing sequence: {rec.label} ({len(rec.sequence)} bp)")
                 self._log_thread_plan(len(rec.sequence))
-            total = 0
-            if fasta_records:
-                hits = self.find_hits(fasta_records)
-                total = len(hits)
-                if total:
-                    output.write(self.format_bytes(fasta_records, hits).decode("utf-8"))
+                if per[i]:
+                    stop = int(ends[line_end[i] - 1])
+                    output.write(text[pos:stop].decode("utf-8"))
+                    pos = stop
+                    total += int(per[i])
+            if err is not None:
+                rec = recs[n_ok]
+                logger.info(f"Processing sequence: {rec.label} ({len(rec.sequence)} bp)")
+                self._log_thread_plan(len(rec.sequence))
+                raise err
         finally:
             if to_file:
                 output.close()
@@ -471,11 +556,17 @@ class MerPCR:
 
     # kept for surface compatibility with code that drives one chunk by hand
     def _process_thread(self, thread_data: ThreadData) -> ThreadData:
-        """One chunk scanned as its own sequence (engine.py:453-505), on the GPU."""
-        rec = FASTARecord(defline=">chunk", sequence=thread_data.sequence, label="chunk")
-        hits = self.find_hits([rec])
+        """One chunk scanned as its own sequence (engine.py:453-505), on the GPU: always one
+        device sequence, whatever threads / emulate_chunks say."""
+        self.device_table()
+        hits = self._search_device(self.encode_sequences([thread_data.sequence]))
         for h in self.hits_as_objects(hits):
             h.pos1 += thread_data.offset
             h.pos2 += thread_data.offset
             thread_data.hits.append(h)
         return thread_data
+
+
+def _hit_dtype():
+    from .._native import HIT_DTYPE
+    return HIT_DTYPE

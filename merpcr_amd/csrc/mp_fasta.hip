@@ -128,15 +128,10 @@ using namespace mp;
 // Streaming state machine over the file: no line is ever buffered whole, so a
 // single-line chromosome costs one pass.  Only an incomplete trailing UTF-8 code point
 // (< 4 bytes) is carried between reads.
-static int load_into(FILE* fp, const char* path, Fasta* f) {
+static int load_into(FILE* fp, const char* path, size_t chunk, Fasta* f) {
     enum { kLineStart, kSeq, kHead } st = kLineStart;
     FastaRec* cur = nullptr;
     std::string head;
-    size_t chunk = 64u << 20;
-    if (const char* e = std::getenv("MP_FASTA_CHUNK")) {  // tests: exercise chunk seams
-        const long v = std::atol(e);
-        if (v >= 4) chunk = (size_t)v;
-    }
     std::vector<uint8_t> buf(chunk + 4);
     size_t carry = 0;
     uint64_t consumed = 0;  // file offset of buf[0]
@@ -229,16 +224,20 @@ static int load_into(FILE* fp, const char* path, Fasta* f) {
     return MP_OK;
 }
 
-MP_EXPORT int mp_fasta_load(const char* path, void** out) {
+MP_EXPORT int mp_fasta_load(const char* path, void** out) { return mp_fasta_load_chunked(path, 0, out); }
+
+MP_EXPORT int mp_fasta_load_chunked(const char* path, uint64_t chunk_bytes, void** out) {
     if (!path || !out) return fail(MP_E_ARG, "mp_fasta_load: null pointer");
+    if (chunk_bytes && chunk_bytes < 4) return fail(MP_E_ARG, "mp_fasta_load: chunk_bytes must be >= 4");
     *out = nullptr;
+    const size_t chunk = chunk_bytes ? (size_t)chunk_bytes : (size_t)64 << 20;
     FILE* fp = std::fopen(path, "rb");
     if (!fp) return fail(MP_E_IO, std::string("cannot open FASTA file: ") + path);
     Fasta* f = new (std::nothrow) Fasta();
     int rc = f ? MP_OK : fail(MP_E_NOMEM, "mp_fasta_load: out of host memory");
     if (!rc) {
         try {
-            rc = load_into(fp, path, f);
+            rc = load_into(fp, path, chunk, f);
         } catch (const std::bad_alloc&) {
             rc = fail(MP_E_NOMEM, "mp_fasta_load: out of host memory");
         }

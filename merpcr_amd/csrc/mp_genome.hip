@@ -198,56 +198,83 @@ static int put_device_bytes(Genome* g, uint32_t seq, uint64_t offset, const uint
 
 using namespace mp;
 
-MP_EXPORT int mp_genome_create(int32_t device, uint32_t n_seq, const uint64_t* seq_len, void** out) {
-    if (!out || (n_seq && !seq_len)) return fail(MP_E_ARG, "mp_genome_create: null pointer");
-    *out = nullptr;
-    Genome* g = new Genome();
-    g->device = device;
+// Host layout of a sequence set: each sequence padded to a multiple of 64 bases.
+static int layout(Genome* g, uint32_t n_seq, const uint64_t* seq_len) {
+    for (uint32_t s = 0; s < n_seq; ++s)
+        if (seq_len[s] >= 0xFFFFFFFFull) return fail(MP_E_ARG, "sequence longer than 2^32-2 bases is not supported");
     g->n_seq = n_seq;
     g->len.assign(seq_len, seq_len + n_seq);
     g->base.resize(n_seq);
     uint64_t off = 0;
     for (uint32_t s = 0; s < n_seq; ++s) {
-        if (g->len[s] >= 0xFFFFFFFFull) {
-            free_genome(g);
-            return fail(MP_E_ARG, "sequence longer than 2^32-2 bases is not supported");
-        }
         g->base[s] = off;
         off += round_up(g->len[s], 64);
     }
     g->total = off;
-    int rc = MP_OK;
-    do {
-        if (hipSetDevice(device) != hipSuccess) { rc = fail(MP_E_HIP, "hipSetDevice failed"); break; }
-        const uint64_t w2 = off / 32 + 4, w1 = off / 64 + 4;
+    return MP_OK;
+}
+
+// Device planes for the current layout (reused when they fit), padding and
+// unwritten bases marked ambiguous, run index emptied.
+static int place(Genome* g) {
+    const uint64_t off = g->total;
+    const uint64_t w2 = off / 32 + 4, w1 = off / 64 + 4;
+    if (off > g->plane_cap || !g->g2) {
+        hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv);
+        g->g2 = g->gexc = g->ginv = nullptr;
+        g->plane_cap = 0;
         if (hipMalloc(&g->g2, w2 * 8) != hipSuccess || hipMalloc(&g->gexc, w1 * 8) != hipSuccess ||
-            hipMalloc(&g->ginv, w1 * 8) != hipSuccess ||
-            hipMalloc(&g->d_base, std::max<uint64_t>(n_seq, 1) * 8) != hipSuccess ||
-            hipMalloc(&g->d_len, std::max<uint64_t>(n_seq, 1) * 8) != hipSuccess ||
-            hipMalloc(&g->d_counter, 64) != hipSuccess || hipMalloc(&g->d_ucount, 64) != hipSuccess) {
-            rc = fail(MP_E_NOMEM, "mp_genome_create: device allocation failed");
-            break;
-        }
-        g->dev_bytes = w2 * 8 + 2 * w1 * 8;
-        if (hipMemset(g->d_ucount, 0, 64) != hipSuccess || hipMemset(g->g2, 0, w2 * 8) != hipSuccess ||
-            hipMemset(g->gexc, 0xFF, w1 * 8) != hipSuccess ||
-            hipMemset(g->ginv, 0xFF, w1 * 8) != hipSuccess) {
-            rc = fail(MP_E_HIP, "mp_genome_create: memset failed");
-            break;
-        }
-        if (n_seq && (hipMemcpy(g->d_base, g->base.data(), n_seq * 8, hipMemcpyHostToDevice) != hipSuccess ||
-                      hipMemcpy(g->d_len, g->len.data(), n_seq * 8, hipMemcpyHostToDevice) != hipSuccess)) {
-            rc = fail(MP_E_HIP, "mp_genome_create: upload failed");
-            break;
-        }
-        rc = grow_runs(g, 1 << 16);
-    } while (0);
+            hipMalloc(&g->ginv, w1 * 8) != hipSuccess)
+            return fail(MP_E_NOMEM, "mp_genome: device allocation failed");
+        g->plane_cap = off;
+    }
+    if (g->n_seq > g->seq_cap || !g->d_base) {
+        hipFree(g->d_base); hipFree(g->d_len);
+        g->d_base = g->d_len = nullptr;
+        g->seq_cap = 0;
+        const uint64_t n = std::max<uint64_t>(g->n_seq, 1);
+        if (hipMalloc(&g->d_base, n * 8) != hipSuccess || hipMalloc(&g->d_len, n * 8) != hipSuccess)
+            return fail(MP_E_NOMEM, "mp_genome: device allocation failed");
+        g->seq_cap = (uint32_t)n;
+    }
+    if (!g->d_counter && (hipMalloc(&g->d_counter, 64) != hipSuccess || hipMalloc(&g->d_ucount, 64) != hipSuccess))
+        return fail(MP_E_NOMEM, "mp_genome: device allocation failed");
+    g->dev_bytes = (g->plane_cap / 32 + 4) * 8 + 2 * (g->plane_cap / 64 + 4) * 8 + g->xr_cap * 9;
+    if (hipMemset(g->d_ucount, 0, 64) != hipSuccess || hipMemset(g->g2, 0, w2 * 8) != hipSuccess ||
+        hipMemset(g->gexc, 0xFF, w1 * 8) != hipSuccess || hipMemset(g->ginv, 0xFF, w1 * 8) != hipSuccess)
+        return fail(MP_E_HIP, "mp_genome: memset failed");
+    if (g->n_seq && (hipMemcpy(g->d_base, g->base.data(), g->n_seq * 8, hipMemcpyHostToDevice) != hipSuccess ||
+                     hipMemcpy(g->d_len, g->len.data(), g->n_seq * 8, hipMemcpyHostToDevice) != hipSuccess))
+        return fail(MP_E_HIP, "mp_genome: upload failed");
+    g->n_xr = 0;
+    g->has_u = false;
+    g->sealed = false;
+    return grow_runs(g, 1 << 16);
+}
+
+MP_EXPORT int mp_genome_create(int32_t device, uint32_t n_seq, const uint64_t* seq_len, void** out) {
+    if (!out || (n_seq && !seq_len)) return fail(MP_E_ARG, "mp_genome_create: null pointer");
+    *out = nullptr;
+    Genome* g = new Genome();
+    g->device = device;
+    int rc = layout(g, n_seq, seq_len);
+    if (!rc && hipSetDevice(device) != hipSuccess) rc = fail(MP_E_HIP, "hipSetDevice failed");
+    if (!rc) rc = place(g);
     if (rc) {
         free_genome(g);
         return rc;
     }
     *out = g;
     return MP_OK;
+}
+
+MP_EXPORT int mp_genome_reset(void* genome, uint32_t n_seq, const uint64_t* seq_len) {
+    Genome* g = (Genome*)genome;
+    if (!g || (n_seq && !seq_len)) return fail(MP_E_ARG, "mp_genome_reset: null pointer");
+    MP_HIP_CHECK(hipSetDevice(g->device));
+    int rc = layout(g, n_seq, seq_len);
+    if (!rc) rc = place(g);
+    return rc;
 }
 
 MP_EXPORT int mp_genome_put_device(void* genome, uint32_t seq, uint64_t offset, const uint8_t* dev_bytes,

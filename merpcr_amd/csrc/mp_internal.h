@@ -160,6 +160,8 @@ struct Genome {
     uint64_t staging_cap = 0;
     bool sealed = false;
     uint64_t dev_bytes = 0;
+    uint64_t plane_cap = 0;   // padded bases the planes hold
+    uint32_t seq_cap = 0;     // sequences d_base / d_len hold
 };
 
 struct Search {
@@ -186,6 +188,11 @@ struct Search {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, evt = nullptr;
     uint32_t* bucket = nullptr;  // device sort: bucket counts, offsets, cursors
     bool sort_crowded = false;   // a device-sort bucket overflowed: later runs go to rocPRIM
+    mp_search_options opt{};     // kernel-path selection (all zero = automatic)
+    uint32_t pair_per_cu = 0;    // resident pair_kernel blocks per CU (occupancy query at create)
+    uint32_t dense_per_cu = 0;   // resident dense_kernel blocks per CU
+    size_t dense_lds = 0;        // dense_kernel dynamic LDS bytes
+    uint64_t n_regrowths = 0;    // list regrowths over the handle's life (tests)
 };
 
 // ---------------------------------------------------------------- device helpers
@@ -308,6 +315,7 @@ inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 int sort_hits(Search* s, uint64_t n, hipStream_t st);
 bool sort_hits_device_ok(const Search* s);
 int sort_hits_device(Search* s, hipStream_t st);  // hit count read on the device, writes s->out
+int alloc_sort_buckets(Search* s);                // the device sort's bucket arrays (at create)
 constexpr int kSortOverflow = 6;                  // counters[6]: a device-sort bucket overflowed
 int sort_runs(Genome* g, hipStream_t st);
 

@@ -24,41 +24,10 @@
 //      wave (primer_ok: bit-sliced accept planes, exception bases resolved through the
 //      run index; lanes split the amplicon-end offsets) and emit 128-bit order keys.
 #include <algorithm>
-#include <cstdlib>
 #include <utility>
 
 #include "mp_internal.h"
 
-// Timing-only ablation builds (scripts/ablate.py); 0 in the product library.
-//   1: no drain (seed stage only)   2: no global filter probe (hash-based stand-in)
-//   3: neither                      4: drain stops after the bucket lookup
-//   5: fingerprint only (survivors are counted, not pair-checked)
-//   6: pair kernel stops after loading the record   7: pair kernel skips the primer-2 compares
-//   8: pair kernel skips its final hit flush          9: pair kernel never writes hits
-//  10: pair kernel stages synthetic words instead of loading the genome
-//  12: ranked scan (W 11-13): LDS prefilter only (no level-2 probes, no drain)
-//  17: pair kernel reports its slowest batch (ticks, phase-1 ticks, staged, kept survivors)
-//  18: pair kernel launched twice (the second runs with warm caches)
-//  19: recs, rank and planes streamed once before the pair kernel (warm caches/TLB)
-//  20/21: scan kernel reports its longest / summed wave time (ticks) as the survivor count
-//  16: the survivor count reports the bucket-tail reference slots instead
-//  15: exception bases count as mismatches without a character lookup
-//  13/14: pair kernel reports its longest / summed wave time (wall-clock ticks) as the
-//      survivor count
-#ifndef MP_ABLATE
-#define MP_ABLATE 0
-#endif
-// Genome planes are streamed once per launch: non-temporal loads keep them from
-// evicting the seed-table lines the probes re-read from L2.
-#ifndef MP_NT_STREAM
-#define MP_NT_STREAM 0
-#endif
-// 32-bit fingerprint path for the common bucket head (seed at the primer start, plain
-// primer, at most 16 bases after the seed) and a wave-uniform skip of the owned-range
-// test when the whole super-step is owned.
-#ifndef MP_FASTFP
-#define MP_FASTFP 1
-#endif
 // survivors per pair-check batch (lanes of the prologue); smaller batches spread the
 // per-survivor loop over more waves
 #ifndef MP_PBATCH
@@ -128,9 +97,6 @@ constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
 constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;  // pair_kernel batch counters, 8 x 256 B
 constexpr int kSchedBase = kPairQBase + 8 * kStatStride;  // scan super-step chunk counters, 8 x 256 B
 constexpr size_t kCounterBytes = (size_t)(kSchedBase + 8 * kStatStride) * 8;
-#ifndef MP_PDYN
-#define MP_PDYN 1
-#endif
 #ifndef MP_PDYN_BATCH
 #define MP_PDYN_BATCH 16
 #endif
@@ -230,9 +196,6 @@ __device__ __forceinline__ bool chunk_ok(const ScanArgs& a, uint64_t G, uint32_t
     const uint64_t inside = sp_lt(len);
     uint64_t mmv = ~match & inside;
     if (len < 32) ex &= ~(0xFFFFFFFFu >> len);
-#if MP_ABLATE == 15  // timing only: exception bases count as mismatches, no lookups
-    if (ex) mmv |= spread32(ex) & inside;
-#else
     if (ex && !a.I) {
         // literal compare (I=0): where the primer base is one of A/C/G/T (a plane bit set),
         // a genome exception character (never exactly A/C/G/T) cannot equal it -- a
@@ -242,7 +205,6 @@ __device__ __forceinline__ bool chunk_ok(const ScanArgs& a, uint64_t G, uint32_t
         ex &= ~compress_even(acgt);
     }
     if (ex) mmv = exception_mismatches(a, ex, gpos_c, ch_c, mmv);
-#endif
     uint64_t prot;
     if (plus) {
         const int64_t a0 = (int64_t)L - a.X - (int64_t)c;  // first protected local position
@@ -348,29 +310,12 @@ __device__ __forceinline__ void stage_try_hit(const ScanArgs& a, HitStage& S, in
     wave_sync_lds();
     if (lane == 0) S.n = at + (uint32_t)__popcll(m);
     wave_sync_lds();
-#if MP_ABLATE == 9
-    if (S.n >= 64) {
-        wave_sync_lds();
-        if (lane == 0) S.n = 0;
-        wave_sync_lds();
-    }
-#else
     if (S.n >= 64) stage_flush(a, S, lane);
-#endif
 }
 
-// Pair-check staging per survivor (MP_PSTAGE2): kPW 2-bit words, kPE exception words and
+// Pair-check staging per survivor: kPW 2-bit words, kPE exception words and
 // the four primer-2 accept planes, [slot][survivor] in the wave's LDS.  At M=50 and
 // primers of <= 25 bases every survivor fits (the tries span <= 125 bases).
-#ifndef MP_PSTAGE2
-#define MP_PSTAGE2 1
-#endif
-#ifndef MP_PPRIO  // wave priority during the pair-check prologue (0 = off)
-#define MP_PPRIO 0
-#endif
-#ifndef MP_P1X  // timing only: 1 = staging loads read a fixed word instead of the genome
-#define MP_P1X 0
-#endif
 constexpr int kPW = 6, kPE = 4, kPSlots = kPW + kPE + 4;
 static_assert(MP_PBATCH <= 64, "pair-check batch is one survivor per lane");
 
@@ -391,10 +336,7 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
 // the windows, else through the accept planes.  The reference's try order 0, -1, +1,
 // ... is restored by the device sort through try_rank(d).
 __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_surv, uint32_t batch, int lane,
-                                 HitStage& S, uint64_t* __restrict__ pst, uint64_t* dbg = nullptr) {
-#if MP_PPRIO
-    __builtin_amdgcn_s_setprio(MP_PPRIO);  // prologue: a short dependent load chain
-#endif
+                                 HitStage& S, uint64_t* __restrict__ pst) {
     const uint64_t i = base + (uint64_t)lane;
     uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
     if ((uint32_t)lane < batch && i < n_surv) v = a.surv[i];
@@ -412,14 +354,7 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         rk = a.rank[rec];
     }
     const uint32_t k = (uint32_t)(gk - sbase);
-#if MP_ABLATE == 17
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint64_t t_rec = wall_clock64();
-#endif
     keep = keep && n - k - r.l1 >= r.l2;
-#if MP_ABLATE == 6
-    keep = keep && r.l1 == 0xFFFFFFFFu;
-#endif
     uint32_t e = 0;
     int hi = 0;
     if (r.size > n - k) {
@@ -429,7 +364,6 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         hi = (int)min<uint32_t>((uint32_t)a.M, n - k - e);
     }
     const int lo = (int)smax64(0, smin64(a.M, (int64_t)e - r.l1 - r.l2));
-#if MP_PSTAGE2
     // Staged survivors: primer 2 within 32 bases and every try inside kPW 2-bit words and
     // kPE exception words.  The lane loads its survivor's words and primer-2 planes now,
     // in parallel with the primer-1 compare, into the wave's LDS stage ([slot][lane], so
@@ -444,36 +378,17 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         fast = keep && r.l2 <= 32u && wl - w0 < (uint64_t)kPW && el - e0 < (uint64_t)kPE;
         if (fast) {
 #pragma unroll
-#if MP_P1X == 3  // timing only: nothing loaded
-            for (int t = 0; t < kPSlots; ++t) pst[t * MP_PBATCH + lane] = w0 + t;
-#else
-            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[MP_P1X == 1 ? (t & 1) : w0 + t] : 0ull;
+            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[w0 + t] : 0ull;
 #pragma unroll
-            for (int t = 0; t < kPE; ++t) pst[(kPW + t) * MP_PBATCH + lane] = e0 + t <= el ? a.gexc[MP_P1X == 1 ? (t & 1) : e0 + t] : 0ull;
-            const uint64_t* pp = a.planes + (MP_P1X == 2 ? 0ull : (uint64_t)r.p2_pl * 4);
+            for (int t = 0; t < kPE; ++t) pst[(kPW + t) * MP_PBATCH + lane] = e0 + t <= el ? a.gexc[e0 + t] : 0ull;
+            const uint64_t* pp = a.planes + (uint64_t)r.p2_pl * 4;
 #pragma unroll
             for (int t = 0; t < 4; ++t) pst[(kPW + kPE + t) * MP_PBATCH + lane] = pp[t];
-#endif
         }
     }
     wave_sync_lds();
-#endif
-#if MP_ABLATE == 17
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint64_t t_stage = wall_clock64();
-#endif
     if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);
     uint64_t todo = __ballot(keep);
-#if MP_PPRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
-#if MP_ABLATE == 17
-    dbg[0] = wall_clock64();
-    dbg[1] = t_rec;
-    dbg[2] = t_stage;
-#else
-    (void)dbg;
-#endif
     while (todo) {
         const int j = (int)__builtin_ctzll(todo);
         todo &= todo - 1;
@@ -484,7 +399,6 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         const int jlo = (int)rl32((uint32_t)lo, j), jhi = (int)rl32((uint32_t)hi, j);
         const int ntry = jlo + jhi + 1;
         const uint64_t P0 = jgk + je - jl2 - (uint32_t)jlo;            // global start of the first try
-#if MP_PSTAGE2
         if (rl32((uint32_t)fast, j)) {
             const uint64_t* sj = pst + j;
             const uint64_t Q0 = sj[(kPW + kPE) * MP_PBATCH], Q1 = sj[(kPW + kPE + 1) * MP_PBATCH];
@@ -525,7 +439,6 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
             }
             continue;
         }
-#endif
         const uint64_t last = P0 + (uint64_t)(ntry - 1) + jl2 - 1;     // last base any try reads
         const uint64_t wlast = (last >> 5) + 1, elast = (last >> 6) + 1;
         uint64_t sw = ~0ull, se = ~0ull;  // staged word bases (wave-uniform)
@@ -549,13 +462,8 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
                     (hi_pos >> 6) + 1 > se + 63) {
                     sw = lo_pos >> 5;
                     se = lo_pos >> 6;
-#if MP_ABLATE == 10
-                    gw = sw * 0x9E3779B97F4A7C15ull + (uint64_t)lane;
-                    ew = 0;
-#else
                     gw = sw + (uint64_t)lane <= wlast ? a.g2[sw + (uint64_t)lane] : 0ull;
                     ew = se + (uint64_t)lane <= elast ? a.gexc[se + (uint64_t)lane] : 0ull;
-#endif
                 }
                 if ((c >> 5) != pchunk) {
                     pchunk = c >> 5;
@@ -578,9 +486,6 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
                 const uint32_t ex = (uint32_t)((es ? (y0 << es) | (y1 >> (64 - es)) : y0) >> 32);
                 const int len = (int)min(32u, jl2 - c);
                 const uint32_t exl = len >= 32 ? ex : ex & ~(0xFFFFFFFFu >> len);
-#if MP_ABLATE == 7
-                ok = ok && (G != ex || q == 0);
-#else
                 // plain primer 2: one XOR/popcount; a genome exception base is a certain
                 // mismatch under the literal rule (I=0), else the lanes need the lookup
                 if (plain2 && (!a.I || __all(!inb || exl == 0))) {
@@ -590,21 +495,16 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
                 } else if (inb && ok) {
                     ok = chunk_ok(a, G, ex, Q0, Q1, Q2, Q3, q, jch + c, len, c, jl2, false, mm);
                 }
-#endif
             }
             stage_try_hit(a, S, lane, inb && ok, jgk, jrk, d);
         }
     }
 }
 
-#ifndef MP_DPP_SCAN
-#define MP_DPP_SCAN 1
-#endif
 // Inclusive wave64 prefix sum.  DPP form: row_shr 1/2/4/8 within each 16-lane row, then
 // row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- six VALU ops with no LDS round
 // trip, where the shuffle form is six dependent ds_bpermute waits.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#if MP_DPP_SCAN
     (void)lane;
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
@@ -613,14 +513,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
-#else
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(v, o, 64);
-        if (lane >= o) v += y;
-    }
-    return v;
-#endif
 }
 
 __device__ __forceinline__ void wave_sync() { wave_sync_lds(); }
@@ -629,7 +521,7 @@ __device__ __forceinline__ void wave_sync() { wave_sync_lds(); }
 // LDS left beside the 128 KiB prefilter (160 KiB per CU) holds 1008 per wave; a denser
 // super-step is drained in rounds.
 constexpr uint32_t kSeedQ = 1008;
-// kMode 1 with MP_RANKQ: the level-2 probe already read each seed's rank word, so the queue
+// kMode 1 with 1: the level-2 probe already read each seed's rank word, so the queue
 // carries the key rank beside the offset (6 B per seed) and the drain skips the rank word.
 constexpr uint32_t kSeedQR = 340;
 struct WaveLds {
@@ -642,17 +534,11 @@ struct WaveLds {
     };
 };
 static_assert(sizeof(WaveLds) <= 2048, "per-wave LDS beside the 128 KiB prefilter");
-#ifndef MP_RANKQ
-#define MP_RANKQ 1
-#endif
 #ifndef MP_L2SLOTS
 #define MP_L2SLOTS 12
 #endif
 // level 2 through a wave-wide LDS list of the positives (full-lane probes) instead of
 // per-lane slots
-#ifndef MP_L2WAVE
-#define MP_L2WAVE 1
-#endif
 
 
 // The current super-step as the wave holds it: lane L owns bases [base + 32L,
@@ -691,9 +577,7 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
                                           uint64_t Gpos, uint32_t expos, bool reuse, bool& exact) {
     const uint32_t k = pos - e.hash_off;
     act = act && pos >= e.hash_off && (uint64_t)k + e.l1 <= n;
-#if MP_FASTFP
     if (!R.owned)
-#endif
         act = act && sbase + k >= a.g_lo && sbase + k < a.g_hi;
     uint64_t G = Gpos;
     uint32_t ex = expos;
@@ -701,7 +585,6 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
         const bool in_regs = k >= R.base && k - R.base < kSuper;
         window_from_regs(a, R, sbase, act ? k : R.base, !act || in_regs, G, ex);
     }
-#if MP_FASTFP
     // seed at the primer start and a plain primer: bases [0, W) matched exactly, so only
     // the <= 16 bases after the seed can mismatch -- one 32-bit XOR/popcount
     const uint32_t W = (uint32_t)a.W;
@@ -724,7 +607,6 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
         k_out = k;
         return true;
     }
-#endif
     if (!act) return false;
     ++ncand;
     if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) return false;
@@ -914,10 +796,6 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
             hva = la && bucket_head<kMode>(a, ha, e0a);
             hvb = lb && bucket_head<kMode>(a, hb, e0b);
         }
-#if MP_ABLATE == 4
-        ncand += (hva && e0a.rec == 0xFFFFFFFFu) + (hvb && e0b.rec == 0xFFFFFFFFu);
-        continue;
-#endif
         heads_and_tails<kMode, kInline>(a, R, sbase, n, hva, pa, e0a, Ga, xa, lane, ncand, C, TC);
         if (b + 64 < qn) heads_and_tails<kMode, kInline>(a, R, sbase, n, hvb, pb, e0b, Gb, xb, lane, ncand, C, TC);
     }
@@ -983,7 +861,7 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
                       make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
 }
 
-// drain_seeds for the ranked queue (kMode 1, MP_RANKQ): the head comes straight from the
+// drain_seeds for the ranked queue (kMode 1, 1): the head comes straight from the
 // queued key rank -- one dependent load (the 8-B head) per seed instead of two.
 template <bool kInline, bool kDefer>
 __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
@@ -1002,13 +880,11 @@ __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs&
         uint32_t xa, xb;
         window_from_regs(a, R, sbase, pa, true, Ga, xa);
         window_from_regs(a, R, sbase, pb, true, Gb, xb);
-#if MP_ABLATE != 4
         if constexpr (kDefer) {  // compact heads tested here, full-head buckets to tail_kernel
             drain_compact(a, R, sbase, n, la, pa, ca, Ga, xa, lane, ncand, C, TC);
             if (b + 64 < qn) drain_compact(a, R, sbase, n, lb, pb, cb, Gb, xb, lane, ncand, C, TC);
             continue;
         }
-#endif
         const uint32_t ha = (uint32_t)(Ga >> shw), hb = (uint32_t)(Gb >> shw);
         Entry e0a{}, e0b{};
         if (la) {
@@ -1019,11 +895,6 @@ __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs&
             if (cb.y & kHead8Full) e0b = a.dents[qb];
             else e0b = head8_entry(cb, hb, (uint32_t)a.W);
         }
-#if MP_ABLATE == 4
-        ncand += (la && e0a.rec == 0xFFFFFFFFu) + (lb && e0b.rec == 0xFFFFFFFFu) + (uint32_t)(Ga == 1) + (uint32_t)(Gb == 1) +
-                 (uint32_t)(xa == 3) + (uint32_t)(xb == 3);
-        continue;
-#endif
         heads_and_tails<1, kInline>(a, R, sbase, n, la, pa, e0a, Ga, xa, lane, ncand, C, TC);
         if (b + 64 < qn) heads_and_tails<1, kInline>(a, R, sbase, n, lb, pb, e0b, Gb, xb, lane, ncand, C, TC);
     }
@@ -1105,10 +976,6 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
                     const uint32_t h = kmer_top<T>(d0, d1, d2) >> shw;
                     const uint32_t fi = kMode == 1 ? h : filter_index(h, a.filt_log2);
                     const bool on = (lmask >> (31 - T)) & 1u;
-#if MP_ABLATE == 2 || MP_ABLATE == 3
-                    gw[T] = (h * 2654435761u) >> 27 == 0 ? 0xFFFFFFFFu : 0u;
-                    (void)on; (void)fi;
-#else
                     // kMode 1: the rank words' bits -- the same lines the drain reads next
                     // for the seeds that pass (a separate bits-only bitmap measured slower).
                     // Byte offset (h >> 5) * 8 straight from the funnel, masked to 0 by the
@@ -1121,7 +988,6 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
                     } else {
                         gw[T] = a.filt[on ? (fi >> 5) : 0u];
                     }
-#endif
                 }()),
              ...);
         }(std::make_integer_sequence<int, 32>{});
@@ -1170,15 +1036,12 @@ __device__ __forceinline__ uint32_t kmer_dyn(uint32_t d0, uint32_t d1, uint32_t 
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
 // ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
 // The next super-step's plane words are loaded before the current one is processed.
-// Dynamic super-step order (MP_SDYN): with a static round-robin the last wave of the scan
-// ended 15% after the mean (c3: 2.76 vs 2.36 ms; MP_ABLATE 20/21) -- super-steps differ in
+// Dynamic super-step order: with a static round-robin the last wave of the scan
+// ended 15% after the mean (c3: 2.76 vs 2.36 ms, per-wave timers) -- super-steps differ in
 // cost and a CU's younger waves get fewer issue slots.  Each XCD (blocks x, x+8, ...) owns
 // a contiguous 1/8 of the super-steps in chunks of kSChunk; its waves take one chunk each,
 // then claim further chunks from the XCD's counter one chunk ahead (the claim's latency
 // hides behind the chunk's work; ~9 atomics per microsecond per counter on c3).
-#ifndef MP_SDYN
-#define MP_SDYN 1
-#endif
 #ifndef MP_SCHUNK
 #define MP_SCHUNK 8
 #endif
@@ -1230,9 +1093,6 @@ template <int kMode, bool kInline, int kK = 1, bool kDefer = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
-#if MP_ABLATE == 20 || MP_ABLATE == 21
-    const uint64_t t_k0 = wall_clock64();
-#endif
 
     // stage the seed prefilter in LDS (once per persistent workgroup)
     for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)
@@ -1250,12 +1110,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     SurvChunk C{0, 64u, 0u};
     SurvChunk TC{0, 64u, 0u};
 
-#if MP_SDYN
     SuperSched sch;
     uint64_t ss = sch.first(a.counters, n_supers, w, kWaves, lane);
-#else
-    uint64_t ss = (uint64_t)blockIdx.x * kWaves + (uint64_t)w;
-#endif
     // span of the super-step being prefetched, cached in registers (wave-uniform): the
     // common path of the prefetch issues only the four plane loads, no waits
     SeqSpan pf{};
@@ -1277,17 +1133,10 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     };
     auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& iv) {
         const uint64_t j = pf_sbase + pf.p_al + (x - pf.super0) * kSuper + (uint64_t)lane * kLanePos;
-#if MP_NT_STREAM
-        w0 = __builtin_nontemporal_load(&a.g2[j >> 5]);
-        w1 = __builtin_nontemporal_load(&a.g2[(j >> 5) + 1]);
-        const uint64_t v0 = __builtin_nontemporal_load(&a.ginv[j >> 6]);
-        const uint64_t v1 = __builtin_nontemporal_load(&a.ginv[(j >> 6) + 1]);
-#else
         w0 = a.g2[j >> 5];
         w1 = a.g2[(j >> 5) + 1];
         const uint64_t v0 = a.ginv[j >> 6];
         const uint64_t v1 = a.ginv[(j >> 6) + 1];
-#endif
         const uint32_t sh = (uint32_t)(j & 32);  // branch-free: both loads always issue
         iv = (v0 << sh) | ((v1 >> (63 - sh)) >> 1);
     };
@@ -1311,29 +1160,14 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
         const uint32_t okm = window_ok_mask(R.iv, W) &
                              bit_range((int)sp.p_lo - (int)pb, (int)smin64((int64_t)sp.p_hi - pb, 32));
-#if MP_SDYN
         const uint64_t nx = sch.next(ss, n_supers, lane);
         (void)stride;
-#else
-        const uint64_t nx = ss + stride;
-#endif
-#if MP_RANKQ
         if constexpr (kMode == 1) {
-#if MP_L2WAVE
             // level 2, wave-compacted: the wave's LDS-positive windows go into the LDS list
             // {key, offset} (the queue's arrays), then every lane probes one list entry per
             // pass -- full lanes, all passes' rank-word loads in flight together -- and the
             // seeds are compacted back into the same arrays as {offset, rank}
             const uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
-#if MP_ABLATE == 12
-            ncand += (uint32_t)__popc(rem);  // level 1 only
-            if (nx < n_supers) {
-                locate(nx);
-                words(nx, nw0, nw1, niv);
-            }
-            ss = nx;
-            continue;
-#endif
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
@@ -1394,103 +1228,15 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         qn += (uint32_t)__popcll(hm);
                     }
                 }
-#if MP_ABLATE == 1 || MP_ABLATE == 3
-                ncand += qn;
-#else
                 wave_sync();
                 if (qn) drain_ranked<kInline, kDefer>(a, R, sbase, n, qn, lane, ncand, L, C, TC);
-#endif
                 wave_sync();
                 r0 += kSeedQR;
             } while (r0 < tot);
             (void)first;
             ss = nx;
             continue;
-#else
-            // level 2 compacted: the LDS-positive windows, MP_L2SLOTS per lane per pass, each
-            // one rank-word load; a seed's rank goes into the queue beside its offset
-            // a lane with more than K positives takes further passes; their seeds join the
-            // same queue, drained once (in rounds only when it fills)
-            constexpr int K = MP_L2SLOTS;
-            uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
-#if MP_ABLATE == 12
-            ncand += (uint32_t)__popc(rem);  // level 1 only
-            rem = 0;
-            if (nx < n_supers) {
-                locate(nx);
-                words(nx, nw0, nw1, niv);
-            }
-            ss = nx;
-            continue;
-#endif
-            bool first = true;
-            uint32_t qfill = 0;  // queued seeds not yet drained (wave-uniform)
-            do {
-                uint32_t sb[K];
-                uint2 rw[K];
-#pragma unroll
-                for (int q = 0; q < K; ++q) {
-                    const bool on = rem != 0;
-                    const uint32_t i = on ? (uint32_t)__clz(rem) : 0u;
-                    rem = on ? rem & ~(0x80000000u >> i) : rem;
-                    const uint32_t h = kmer_dyn(d0, d1, d2, i) >> shw;
-                    sb[q] = on ? (i << 5) | (h & 31u) : 0xFFFFFFFFu;
-                    rw[q] = a.rk[on ? (h >> 5) : 0u];
-                }
-                if (first) {  // the next super-step's words, issued after this step's probes
-                    first = false;
-                    if (nx < n_supers) {
-                        locate(nx);
-                        words(nx, nw0, nw1, niv);
-                    }
-                }
-                uint32_t hs = 0;
-#pragma unroll
-                for (int q = 0; q < K; ++q)
-                    hs |= (uint32_t)(sb[q] != 0xFFFFFFFFu && ((rw[q].x >> (sb[q] & 31u)) & 1u)) << q;
-                const uint32_t c = (uint32_t)__popc(hs);
-                const uint32_t incl = wave_incl_scan(c, lane);
-                const uint32_t total = rl32(incl, 63);
-#if MP_ABLATE == 1 || MP_ABLATE == 3
-                ncand += total;
-#else
-                // queue this pass's seeds; drain when the queue is full or after the last pass
-                const bool last = !__any(rem != 0);
-                uint32_t done = 0;  // this pass's seeds already queued
-                for (;;) {
-                    const uint32_t wr = min(kSeedQR - qfill, total - done);
-                    if (wr) {
-                        uint32_t qi = incl - c;  // this lane's first seed in the pass
-#pragma unroll
-                        for (int q = 0; q < K; ++q) {
-                            if ((hs >> q) & 1u) {
-                                if (qi - done < wr) {
-                                    const uint32_t bq = sb[q] & 31u;
-                                    L.rq.q[qfill + qi - done] = (uint16_t)((uint32_t)lane * kLanePos + (sb[q] >> 5));
-                                    L.rq.r[qfill + qi - done] = rw[q].y + (uint32_t)__popc(rw[q].x & ((1u << bq) - 1u));
-                                }
-                                ++qi;
-                            }
-                        }
-                        done += wr;
-                        qfill += wr;
-                    }
-                    if (qfill == kSeedQR || (last && done == total && qfill)) {
-                        wave_sync();
-                        drain_ranked<kInline, kDefer>(a, R, sbase, n, qfill, lane, ncand, L, C, TC);
-                        wave_sync();
-                        qfill = 0;
-                    }
-                    if (done == total) break;
-                }
-                rem = last ? 0u : rem;
-#endif
-            } while (__any(rem != 0));
-            ss = nx;
-            continue;
-#endif
         }
-#endif
         uint32_t hits = probe32<kMode>(a, s_lf, d0, d1, d2, shw, okm, [&] {
             // prefetch the next super-step's words (issued after this step's probes)
             if (nx < n_supers) {
@@ -1502,9 +1248,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint32_t c = (uint32_t)__popc(hits);
         const uint32_t incl = wave_incl_scan(c, lane);
         const uint32_t total = rl32(incl, 63);
-#if MP_ABLATE == 1 || MP_ABLATE == 3
-        ncand += total;
-#else
         // queue this super-step's seed offsets (lane-major = window order) and drain them
         for (uint32_t rb = 0; rb < total; rb += kSeedQ) {
             uint32_t m = hits, q = incl - c;
@@ -1518,18 +1261,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             drain_seeds<kMode, kInline>(a, R, sbase, n, min(total - rb, kSeedQ), lane, ncand, L, C, TC);
             wave_sync();
         }
-#endif
         ss = nx;
     }
     close_chunked(a.surv, a.surv_cap, lane, C);
     close_chunked<2>(a.tails, a.tails_cap, lane, TC);
     // candidate statistics
     add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);
-#if MP_ABLATE == 20  // survivors stat = latest wave end (ticks after its block started)
-    if (lane == 0) atomicMax(&a.counters[5], (unsigned long long)(wall_clock64() - t_k0));
-#elif MP_ABLATE == 21  // survivors stat = sum over waves
-    if (lane == 0) atomicAdd(&a.counters[5], (unsigned long long)(wall_clock64() - t_k0));
-#endif
 }
 
 // Dense seeds (W <= kDenseMaxW, e.g. W=8: ~95% of windows hit one of 62k keys, 3.2 records
@@ -1615,12 +1352,8 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     uint32_t ncand = 0;
     SurvChunk C{0, 64u, 0u};
 
-#if MP_SDYN
     SuperSched sch;
     uint64_t ss = sch.first(a.counters, n_supers, w, kDenseWaves, lane);
-#else
-    uint64_t ss = (uint64_t)blockIdx.x * kDenseWaves + (uint64_t)w;
-#endif
     SeqSpan pf{};
     pf.super0 = 1;
     uint64_t pf_end = 0, pf_sbase = 0;
@@ -1668,12 +1401,8 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         // otherwise; under I=0 such a base reads as 'A' and can only hide a mismatch, and U
         // compares as T under I=1)
         const uint32_t slowm = a.I ? ~window_ok_mask(iv, 16u) : 0u;
-#if MP_SDYN
         const uint64_t nx = sch.next(ss, n_supers, lane);
         (void)stride;
-#else
-        const uint64_t nx = ss + stride;
-#endif
         if (nx < n_supers) {  // next super-step's words, in flight during this one
             locate(nx);
             words(nx, nw0, nw1, niv);
@@ -1858,9 +1587,6 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
 #endif
 __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
-#if MP_ABLATE == 17
-    const uint64_t t_k0 = wall_clock64();
-#endif
     if (blockIdx.x == 0 && threadIdx.x < 64) {  // statistics of the scan / tail kernels (add_stats)
         unsigned long long c = a.counters[kStatBase + threadIdx.x * kStatStride];
         unsigned long long v = a.counters[kStatBase + threadIdx.x * kStatStride + 1];
@@ -1890,10 +1616,6 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
     const uint64_t rounds = umax64(1, (n_surv + waves * MP_PBATCH - 1) / (waves * MP_PBATCH));
     const uint32_t batch = (uint32_t)umax64(4, umin64(MP_PBATCH, (n_surv + waves * rounds - 1) / (waves * rounds)));
     const uint64_t stride = waves * batch;
-#if MP_ABLATE == 13 || MP_ABLATE == 14
-    const uint64_t t_start = wall_clock64();
-#endif
-#if MP_PDYN
     // Dynamic batches: survivors cost very different amounts (primer-1 failures leave in
     // the prologue), so a static split left the slowest wave ~1.7x the mean.  Each XCD
     // (blocks x, x+8, ...) owns 1/8 of the batches: its waves take one batch each, then
@@ -1905,48 +1627,16 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
         const uint32_t x = blockIdx.x % g;
         const uint64_t lo_b = nbat * x / g, hi_b = nbat * (x + 1) / g;
         const uint64_t nw_x = (uint64_t)((gridDim.x - x + g - 1u) / g) * 4u;  // waves of this group
-#if MP_PDYN == 2  // every batch claimed from the counter, the first too
-        uint64_t bi;
-        {
-            unsigned long long t = 0;
-            if (lane == 0) t = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
-            bi = lo_b + (uint64_t)__shfl((long long)t, 0, 64);
-        }
-        const uint64_t nw_d = 0;
-#else
         uint64_t bi = lo_b + (uint64_t)(blockIdx.x / g) * 4u + (threadIdx.x >> 6);
         const uint64_t nw_d = nw_x;
-#endif
         while (bi < hi_b) {
-#if MP_ABLATE == 17  // survivors stat = slowest batch: ticks << 40 | phase-1 ticks << 16 | fast << 8 | kept
-            uint64_t dbg[3] = {0, 0, 0};
-            const uint64_t t0 = wall_clock64();
-            pair_check_batch(a, bi * db, n_surv, db, lane, S, s_pst[threadIdx.x >> 6], dbg);
-            const uint64_t t1 = wall_clock64();
-            if (lane == 0)
-                atomicMax(&a.counters[5], (unsigned long long)(((t1 - t0) << 40) | (umin64((dbg[1] - t0) >> 4, 0x1FFF) << 27) |
-                                                               (umin64((dbg[2] - t0) >> 4, 0x1FFF) << 14) |
-                                                               umin64((dbg[0] - t0) >> 4, 0x3FFF)));
-            (void)t_k0;
-#else
             pair_check_batch(a, bi * db, n_surv, db, lane, S, s_pst[threadIdx.x >> 6]);
-#endif
             unsigned long long t = 0;
             if (lane == 0) t = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
             bi = lo_b + nw_d + (uint64_t)__shfl((long long)t, 0, 64);
         }
     }
     (void)stride;
-#else
-    for (uint64_t b = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * batch; b < n_surv; b += stride)
-        pair_check_batch(a, b, n_surv, batch, lane, S, s_pst[threadIdx.x >> 6]);
-#endif
-#if MP_ABLATE == 13  // survivors stat = longest wave (wall-clock ticks)
-    if (lane == 0) atomicMax(&a.counters[5], (unsigned long long)(wall_clock64() - t_start));
-#elif MP_ABLATE == 14  // survivors stat = sum over waves
-    if (lane == 0) atomicAdd(&a.counters[5], (unsigned long long)(wall_clock64() - t_start));
-#endif
-#if MP_ABLATE != 8 && MP_ABLATE != 9
     // the block's four stages leave with one returning atomic: one per wave at the end of
     // the kernel would serialise ~5k atomics on the hit counter (~88 per microsecond)
     __syncthreads();
@@ -1965,17 +1655,6 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
             a.hit_lo[off + i] = S.lo[i];
         }
     }
-#endif
-}
-
-// Timing experiment (MP_ABLATE 19): stream a table once so its pages and lines are warm.
-__global__ void warm_kernel(const uint4* __restrict__ p, uint64_t n16, unsigned long long* sink) {
-    uint32_t acc = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 v = p[i];
-        acc ^= v.x ^ v.y ^ v.z ^ v.w;
-    }
-    if (acc == 0x9E3779B9u) atomicAdd(sink, 1ull);
 }
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
@@ -2051,9 +1730,27 @@ static int alloc_tails(Search* s, uint64_t cap) {
     return MP_OK;
 }
 
+constexpr uint64_t kDefaultHitCap = 1 << 16, kDefaultSurvCap = 1 << 20, kDefaultTailCap = 1 << 18;
+
 }  // namespace mp
 
 using namespace mp;
+
+MP_EXPORT int mp_search_set_options(void* search, const mp_search_options* opt) {
+    Search* s = (Search*)search;
+    if (!s || !opt) return fail(MP_E_ARG, "mp_search_set_options: null pointer");
+    if (opt->tails < MP_TAILS_AUTO || opt->tails > MP_TAILS_KERNEL || opt->sort < MP_SORT_AUTO ||
+        opt->sort > MP_SORT_RADIX128 || opt->sort_bucket_bits < 0 || opt->sort_bucket_bits > 16 ||
+        opt->pair_blocks_per_cu < 0)
+        return fail(MP_E_ARG, "mp_search_set_options: option out of range");
+    MP_HIP_CHECK(hipSetDevice(s->genome->device));
+    s->opt = *opt;
+    s->sort_crowded = false;
+    int rc = alloc_hits(s, opt->hit_cap ? opt->hit_cap : kDefaultHitCap);
+    if (!rc) rc = alloc_surv(s, opt->surv_cap ? opt->surv_cap : kDefaultSurvCap);
+    if (!rc) rc = alloc_tails(s, opt->tail_cap ? opt->tail_cap : kDefaultTailCap);
+    return rc;
+}
 
 MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
     if (!table || !genome || !out) return fail(MP_E_ARG, "mp_search_create: null pointer");
@@ -2071,15 +1768,24 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
         if (hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess ||
             s->n_cu <= 0)
             s->n_cu = 256;
+        int occ = 0;  // persistent pair check: every resident block slot once
+        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel, 256, 0) == hipSuccess && occ > 0)
+                             ? (uint32_t)occ : 5u;
+        s->dense_lds = (sizeof(uint2) + sizeof(uint32_t)) *
+                       std::max<size_t>(1, ((size_t)1 << (2 * std::min<int>(t->prm.wordsize, kDenseMaxW))) / 32);
+        occ = 0;
+        s->dense_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dense_kernel, kDenseBlock, s->dense_lds) ==
+                               hipSuccess && occ > 0) ? (uint32_t)occ : 1u;
         if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
             hipEventCreate(&s->ev2) != hipSuccess || hipEventCreate(&s->ev3) != hipSuccess ||
             hipEventCreate(&s->evt) != hipSuccess) {
             rc = fail(MP_E_HIP, "event creation failed");
             break;
         }
-        rc = alloc_hits(s, 1 << 16);
-        if (!rc) rc = alloc_surv(s, 1 << 20);
-        if (!rc) rc = alloc_tails(s, 1 << 18);
+        rc = alloc_hits(s, kDefaultHitCap);
+        if (!rc) rc = alloc_surv(s, kDefaultSurvCap);
+        if (!rc) rc = alloc_tails(s, kDefaultTailCap);
+        if (!rc) rc = alloc_sort_buckets(s);
     } while (0);
     if (rc) {
         free_search(s);
@@ -2159,8 +1865,8 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.has_u = g->has_u ? 1 : 0;
     a.seq_base = g->d_base; a.seq_len = g->d_len;
     a.spans = s->spans; a.n_spans = n_real_spans;
-    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M; a.defer_full = t->defer_full;
-    if (const char* f = std::getenv("MP_DEFER")) a.defer_full = a.defer_full && f[0] != '0';  // tests: old drain
+    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
+    a.defer_full = t->defer_full && !s->opt.no_defer;
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
@@ -2180,13 +1886,16 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     // pair kernel reads the survivor count on the device.  A list that overflowed is
     // grown and the whole pass rerun.
     bool inl = t->n_rec > t->n_keys + t->n_keys / 4;  // bucket tails inline vs tail_kernel
-    if (const char* f = std::getenv("MP_TAILS")) {    // tests: force one tail path
-        if (f[0] == 'i') inl = true;
-        if (f[0] == 'k') inl = false;
-    }
-    // W <= kDenseMaxW: dense_kernel (rank bitmap in LDS, lane-serial bucket walk)
-    bool dense = (uint32_t)t->prm.wordsize <= kDenseMaxW;
-    if (const char* f = std::getenv("MP_DENSE")) dense = dense && f[0] != '0';  // tests: old path
+    if (s->opt.tails == MP_TAILS_INLINE) inl = true;
+    if (s->opt.tails == MP_TAILS_KERNEL) inl = false;
+    // W <= kDenseMaxW: dense_kernel (bucket index in LDS, filter-word octs)
+    const bool dense = (uint32_t)t->prm.wordsize <= kDenseMaxW && !s->opt.no_dense;
+    const size_t dense_lds = s->dense_lds;
+    const uint32_t dense_per_cu = s->dense_per_cu;
+    // A list that overflowed is grown and its producers rerun: the scan (and tail_kernel)
+    // when survivors or bucket-tail references were lost, only the pair check and the sort
+    // when just the hit list was too small.
+    bool rescan = true;
     for (int attempt = 0; attempt < 4; ++attempt) {
         a.hit_hi = s->keys;
         a.hit_lo = s->keys + s->cap;
@@ -2196,54 +1905,46 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         a.surv_cap = s->surv_cap;
         a.tails = s->tails;
         a.tails_cap = s->tails_cap;
-        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
-        MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-        if (dense) {
-            const size_t lds = (sizeof(uint2) + sizeof(uint32_t)) * std::max<size_t>(1, ((size_t)1 << (2 * t->prm.wordsize)) / 32);
-            int per_cu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dense_kernel, kDenseBlock, lds) != hipSuccess ||
-                per_cu < 1)
-                per_cu = 1;
-            const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
-                                                                (uint64_t)s->n_cu * (uint64_t)per_cu);
-            hipLaunchKernelGGL(dense_kernel, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
-        } else if (inl) {
-            if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
-            else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
-            else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
-            else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
-        } else {
-            if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
-            else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
-                hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
-            else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);
-            else if (t->filt_direct && a.defer_full)
-                hipLaunchKernelGGL((scan_kernel<1, false, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);
-            else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, false, 1>), dim3(grid), dim3(kBlock), 0, st, a);
-            else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
-        }
-        MP_HIP_CHECK(hipGetLastError());
-        MP_HIP_CHECK(hipEventRecord(s->evt, st));
-        if (!dense && !inl && (t->max_bucket > 1 || a.defer_full)) {  // defer_full: single-record full heads too
-            hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
+        if (rescan) {
+            MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
+            MP_HIP_CHECK(hipEventRecord(s->ev0, st));
+            if (dense) {
+                const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
+                                                                    (uint64_t)s->n_cu * (uint64_t)dense_per_cu);
+                hipLaunchKernelGGL(dense_kernel, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
+            } else if (inl) {
+                if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+                else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
+            } else {
+                if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
+                    hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct && a.defer_full)
+                    hipLaunchKernelGGL((scan_kernel<1, false, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, false, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+                else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
+            }
             MP_HIP_CHECK(hipGetLastError());
+            MP_HIP_CHECK(hipEventRecord(s->evt, st));
+            if (!dense && !inl && (t->max_bucket > 1 || a.defer_full)) {  // defer_full: single-record full heads too
+                hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
+                MP_HIP_CHECK(hipGetLastError());
+            }
+        } else {  // hit list regrown: counters of the pair check and the sort only
+            MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long), st));
+            MP_HIP_CHECK(hipMemsetAsync(s->counters + kSortOverflow, 0, sizeof(unsigned long long), st));
+            MP_HIP_CHECK(hipMemsetAsync(s->counters + kPairQBase, 0, 8 * kStatStride * sizeof(unsigned long long), st));
+            MP_HIP_CHECK(hipEventRecord(s->ev0, st));
+            MP_HIP_CHECK(hipEventRecord(s->evt, st));
         }
-#if MP_ABLATE == 19
-        hipLaunchKernelGGL(warm_kernel, dim3(512), dim3(256), 0, st, (const uint4*)t->recs, (uint64_t)t->n_rec * 2, s->counters + 7);
-        hipLaunchKernelGGL(warm_kernel, dim3(512), dim3(256), 0, st, (const uint4*)t->rank, (uint64_t)t->n_rec / 4, s->counters + 7);
-        hipLaunchKernelGGL(warm_kernel, dim3(512), dim3(256), 0, st, (const uint4*)t->planes, t->planes_words / 2, s->counters + 7);
-#endif
         MP_HIP_CHECK(hipEventRecord(s->ev1, st));
-        int pair_per_cu = 0;  // persistent: every resident block slot once
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pair_per_cu, pair_kernel, 256, 0) != hipSuccess ||
-            pair_per_cu < 1)
-            pair_per_cu = 5;
-        if (const char* f = std::getenv("MP_PAIR_PER_CU")) pair_per_cu = std::max(1, std::min(pair_per_cu, std::atoi(f)));  // timing
-        hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * (uint32_t)pair_per_cu), dim3(256), 0, st, a);
+        const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
+                                                               : s->pair_per_cu;
+        hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(256), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
-#if MP_ABLATE == 18  // timing only: the pair kernel twice (warm second launch; hits doubled)
-        hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * (uint32_t)pair_per_cu), dim3(256), 0, st, a);
-#endif
         MP_HIP_CHECK(hipEventRecord(s->ev2, st));
         if (dev_sort) {  // hit order on the device count: no host round trip before the sort
             const int src = sort_hits_device(s, st);
@@ -2252,21 +1953,25 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         }
         MP_HIP_CHECK(hipMemcpyAsync(cnt, s->counters, sizeof(cnt), hipMemcpyDeviceToHost, st));
         MP_HIP_CHECK(hipStreamSynchronize(st));
+        if (rescan) {
+            MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
+            MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
+        }
         if (cnt[2] <= s->surv_cap && cnt[4] <= s->tails_cap && cnt[0] <= s->cap) break;
+        ++s->n_regrowths;
         int rc = MP_OK;
+        rescan = cnt[4] > s->tails_cap || cnt[2] > s->surv_cap;
         if (cnt[4] > s->tails_cap) rc = alloc_tails(s, cnt[4] + cnt[4] / 4 + 1024);
         if (!rc && cnt[2] > s->surv_cap) rc = alloc_surv(s, cnt[2] + cnt[2] / 2 + 1024);
         // hits are produced from the survivors only when those all fit
-        if (!rc && cnt[2] <= s->surv_cap && cnt[0] > s->cap) rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
+        if (!rc && !rescan && cnt[0] > s->cap) rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
         if (rc) return rc;
     }
     if (cnt[2] > s->surv_cap || cnt[4] > s->tails_cap || cnt[0] > s->cap)
         return fail(MP_E_STATE, "mp_search_run: list overflow after growth");
-    MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
-    MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
     MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     s->n_candidates = cnt[1];
-    s->n_survivors = (MP_ABLATE == 13 || MP_ABLATE == 14 || MP_ABLATE == 17 || MP_ABLATE == 20 || MP_ABLATE == 21) ? cnt[5] : MP_ABLATE == 16 ? cnt[4] : cnt[3];
+    s->n_survivors = cnt[3];
     const uint64_t nh = cnt[0];
     if (dev_sort && cnt[kSortOverflow]) s->sort_crowded = true;
     if (!dev_sort || cnt[kSortOverflow]) {  // 128-bit order key, or a crowded bucket: rocPRIM
@@ -2323,6 +2028,13 @@ MP_EXPORT int mp_search_last_stats(void* search, float* scan_ms, uint64_t* n_win
     if (scan_ms) *scan_ms = s->scan_ms;
     if (n_windows) *n_windows = s->n_windows;
     if (n_candidates) *n_candidates = s->n_candidates;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_search_regrowths(void* search, uint64_t* n_regrowths) {
+    Search* s = (Search*)search;
+    if (!s || !n_regrowths) return fail(MP_E_ARG, "mp_search_regrowths: null pointer");
+    *n_regrowths = s->n_regrowths;
     return MP_OK;
 }
 

@@ -7,7 +7,6 @@
 // -- SURVEY 8a-8.  Hits carry it as a 128-bit key (hi = global k coordinate,
 // lo = rank(record) << 32 | try rank) and two stable LSD passes order them.
 #include <algorithm>
-#include <cstdlib>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -221,7 +220,12 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
 bool sort_hits_device_ok(const Search* s) {
     const unsigned hi_bits = bits_for(s->genome->total);
     const unsigned try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
-    return hi_bits + s->table->rank_bits + try_bits <= 64 && !std::getenv("MP_SORT2") && !std::getenv("MP_SORT_ROCPRIM");
+    return hi_bits + s->table->rank_bits + try_bits <= 64 && s->opt.sort == MP_SORT_AUTO;
+}
+
+int alloc_sort_buckets(Search* s) {
+    if (!s->bucket) MP_HIP_CHECK(hipMalloc(&s->bucket, (3ull << kMaxBucketBits) * 4 + 16));
+    return MP_OK;
 }
 
 int sort_hits_device(Search* s, hipStream_t st) {
@@ -232,11 +236,12 @@ int sort_hits_device(Search* s, hipStream_t st) {
     // ~32 hits per bucket at the buffer's capacity (the count is not known on the host)
     unsigned bb = bits_for(s->cap / 32);
     bb = std::min(std::max(bb, 6u), kMaxBucketBits);
-    if (const char* f = std::getenv("MP_SORT_BUCKET_BITS")) bb = (unsigned)std::max(1, std::atoi(f));  // tests
+    if (s->opt.sort_bucket_bits > 0) bb = std::min((unsigned)s->opt.sort_bucket_bits, kMaxBucketBits);
     bb = std::min(bb, key_bits);
     const unsigned shift = key_bits - bb;
     const uint32_t nb = 1u << bb;
-    if (!s->bucket) MP_HIP_CHECK(hipMalloc(&s->bucket, (3ull << kMaxBucketBits) * 4 + 16));
+    const int arc = alloc_sort_buckets(s);
+    if (arc) return arc;
     uint32_t* cnt = s->bucket;
     uint32_t* off = cnt + (1u << kMaxBucketBits);
     uint32_t* cursor = off + (1u << kMaxBucketBits) + 1;
@@ -266,7 +271,7 @@ int sort_hits(Search* s, uint64_t n, hipStream_t st) {
     // try ranks are <= 2M (engine.py:540-560: d in [-M, M])
     const unsigned try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
     const unsigned low_bits = s->table->rank_bits + try_bits;
-    if (hi_bits + low_bits <= 64 && !std::getenv("MP_SORT2")) {  // MP_SORT2: tests of the two-pass path
+    if (hi_bits + low_bits <= 64 && s->opt.sort != MP_SORT_RADIX128) {
         // the whole order key fits 64 bits: one keys-only radix sort
         const unsigned blocks = (unsigned)((n + 255) / 256);
         hipLaunchKernelGGL(pack_keys, dim3(blocks), dim3(256), 0, st, hi, lo, n, try_bits, low_bits, s->tmp_lo);

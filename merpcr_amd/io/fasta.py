@@ -23,7 +23,7 @@ from typing import List
 
 from ..core.models import FASTARecord
 
-logger = logging.getLogger(__name__)
+logger = logging.getLogger("merpcr.io.fasta")  # the reference module's logger name
 
 KEEP_CHARS = "ABCDGHKMNRSTVWXYabcdghkmnrstvwxyſ"
 _DROP = re.compile("[^" + re.escape(KEEP_CHARS) + "]+")
@@ -45,7 +45,7 @@ class FASTALoader:
     """Loads FASTA files into FASTARecord lists (reference: io/fasta.py:15-71)."""
 
     @staticmethod
-    def load_file(filename: str) -> List[FASTARecord]:
+    def load_file(filename: str, _chunk_bytes: int = 0) -> List[FASTARecord]:
         if not _utf8_locale():
             return FASTALoader.load_file_py(filename)
         from .. import _native
@@ -55,7 +55,7 @@ class FASTALoader:
             return []
         logger.info(f"Reading FASTA file: {filename}")
         records = []
-        for defline, seq in _native.fasta_read(filename):
+        for defline, seq in _native.fasta_read(filename, _chunk_bytes):
             records.append(FASTARecord(defline=defline, sequence=seq.decode("utf-8")))
         logger.info(f"Loaded {len(records)} sequences in {time.time() - start:.2f} seconds")
         return records

@@ -4,6 +4,7 @@ Run only in the build container, where the reference is importable:
 
     PYTHONPATH=/root/reference/src python3 tests/golden/make_golden.py
     PYTHONPATH=/root/reference/src python3 tests/golden/make_golden.py --chunked   # -T N corpus
+    PYTHONPATH=/root/reference/src python3 tests/golden/make_golden.py --errors    # error paths
 
 The reference never ships with this repository and never runs on the GPU box;
 what is committed is data only: the seeded inputs each case was built from and
@@ -253,6 +254,107 @@ def run_ref(params, sts_text, records=None, fasta_text=None, threads=1):
     return res
 
 
+class _Capture(logging.Handler):
+    def __init__(self):
+        super().__init__(logging.DEBUG)
+        self.msgs = []
+
+    def emit(self, record):
+        self.msgs.append([record.levelname, record.getMessage()])
+
+
+def run_ref_err(params, sts_text, records, threads=1):
+    """run_ref for the error paths: the exception type the reference raises from
+    load_sts_file or search (if any), the output it wrote before it, and its log lines
+    (minus timings)."""
+    MerPCR, FASTARecord = _ref()
+    cap = _Capture()
+    lg = logging.getLogger("merpcr")
+    lg.addHandler(cap)
+    lg.setLevel(logging.DEBUG)
+    res = {}
+    try:
+        eng = MerPCR(threads=threads, **params)
+        with tempfile.TemporaryDirectory() as td:
+            sp = os.path.join(td, "x.sts")
+            with open(sp, "w") as fh:
+                fh.write(sts_text)
+            try:
+                res["load_ok"] = eng.load_sts_file(sp)
+                res["load_error"] = None
+            except Exception as e:  # noqa: BLE001 - record the reference's exception type
+                res["load_ok"] = None
+                res["load_error"] = type(e).__name__
+            res["n_records"] = len(eng.sts_records)
+            res["keys"] = sorted(eng.sts_table)
+            if res["load_ok"]:
+                recs = [FASTARecord(defline=d, sequence=s) for d, s in records]
+                op = os.path.join(td, "out.txt")
+                try:
+                    res["n_hits"] = eng.search(recs, op)
+                    res["search_error"] = None
+                except Exception as e:  # noqa: BLE001
+                    res["search_error"] = type(e).__name__
+                import gc
+                gc.collect()  # the reference leaves its output file to be closed by the collector
+                with open(op) as fh:
+                    res["output"] = fh.read()
+    finally:
+        lg.removeHandler(cap)
+    res["log"] = [m for m in cap.msgs if " seconds" not in m[1] and not m[1].startswith("Reading STS file")]
+    return res
+
+
+def error_cases(rng):
+    """Characters beyond U+00FF (after upper()) in primers and sequences: the reference's
+    scode[ord(c)] lookups raise IndexError when the hash or the scan reaches them
+    (engine.py:345, 472, 497); characters that upper-case into Latin-1 do not."""
+    MerPCR, _ = _ref()
+    odd = ["\u03a9", "\u00ff", "\u0131", "\u00df", "\u00e9", "\u017f", "\u4e2d", "\u00b5", "N", "n", "U"]
+    kats = []
+    for _ in range(400):
+        W = rng.randint(3, 12)
+        L = rng.randint(0, 24)
+        p = "".join(rng.choice(odd) if rng.random() < 0.12 else rng.choice("ACGTacgt") for _ in range(L))
+        try:
+            r = list(MerPCR(wordsize=W)._hash_value(p))
+        except IndexError:
+            r = "IndexError"
+        kats.append([p, W, r])
+    cases = []
+    base = "".join(rng.choice("ACGT") for _ in range(3000))
+    for i in range(60):
+        W = rng.choice([4, 6, 8, 11])
+        prm = dict(wordsize=W, margin=rng.choice([0, 5, 50]), mismatches=rng.randint(0, 2), three_prime_match=1,
+                   iupac_mode=rng.randint(0, 1), default_pcr_size=240)
+        lines = []
+        for s in range(rng.randint(1, 4)):
+            a = rng.randrange(0, 2500)
+            p1 = base[a:a + rng.randint(W, 22)]
+            q = a + rng.randint(100, 300)
+            p2 = _rc(base[q - rng.randint(W, 22):q])
+            if i % 3 == 0 and rng.random() < 0.6:  # an odd character in a primer
+                which = rng.choice([0, 1])
+                pr = list(p1 if which == 0 else p2)
+                pr[rng.randrange(len(pr))] = rng.choice(odd[:8])
+                if which == 0:
+                    p1 = "".join(pr)
+                else:
+                    p2 = "".join(pr)
+            lines.append(f"S{s}\t{p1}\t{p2}\t{q - a}\tal{s}")
+        recs = []
+        for r in range(rng.randint(1, 3)):
+            s = list(base[rng.randrange(0, 500):][:rng.randint(0, 2500)])
+            if i % 3 == 1 and s and rng.random() < 0.5:  # an odd character in a sequence
+                s[rng.randrange(len(s))] = rng.choice(odd[:8])
+            if i % 3 == 2 and rng.random() < 0.3:  # a short sequence (<= W) with one
+                s = [rng.choice(odd[:8])] + list(base[:rng.randint(0, W - 1)])
+            recs.append([f">r{r} d", "".join(s)])
+        sts = "\n".join(lines) + "\n"
+        cases.append({"params": prm, "sts_text": sts, "records": recs, **run_ref_err(prm, sts, recs)})
+    return {"hash": kats, "cases": cases}
+
+
 def unit_kats(rng):
     MerPCR, _ = _ref()
     kat = {"hash": [], "revcomp": [], "compare": [], "pcr_size": []}
@@ -366,6 +468,15 @@ def chunked_cases():
 
 
 def main():
+    if "--errors" in sys.argv:
+        erng = random.Random(2026)
+        obj = error_cases(erng)
+        print("errors: hash raises", sum(k[2] == "IndexError" for k in obj["hash"]),
+              "load raises", sum(c["load_error"] is not None for c in obj["cases"]),
+              "search raises", sum(bool(c.get("search_error")) for c in obj["cases"]), file=sys.stderr)
+        with gzip.open(os.path.join(HERE, "errors.json.gz"), "wt") as fh:
+            json.dump(obj, fh, separators=(",", ":"))
+        return
     if "--chunked" in sys.argv:
         logging.disable(logging.CRITICAL)
         with gzip.open(os.path.join(HERE, "chunked.json.gz"), "wt") as fh:

@@ -31,9 +31,9 @@ def _expected(path):
         return type(e)
 
 
-def _native_read(path):
+def _native_read(path, chunk=0):
     try:
-        return [(r.defline, r.sequence, r.label) for r in FASTALoader.load_file(path)]
+        return [(r.defline, r.sequence, r.label) for r in FASTALoader.load_file(path, _chunk_bytes=chunk)]
     except Exception as e:  # noqa: BLE001
         return type(e)
 
@@ -57,11 +57,9 @@ def _random_text(rng):
     return "".join(out)
 
 
-@pytest.mark.parametrize("chunk", [None, "4", "7", "64"])
-def test_native_matches_python_loop(tmp_path, monkeypatch, chunk):
-    if chunk:
-        monkeypatch.setenv("MP_FASTA_CHUNK", chunk)
-    rng = random.Random(1234 + (int(chunk) if chunk else 0))
+@pytest.mark.parametrize("chunk", [0, 4, 7, 64])
+def test_native_matches_python_loop(tmp_path, chunk):
+    rng = random.Random(1234 + chunk)
     p = str(tmp_path / "x.fa")
     for i in range(300):
         text = _random_text(rng)
@@ -70,7 +68,7 @@ def test_native_matches_python_loop(tmp_path, monkeypatch, chunk):
         with open(p, "wb") as fh:
             fh.write(text.encode("utf-8"))
         exp = _expected(p)
-        got = _native_read(p)
+        got = _native_read(p, chunk)
         if isinstance(exp, type) and exp is IndexError:  # '>' alone: FASTARecord label
             assert got is IndexError
             continue
@@ -91,15 +89,14 @@ def test_invalid_utf8_raises_like_reference(tmp_path, blob):
         FASTALoader.load_file(p)
 
 
-def test_crlf_split_across_chunks(tmp_path, monkeypatch):
+def test_crlf_split_across_chunks(tmp_path):
     p = str(tmp_path / "crlf.fa")
     text = ">s1 d\r\nACGT\r\n\r\nGG\r>s2\r\nTT\r\n"
     with open(p, "wb") as fh:
         fh.write(text.encode())
     exp = _expected(p)
     for c in range(4, len(text) + 2):
-        monkeypatch.setenv("MP_FASTA_CHUNK", str(c))
-        assert _native_read(p) == exp, c
+        assert _native_read(p, c) == exp, c
 
 
 def test_missing_and_empty(tmp_path):

@@ -72,15 +72,14 @@ def test_bundled_search_to_file():
     assert text == "L78833\t75823..76023\tAFM248yg9\t(D17S932)  Chr.17, 63.7 cM\t(-)\n"
 
 
-@pytest.mark.parametrize("bits", [None, "1", "4"])
-def test_dense_repeat_order(bits, monkeypatch):
+@pytest.mark.parametrize("bits", [0, 1, 4])
+def test_dense_repeat_order(bits):
     """15,936 hits on an 8 kbp repeat; with 2 forced device-sort buckets they overflow the
     per-bucket capacity and the rocPRIM fallback orders them, with 16 each bucket holds
     ~1,000 keys ranked in LDS."""
-    if bits:
-        monkeypatch.setenv("MP_SORT_BUCKET_BITS", bits)
     case = load_golden("repeat.json.gz")
     eng = _engine(case["params"])
+    eng.search_options = dict(sort_bucket_bits=bits)
     with tempfile.TemporaryDirectory() as td:
         assert _load_sts(eng, case["sts_text"], td)
         recs = _records(case, eng, td)
@@ -91,20 +90,19 @@ def test_dense_repeat_order(bits, monkeypatch):
 
 @pytest.mark.parametrize("tails", ["auto", "inline", "kernel"])
 @pytest.mark.parametrize("name", ["random_cases.json.gz", "special_cases.json.gz"])
-def test_golden_corpus(name, tails, monkeypatch):
+def test_golden_corpus(name, tails):
     """Every recorded reference case through the default kernels (dense_kernel for W <= 9),
     and again through scan_kernel with the multi-record bucket tails forced to each of its
-    two paths (MP_DENSE=0, MP_TAILS), with the two-pass hit ordering (MP_SORT2) and without
-    deferring full-head buckets to tail_kernel (MP_DEFER=0)."""
+    two paths, with the two-pass 128-bit hit ordering and without deferring full-head
+    buckets to tail_kernel (mp_search_options)."""
+    opts = {}
     if tails != "auto":
-        monkeypatch.setenv("MP_TAILS", tails)
-        monkeypatch.setenv("MP_DENSE", "0")
-        monkeypatch.setenv("MP_SORT2", "1")  # and the two-pass 128-bit hit ordering
-        monkeypatch.setenv("MP_DEFER", "0")  # and the drain that tests full heads itself
+        opts = dict(tails=tails, dense=False, sort="radix128", defer=False)
     cases = load_golden(name)["cases"]
     bad = []
     for i, case in enumerate(cases):
         eng = _engine(case["params"])
+        eng.search_options = opts
         with tempfile.TemporaryDirectory() as td:
             ok = _load_sts(eng, case["sts_text"], td)
             assert ok == case["load_ok"], i
@@ -117,16 +115,16 @@ def test_golden_corpus(name, tails, monkeypatch):
     assert not bad, bad[:3]
 
 
-@pytest.mark.parametrize("bits", ["1", "4"])
-def test_device_sort_crowded_buckets(bits, monkeypatch):
+@pytest.mark.parametrize("bits", [1, 4])
+def test_device_sort_crowded_buckets(bits):
     """The device-count bucket sort with forced coarse buckets: 2 buckets overflow the
     per-bucket LDS capacity on the larger cases (rocPRIM fallback), 16 buckets rank
     hundreds of keys per workgroup.  Every golden case must still match byte for byte."""
-    monkeypatch.setenv("MP_SORT_BUCKET_BITS", bits)
     bad = []
     for name in ("special_cases.json.gz", "random_cases.json.gz"):
         for i, case in enumerate(load_golden(name)["cases"][:200]):
             eng = _engine(case["params"])
+            eng.search_options = dict(sort_bucket_bits=bits)
             with tempfile.TemporaryDirectory() as td:
                 if not _load_sts(eng, case["sts_text"], td):
                     continue
@@ -252,15 +250,12 @@ def test_cli_threads_emulation(tmp_path):
 @pytest.mark.parametrize("W,n_sts,glen,N,I,iupac", [(8, 4000, 3_000_000, 1, 0, 0.0), (9, 6000, 2_000_000, 2, 1, 0.1),
                                                     (11, 20000, 4_000_000, 1, 1, 0.1),
                                                     (12, 40000, 4_000_000, 1, 0, 0.0)])  # > 65536 keys: 2-bit LDS filter
-def test_dense_tables_vs_c_oracle(tails, W, n_sts, glen, N, I, iupac, monkeypatch):
+def test_dense_tables_vs_c_oracle(tails, W, n_sts, glen, N, I, iupac):
     """Larger tables (multi-record buckets everywhere at W=8) through the default kernels
     and through scan_kernel with both tail paths, against the C oracle byte for byte, with
     planted amplicons and N runs."""
     from merpcr_amd import synth
     from oracle import c_oracle as C
-    if tails != "auto":
-        monkeypatch.setenv("MP_TAILS", tails)
-        monkeypatch.setenv("MP_DENSE", "0")
     sts = synth.make_sts(n_sts, seed=7, W=W, iupac=iupac)
     rng = np.random.default_rng(3)
     g = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, glen)].copy()
@@ -274,6 +269,8 @@ def test_dense_tables_vs_c_oracle(tails, W, n_sts, glen, N, I, iupac, monkeypatc
     seq = g.tobytes().decode("ascii")
     prm = dict(wordsize=W, mismatches=N, iupac_mode=I, margin=50)
     eng = MerPCR(**prm)
+    if tails != "auto":
+        eng.search_options = dict(tails=tails, dense=False)
     with tempfile.TemporaryDirectory() as td:
         assert _load_sts(eng, sts.text(), td)
     hits = eng.find_hits([FASTARecord(defline=">chrD", sequence=seq)])
@@ -369,7 +366,7 @@ def test_seed_queue_rounds(W):
 
 
 @pytest.mark.parametrize("N,X", [(0, 0), (1, 1), (2, 0)])
-def test_full_head_prefilter_buckets(N, X, monkeypatch):
+def test_full_head_prefilter_buckets(N, X):
     """Buckets of 2-4 records that share a primer-1 seed (kHead8Filt prefilter on the full
     8-B head for 1-3 records, plain deferral for 4), some also sharing the filter bases,
     with planted amplicons of every record: the deferring drain against the C oracle."""
@@ -404,3 +401,65 @@ def test_full_head_prefilter_buckets(N, X, monkeypatch):
     ref = C.search(table, [g], O.params(**prm), 8)
     assert len(ref) > 1000
     assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes()
+
+
+def test_forced_regrowth_is_identical():
+    """Survivor, bucket-tail and hit lists created one entry long (mp_search_options):
+    every list overflows, is regrown and its producers rerun; the output is byte-identical
+    to the default capacities and the regrowths are counted."""
+    sts_text, seq = _synthetic(21, 300, 300_000, 11, 1, 0)
+    recs = [FASTARecord(defline=">chrG", sequence=seq)]
+    ref_eng = MerPCR(wordsize=11, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(ref_eng, sts_text, td)
+    exp = _device_lines(ref_eng, recs)
+    for opts in (dict(hit_cap=1, surv_cap=1, tail_cap=1), dict(hit_cap=1),
+                 dict(hit_cap=1, surv_cap=1, tail_cap=1, tails="inline", dense=False)):
+        eng = MerPCR(wordsize=11, mismatches=1)
+        eng.search_options = opts
+        with tempfile.TemporaryDirectory() as td:
+            assert _load_sts(eng, sts_text, td)
+        assert _device_lines(eng, recs) == exp, opts
+        assert eng.last_search_stats["regrowths"] >= 1, opts
+    assert len(exp) > 100
+
+
+def test_handles_reused_across_searches():
+    """One engine, several search() calls of different sizes and record counts: the genome
+    and search handles are re-laid out (mp_genome_reset), the results equal a fresh engine's;
+    a repeated small search orders its hits in well under a millisecond."""
+    sts_text, seq = _synthetic(22, 200, 400_000, 11, 1, 0, nrun=True)
+    eng = MerPCR(wordsize=11, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    sets = [[seq], [seq[:50_000], seq[50_000:51_000]], [seq[100_000:]], ["ACGT" * 5, "", seq[:200_000]], [seq]]
+    for seqs in sets:
+        recs = [FASTARecord(defline=f">r{i}", sequence=s) for i, s in enumerate(seqs)]
+        fresh = MerPCR(wordsize=11, mismatches=1)
+        with tempfile.TemporaryDirectory() as td:
+            assert _load_sts(fresh, sts_text, td)
+        assert _device_lines(eng, recs) == _device_lines(fresh, recs)
+    small = [FASTARecord(defline=">s", sequence=seq[:120_000])]
+    eng.find_hits(small)
+    eng.find_hits(small)
+    assert eng.last_search_stats["order_ms"] < 1.0, eng.last_search_stats
+
+
+def test_latin1_primer_character_first_search():
+    """A Latin-1 primer character ('É', not IUPAC: literal equality) matched by the same
+    genome character: the first search after load_sts_file already finds the hit (its byte
+    code is registered before the genome is encoded), and repeated searches agree."""
+    p1, p2 = "ACGTTGCAAGCTTAGCÉA", "GGATCCTTAGGCATCAGG"
+    body = "".join(random.Random(5).choice("ACGT") for _ in range(400))
+    seq = body[:100] + p1 + body[100:250] + p2 + body[250:]  # the "+" record: p1 ... p2 literal
+    sts_text = f"LAT\t{p1}\t{p2}\t{len(p1) + 150 + len(p2)}\n"
+    prm = dict(wordsize=8, mismatches=0, margin=5)
+    eng = MerPCR(**prm)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    recs = [FASTARecord(defline=">lat", sequence=seq)]
+    table = O.load_sts_lines(sts_text.splitlines(True), 8, 240)
+    exp = O.search_lines([("lat", seq)], table, O.params(**prm))
+    assert len(exp) == 1
+    assert _device_lines(eng, recs) == exp
+    assert _device_lines(eng, recs) == exp

@@ -71,7 +71,7 @@ def _load(eng, path, native, caplog):
     caplog.clear()
     start = time.time()
     eng.sts_records, eng.sts_table, eng._sts_keys, eng.max_pcr_size = [], {}, [], 0
-    with caplog.at_level(logging.INFO, logger="merpcr_amd"):
+    with caplog.at_level(logging.INFO, logger="merpcr"):
         if native:
             ok = eng._load_sts_native(path, start)
         else:
