@@ -4,16 +4,17 @@ Workload (BASELINE.json metric "W=11 N=1"; configs[2]):
   c3 = 100k synthetic STS primer pairs vs a 3 Gbp human-size synthetic genome
        (24 records), W=11 N=1 M=50, every STS planted in both orientations.
 A step is one full pass of the hot path over the resident genome: seed scan +
-primer verify + pair-check kernel, device ordering of the hits and the hit-count
+primer verify + pair-check kernels, device ordering of the hits and the hit-count
 readback (mp_search_run); for N > 1 also the RCCL gatherv of every rank's hits
-to rank 0.  Inputs (seed table + packed genome) are resident in HBM before the
-timed region.  Multi-GPU: one process per GPU.  Default --scaling weak: the job is
-N genomes' worth of contigs, contig-sharded, one config-sized set of records per
-rank (each rank's contigs drawn from its own seed), so per-GPU work is fixed and
-`value` = all ranks' bases / the slowest rank's step time.  --scaling strong
-splits ONE genome's (sequence, k) space into equal contiguous owned ranges.
+to rank 0 (mp_comm_gather_hits, inside the library).  Inputs (seed table + packed
+genome) are resident in HBM before the timed region.  Multi-GPU: one process per
+GPU; torch.distributed (gloo) is only the control plane (RCCL unique id, barrier,
+max-over-ranks timing).  Default --scaling strong: ONE genome's (sequence, k) space
+split into N equal owned ranges (the metric's "contig-sharded 1->8"); --scaling weak
+gives every rank a config-sized contig set of its own.
 
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0; exits 1 if the GPU hit list differs from the CPU
+oracle's on the baseline sample.
 """
 
 from __future__ import annotations
@@ -34,15 +35,29 @@ METRIC = "genome bases scanned/sec (Gbp/s) + STS hits/sec, W=11 N=1, 1/2/4/8 MI3
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip parameters)
 BYTES_PER_BASE = 0.375       # 2-bit plane + 1-bit ambiguity plane, read once
 BYTES_PER_HIT = 16           # 128-bit order key written per raw hit
+N_SIMD, N_CU = 1024, 256     # MI355X: 256 CUs x 4 SIMD-32
+L2_REQ_PEAK = 34.5e12 / 128  # L2 bandwidth / 128-B line (MI355X_MICROARCH.md, L2): ~270G requests/s
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(workload: str):
-    """HBM bytes per scan launch from the newest committed PMC pass of this workload
-    (profiles/<tag>_pmc.json next to the bench line it was collected with), else None."""
+def host_cores() -> int:
+    """CPUs this job may use: the affinity mask, capped by a cgroup CPU quota if one is set."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(-(-int(q) // int(per)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def pmc_profile(workload: str):
+    """Newest committed PMC summary of this workload (profiles/<tag>_pmc.json next to the
+    bench line it was collected with), or (None, None)."""
     import glob
     best = None
     for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")):
@@ -55,14 +70,38 @@ def pmc_traffic(workload: str):
         except (OSError, ValueError, KeyError):
             continue
         if "hbm_traffic_bytes_per_launch" in d and (best is None or os.path.getmtime(f) > best[0]):
-            best = (os.path.getmtime(f), d["hbm_traffic_bytes_per_launch"], tag)
+            best = (os.path.getmtime(f), d, tag)
     return (best[1], best[2]) if best else (None, None)
 
 
-def cpu_baseline(eng, names, lens, buf, offs, cfg, hits_dev, budget_s: float, threads: int):
+def issue_bound(pmc: dict):
+    """Issue-side utilisation of the dominant kernel from its committed PMC passes:
+    VALU = SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (1024 SIMDs x kernel cycles),
+    kernel cycles = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs); LDS = LDS-array cycles
+    (SQ_LDS_IDX_ACTIVE) / (256 CUs x kernel cycles); the bank-conflict share of them; and the
+    L2 request rate against the ~270G/s line ceiling (34.5 TB/s / 128 B)."""
+    c = pmc.get("counters_mean_per_dispatch", {})
+    out = {}
+    cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    if cyc > 0 and "SQ_INSTS_VALU" in c:
+        out["valu_frac"] = round(c["SQ_INSTS_VALU"] * 2.0 / (N_SIMD * cyc), 4)
+    if cyc > 0 and "SQ_LDS_IDX_ACTIVE" in c:
+        out["lds_frac"] = round(c["SQ_LDS_IDX_ACTIVE"] / (N_CU * cyc), 4)
+    if c.get("SQ_LDS_IDX_ACTIVE"):
+        out["lds_bank_conflict_ratio"] = round(c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"], 4)
+    if "SQ_WAIT_ANY" in c and c.get("SQ_WAVE_CYCLES"):
+        out["wave_wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+    req = c.get("TCC_REQ_sum") or (c.get("TCC_HIT_sum", 0.0) + c.get("TCC_MISS_sum", 0.0))
+    dur = pmc.get("avg_duration_ns_trace")
+    if req and dur:
+        out["l2_req_per_launch"] = int(req)
+        out["l2_req_frac"] = round(req / (dur * 1e-9) / L2_REQ_PEAK, 4)
+    return out
+
+
+def cpu_baseline(eng, lens, buf, offs, cfg, hits_dev, budget_s: float, threads: int):
     """Time the C oracle (scalar restatement, `threads` pthreads over k ranges) on whole
     leading records of the same genome, and check its hits against the GPU's."""
-    import torch
     from oracle import c_oracle as C
     from oracle import epcr_oracle as O
 
@@ -85,23 +124,50 @@ def cpu_baseline(eng, names, lens, buf, offs, cfg, hits_dev, budget_s: float, th
     dt = time.time() - t
     mine = hits_dev[hits_dev["seq"] < nrec]
     parity = bool(len(mine) == len(ref) and mine.tobytes() == ref.tobytes())
-    # the reference algorithm itself, as plain per-base Python (oracle/epcr_oracle.py), on 1 Mbp
-    sub = probe[:1_000_000].tobytes().decode("ascii")
-    t = time.time()
-    O.scan_sequence(sub, table, prm)
-    py_rate = len(sub) / (time.time() - t)
     return {
         "value": round(nb / dt / 1e9, 6), "unit": "Gbp/s", "cores": threads, "kind": "port",
-        "sample": f"{nrec} whole leading record(s) = {nb / 1e6:.1f} Mbp of the same genome, same 100k-STS "
-                  f"table, C restatement of engine.py:453-642 (oracle/epcr_oracle.c), {threads} thread(s)",
+        "sample": f"{nrec} whole leading record(s) = {nb / 1e6:.1f} Mbp of the same genome, same STS "
+                  f"table, C restatement of engine.py:453-642 (oracle/epcr_oracle.c), {threads} thread(s) "
+                  f"= every CPU this job may use (affinity mask and cgroup quota)",
         "seconds": round(dt, 3), "hits": int(len(ref)),
         "parity_vs_gpu": parity,
-        "reference_algorithm_python_mbps": round(py_rate / 1e6, 3),
-    }
+    }, table, prm
+
+
+def reference_model(table, prm, buf, offs, lens, cores: int, budget_s: float):
+    """The reference's own execution model at -T <cores> (engine.py:380-434): the Python
+    restatement of the scan (oracle/epcr_oracle.py) over the reference's chunk plan of a
+    record prefix, one ProcessPool worker per chunk receiving the pickled table, pool start
+    included as in the reference.  The prefix is sized to ~budget_s from a one-core
+    calibration (no extrapolation: the figure is the measured prefix)."""
+    import concurrent.futures
+    import multiprocessing
+    from oracle import epcr_oracle as O
+
+    rec0 = buf[int(offs[0]):int(offs[0]) + lens[0]]
+    probe = rec0[:200_000].cpu().numpy().tobytes().decode("ascii")
+    t = time.time()
+    O.scan_sequence(probe, table, prm)
+    rate1 = len(probe) / max(time.time() - t, 1e-6)
+    n = int(min(100_000_000, lens[0], rate1 * cores * budget_s))
+    seq = rec0[:n].cpu().numpy().tobytes().decode("ascii")
+    plan = O.chunk_plan(n, cores, table.max_pcr_size, prm["margin"])
+    tasks = [(seq[o:o + ln], o, table, prm) for o, ln in plan]
+    t = time.time()
+    with concurrent.futures.ProcessPoolExecutor(max_workers=len(plan),
+                                                mp_context=multiprocessing.get_context("spawn")) as ex:
+        hits = sum(len(h) for h in ex.map(O.scan_chunk, tasks))
+    dt = time.time() - t
+    return {"value": round(n / dt / 1e6, 3), "unit": "Mbp/s", "cores": len(plan), "kind": "port",
+            "sample": f"first {n / 1e6:.1f} Mbp of record 0, {len(plan)} chunks (-T {cores} plan, engine.py:380-410), "
+                      f"one spawned worker per chunk, the table pickled into every task as the reference's bound-method submit does, pure-Python scan "
+                      f"(oracle/epcr_oracle.py restating engine.py:453-642)",
+            "seconds": round(dt, 3), "hits_with_chunk_duplicates": int(hits),
+            "one_core_mbps": round(rate1 / 1e6, 3)}
 
 
 def end_to_end(eng, table, names, lens, buf, offs, device, stream):
-    """One untimed-by-the-metric pass from host bytes to output text (SURVEY 8d t_e2e):
+    """One pass from host bytes to output text (SURVEY 8d t_e2e), not the metric:
     H2D + 2-bit pack + exception index (mp_genome_put/seal), search, hit fetch and the
     native formatter.  Filtered FASTA bytes start in host memory, as after FASTA load."""
     import torch
@@ -134,6 +200,43 @@ def end_to_end(eng, table, names, lens, buf, offs, device, stream):
                     "not the metric"}
 
 
+def end_to_end_file(sts_path, names, lens, buf, offs, cfg, device):
+    """The CLI from files: the genome written as FASTA (60-column lines), then
+    `python -m merpcr_amd sts fasta -O out` timed in a child process: FASTA parse
+    (mp_fasta_load), upload + pack, search, format and write.  Not the metric."""
+    import subprocess
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        fa = os.path.join(td, "g.fa")
+        t = time.time()
+        with open(fa, "wb") as fh:
+            for r, nm in enumerate(names):
+                s = buf[int(offs[r]):int(offs[r]) + lens[r]].cpu().numpy()
+                fh.write(f">{nm} synthetic\n".encode())
+                full = (len(s) // 60) * 60
+                body = np.empty((full // 60, 61), dtype=np.uint8)
+                body[:, :60] = s[:full].reshape(-1, 60)
+                body[:, 60] = 10
+                fh.write(body.tobytes())
+                if len(s) > full:
+                    fh.write(s[full:].tobytes() + b"\n")
+        write_s = time.time() - t
+        out = os.path.join(td, "hits.txt")
+        cmd = [sys.executable, "-m", "merpcr_amd", sts_path, fa, "-W", str(cfg["W"]), "-N", str(cfg["N"]),
+               "-M", str(cfg["M"]), "-I", str(cfg["I"]), "-O", out, "--device", str(device)]
+        t = time.time()
+        res = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
+        dt = time.time() - t
+        if res.returncode:
+            log(res.stderr[-2000:])
+            return {"error": f"CLI exit {res.returncode}"}
+        lines = sum(1 for _ in open(out, "rb"))
+        size = os.path.getsize(fa)
+    return {"seconds": round(dt, 3), "gbp_per_s": round(sum(lens) / dt / 1e9, 3), "fasta_bytes": size,
+            "hit_lines": lines, "fasta_write_s": round(write_s, 3),
+            "note": "python -m merpcr_amd on a 60-column FASTA file to an output file, child process wall "
+                    "time (interpreter start, FASTA parse, upload + pack, search, format, write); not the metric"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -142,12 +245,14 @@ def main():
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the config's genome and STS set")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cores))")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = every usable CPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ref-model", action="store_true", help="skip the Python ProcessPool (-T) line")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-bytes-to-output-text pass")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: each rank scans its own config-sized contig set (N x the genome); "
-                         "strong: one genome split in N owned ranges")
+    ap.add_argument("--e2e-file", action="store_true", help="also time the CLI from a FASTA file")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong: one genome split in N owned ranges; weak: each rank scans its own "
+                         "config-sized contig set (N x the genome)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time only rank 0's owned range of an N-way split on this one GPU "
                          "(no collective); the JSON line is then not the metric")
@@ -155,16 +260,18 @@ def main():
 
     import torch
     from merpcr_amd import MerPCR, _native, synth
-    from merpcr_amd.dist import HIT_BYTES, gather_hits, shard_ranges
+    from merpcr_amd.dist import HIT_BYTES, native_comm, shard_ranges
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    comm = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")          # control plane only
+        comm = native_comm(local)                 # data plane: RCCL inside libmerpcr_hip
 
     cfg = dict(synth.CONFIGS[args.config])
     total = int(cfg["total"] * args.scale) // 64 * 64
@@ -179,7 +286,8 @@ def main():
     table = eng.device_table()
     weak = args.scaling == "weak"
     names, lens, buf, offs, planted = synth.build_genome_torch(
-        total, cfg["records"], sts, seed=1 + (rank if weak else 0), N=cfg["N"], M=cfg["M"], W=cfg["W"], nrun=cfg["nrun"], device=dev)
+        total, cfg["records"], sts, seed=1 + (rank if weak else 0), N=cfg["N"], M=cfg["M"], W=cfg["W"],
+        nrun=cfg["nrun"], device=dev)
     torch.cuda.synchronize()
     genome = _native.Genome(local, lens)
     stream = torch.cuda.current_stream().cuda_stream
@@ -191,27 +299,34 @@ def main():
     search = _native.Search(table, genome)
     if args.shard_of > 1:
         rng = shard_ranges(lens, args.shard_of)[0]
-    elif weak:
-        rng = None          # this rank's own contigs, whole
+    elif weak or world == 1:
+        rng = None          # this rank's own contigs / the whole genome
     else:
         rng = shard_ranges(lens, world)[rank]
     setup_s = time.time() - t_setup
     log(f"[rank {rank}] setup {setup_s:.1f}s (pack {pack_s:.2f}s) records={len(lens)} bases={sum(lens)} "
-        f"sts={n_sts} recs={table.n_rec} planted={planted} table={table.stats()} genome={genome.stats()}")
+        f"sts={n_sts} recs={table.n_rec} planted={planted} table={table.stats()} genome={genome.stats()} "
+        f"range={rng}")
 
-    comm = None
+    gathered = None
     if world > 1:
-        comm = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+        gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)  # rank 0's gather buffer
 
     def step():
-        nonlocal comm
+        nonlocal gathered
         n = search.run(rng, stream)
         if world > 1:
-            need = max(n, 1) * HIT_BYTES
-            if comm.numel() < need:
-                comm = torch.empty(need * 2, dtype=torch.uint8, device=dev)
-            search.fetch_device(comm.data_ptr(), comm.numel() // HIT_BYTES, stream)
-            gather_hits(comm, n, seq_base=rank * len(lens) if weak else 0)
+            cap = gathered.numel() // HIT_BYTES if rank == 0 else 0
+            try:
+                n = comm.gather_hits(search, gathered.data_ptr(), cap, len(lens) * rank if weak else 0, stream)
+            except _native.NativeError as e:
+                if e.code != _native.MP_E_CAP:
+                    raise
+                # rank 0's buffer too small: every rank got MP_E_CAP; grow and gather again
+                need = comm.last_total
+                gathered = torch.empty(need * 2 * HIT_BYTES, dtype=torch.uint8, device=dev)
+                cap = gathered.numel() // HIT_BYTES if rank == 0 else 0
+                n = comm.gather_hits(search, gathered.data_ptr(), cap, len(lens) * rank if weak else 0, stream)
         return n
 
     for _ in range(args.warmup):
@@ -233,33 +348,31 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     st = search.last_stats()
-    local_stats = torch.tensor([elapsed, float(nhits), float(st["windows"]), float(np.mean(scan_ms)),
-                                float(sum(lens))],
-                               dtype=torch.float64, device=dev)
     if world > 1:
-        mx = local_stats.clone()
-        torch.distributed.all_reduce(mx[:1], op=torch.distributed.ReduceOp.MAX)
-        sm = local_stats.clone()
-        torch.distributed.all_reduce(sm, op=torch.distributed.ReduceOp.SUM)
+        mx = torch.tensor([elapsed], dtype=torch.float64)
+        torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
+        sm = torch.tensor([float(sum(lens))], dtype=torch.float64)
+        torch.distributed.all_reduce(sm)
         elapsed = float(mx[0])
-        tot_hits, tot_windows = float(sm[1]), float(sm[2])
-        tot_bases = float(sm[4]) if weak else float(sum(lens))
+        tot_bases = float(sm[0]) if weak else float(sum(lens))
     else:
-        tot_hits, tot_windows = float(nhits), float(st["windows"])
         tot_bases = float(sum(lens))
+    tot_hits = float(nhits)  # after the gather: every rank's hits (N > 1)
     if rank != 0:
+        comm.close()
         torch.distributed.destroy_process_group()
         return
     bases = float(sum(lens))          # one rank's genome (= the whole job's at N=1 or strong)
     t_step = elapsed / args.steps
     kern_s = float(np.mean(scan_ms)) / 1e3
-    alg_bytes = BYTES_PER_BASE * st["windows"] + BYTES_PER_HIT * nhits  # rank 0's scan launch
+    alg_bytes = BYTES_PER_BASE * st["windows"] + BYTES_PER_HIT * search.last_hits()  # rank 0's scan launch
     achieved = alg_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
     workload = (f"{args.config}: {n_sts} STS vs {bases / 1e9:.3f} Gbp ({len(lens)} records), "
                 f"W={cfg['W']} N={cfg['N']} M={cfg['M']} I={cfg['I']}")
     if world > 1 and weak:
         workload += f" per rank ({world} contig sets, {tot_bases / 1e9:.3f} Gbp in all)"
-    traffic, traffic_src = pmc_traffic(workload) if world == 1 else (None, None)
+    pmc, pmc_tag = pmc_profile(workload) if world == 1 and args.shard_of <= 1 else (None, None)
+    traffic = pmc["hbm_traffic_bytes_per_launch"] if pmc else None
     out = {
         "metric": METRIC,
         "value": round(tot_bases / max(args.shard_of, 1) / t_step / 1e9, 4),
@@ -276,8 +389,8 @@ def main():
         "config": {"workload": workload,
                    "sts": n_sts, "records": len(lens), "bases": int(bases), "W": cfg["W"], "N": cfg["N"],
                    "M": cfg["M"], "I": cfg["I"],
-                   "parallelism": (f"contig shards x{world} (per-rank contig set, RCCL hit gatherv)" if weak
-                                   else f"owned-k shards x{world} (RCCL hit gatherv)")},
+                   "parallelism": (f"contig sets x{world} (one per rank, RCCL hit gatherv)" if weak
+                                   else f"owned (sequence, k) ranges x{world} of one genome (RCCL hit gatherv)")},
         "hits": int(tot_hits),
         "hits_per_s": round(tot_hits / t_step, 1),
         "scan_kernel_ms": round(kern_s * 1e3, 3),
@@ -290,22 +403,35 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": int(traffic) if traffic else None,
-                     "traffic_source": f"profiles/{traffic_src}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, "
+                     "traffic_source": f"profiles/{pmc_tag}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, "
                                        "gfx950-corrected; includes Infinity-Cache hits)" if traffic else None,
                      "kernel": "mp::dense_kernel" if cfg["W"] <= 9 else "mp::scan_kernel",
-                     "alg_bytes_per_launch": int(alg_bytes)},
+                     "alg_bytes_per_launch": int(alg_bytes),
+                     "issue": (dict(issue_bound(pmc), source=f"profiles/{pmc_tag}_pmc.json") if pmc else None)},
+        "setup_s": round(setup_s, 2),
     }
     if args.shard_of > 1:
         out["diagnostic"] = f"rank 0 of a {args.shard_of}-way owned-range split, alone on one GPU (not the metric)"
+    parity_ok = True
     if world == 1 and not args.no_e2e:
         out["e2e"] = end_to_end(eng, table, names, lens, buf, offs, local, stream)
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and args.e2e_file:
+        out["e2e_file"] = end_to_end_file(eng._sts_path, names, lens, buf, offs, cfg, local)
+    if world == 1 and not args.no_cpu_baseline and args.shard_of <= 1:
         hits = search.fetch(nhits)
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(eng, names, lens, buf, offs, cfg, hits, args.cpu_budget, threads)
+        threads = args.cpu_threads or host_cores()
+        out["cpu_baseline"], otable, oprm = cpu_baseline(eng, lens, buf, offs, cfg, hits, args.cpu_budget, threads)
+        parity_ok = out["cpu_baseline"]["parity_vs_gpu"]
+        if not args.no_ref_model:
+            out["cpu_baseline_reference_model"] = reference_model(otable, oprm, buf, offs, lens, threads,
+                                                                  args.cpu_budget)
     print(json.dumps(out), flush=True)
     if world > 1:
+        comm.close()
         torch.distributed.destroy_process_group()
+    if not parity_ok:
+        log("FAIL: the GPU hit list differs from the CPU oracle's on the baseline sample")
+        sys.exit(1)
 
 
 if __name__ == "__main__":

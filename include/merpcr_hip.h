@@ -160,6 +160,40 @@ int mp_search_survivors(void* search, uint64_t* n_survivors);
 int mp_search_timing(void* search, float* scan_ms, float* tail_ms, float* pair_ms, float* order_ms);
 void mp_search_destroy(void* search);
 
+/* ---- multi-GPU (replaces the -T ProcessPool fan-out over chunks of a record,
+ * engine.py:386-422) --------------------------------------------------
+ * One process, several devices: the genome's (sequence, k) space is split into owned
+ * ranges of equal base count, one per device (contiguous, in device order); each device
+ * packs only the bases its range reads and searches it in a host thread of its own; the
+ * sorted per-device lists are gathered into devices[0] by one grouped ncclSend/ncclRecv
+ * over RCCL (xGMI).  Their concatenation is exactly the single-device hit list.
+ * tables[i] must have been created on devices[i] from the same records.  A device listed
+ * twice (tests on one GPU) is gathered by device copies: RCCL admits one rank per device. */
+int mp_multi_create(uint32_t n_dev, const int32_t* devices, void* const* tables, void** multi_out);
+/* (Re)lay out the sequence set on every device and split it into owned ranges. */
+int mp_multi_genome(void* multi, uint32_t n_seq, const uint64_t* seq_len);
+/* Whole sequence `seq` from host memory (each device packs its share + halo). */
+int mp_multi_put(void* multi, uint32_t seq, const uint8_t* host_bytes, uint64_t nbytes);
+int mp_multi_seal(void* multi);
+/* Search every device's owned range and gather: *n_hits = all hits, in output order. */
+int mp_multi_run(void* multi, uint64_t* n_hits);
+int mp_multi_fetch(void* multi, mp_hit* out, uint64_t cap);
+/* Device i's search handle (borrowed: stats, timings), its owned range and the last
+ * gather's duration on devices[0]'s stream. */
+int mp_multi_device_search(void* multi, uint32_t i, void** search, mp_range* owned, float* gather_ms);
+void mp_multi_destroy(void* multi);
+
+/* One process per GPU (torchrun-style launch): every rank creates a communicator from an
+ * RCCL unique id that rank 0 made (mp_comm_unique_id, 128 bytes) and the caller shared
+ * out of band; mp_comm_gather_hits then gathers each rank's last mp_search_run result to
+ * rank 0 (dev_out on rank 0's device, cap entries), in rank order, adding seq_shift to each
+ * rank's sequence indices.  Collective; *n_total = all ranks' hits, on every rank. */
+int mp_comm_unique_id(uint8_t* id128);
+int mp_comm_create(const uint8_t* id128, int32_t nranks, int32_t rank, int32_t device, void** comm_out);
+int mp_comm_gather_hits(void* comm, void* search, uint32_t seq_shift, mp_hit* dev_out, uint64_t cap,
+                        uint64_t* n_total, void* stream);
+void mp_comm_destroy(void* comm);
+
 /* ---- FASTA input (replaces FASTALoader.load_file, src/merpcr/io/fasta.py:18-71) --
  * Reads `path` as the reference's text-mode loop does: strict UTF-8, universal
  * newlines, Python str.strip() whitespace, '>' headers (defline = stripped line),

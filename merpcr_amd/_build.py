@@ -12,7 +12,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIBDIR, "libmerpcr_hip.so")
-SOURCES = ["mp_table.hip", "mp_genome.hip", "mp_search.hip", "mp_sort.hip", "mp_fasta.hip", "mp_format.hip", "mp_sts.hip"]
+SOURCES = ["mp_table.hip", "mp_genome.hip", "mp_search.hip", "mp_sort.hip", "mp_multi.hip", "mp_fasta.hip",
+           "mp_format.hip", "mp_sts.hip"]
 HEADERS = ["mp_internal.h", "mp_text.h", os.path.join("..", "..", "include", "merpcr_hip.h")]
 ARCH = os.environ.get("MERPCR_OFFLOAD_ARCH", "gfx950")
 
@@ -59,7 +60,8 @@ def build_native(force: bool = False, verbose: bool = False, defines=(), lib: st
                 if res.returncode:
                     raise RuntimeError(f"hipcc failed for {cmd[-3]}")
     if force or jobs or _stale(lib, objs):
-        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs
+        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + [
+            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode:
             print(" ".join(cmd))

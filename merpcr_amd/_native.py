@@ -33,6 +33,9 @@ EXPORTS = (
     "mp_genome_stats", "mp_genome_reset", "mp_genome_destroy",
     "mp_search_create", "mp_search_set_options", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
     "mp_search_last_stats", "mp_search_regrowths", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
+    "mp_multi_create", "mp_multi_genome", "mp_multi_put", "mp_multi_seal", "mp_multi_run", "mp_multi_fetch",
+    "mp_multi_device_search", "mp_multi_destroy",
+    "mp_comm_unique_id", "mp_comm_create", "mp_comm_gather_hits", "mp_comm_destroy",
     "mp_fasta_load", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record", "mp_fasta_destroy",
     "mp_format_hits",
     "mp_sts_parse", "mp_sts_info", "mp_sts_arrays", "mp_sts_destroy",
@@ -102,6 +105,20 @@ def _sig(lib):
     lib.mp_search_timing.argtypes = [P, POINTER(c_float), POINTER(c_float), POINTER(c_float), POINTER(c_float)]
     lib.mp_search_destroy.argtypes = [P]
     lib.mp_search_destroy.restype = None
+    lib.mp_multi_create.argtypes = [c_uint32, POINTER(c_int32), POINTER(c_void_p), POINTER(c_void_p)]
+    lib.mp_multi_genome.argtypes = [P, c_uint32, P]
+    lib.mp_multi_put.argtypes = [P, c_uint32, P, c_uint64]
+    lib.mp_multi_seal.argtypes = [P]
+    lib.mp_multi_run.argtypes = [P, u64p]
+    lib.mp_multi_fetch.argtypes = [P, P, c_uint64]
+    lib.mp_multi_device_search.argtypes = [P, c_uint32, POINTER(c_void_p), POINTER(MPRange), POINTER(c_float)]
+    lib.mp_multi_destroy.argtypes = [P]
+    lib.mp_multi_destroy.restype = None
+    lib.mp_comm_unique_id.argtypes = [P]
+    lib.mp_comm_create.argtypes = [P, c_int32, c_int32, c_int32, POINTER(c_void_p)]
+    lib.mp_comm_gather_hits.argtypes = [P, P, c_uint32, P, c_uint64, u64p, P]
+    lib.mp_comm_destroy.argtypes = [P]
+    lib.mp_comm_destroy.restype = None
     lib.mp_fasta_load.argtypes = [c_char_p, POINTER(c_void_p)]
     lib.mp_fasta_load_chunked.argtypes = [c_char_p, c_uint64, POINTER(c_void_p)]
     lib.mp_fasta_info.argtypes = [P, u64p, u64p]
@@ -255,7 +272,12 @@ class Search:
             r = MPRange(*rng)
         check(lib().mp_search_run(self._h, ctypes.byref(r) if r is not None else None,
                                   c_void_p(stream or 0), ctypes.byref(n)))
+        self._last_n = n.value
         return n.value
+
+    def last_hits(self) -> int:
+        """Hits of this handle's last run (its own owned range)."""
+        return getattr(self, "_last_n", 0)
 
     def fetch(self, n: int, stream=None) -> np.ndarray:
         out = np.empty(n, dtype=HIT_DTYPE)
@@ -284,6 +306,105 @@ class Search:
     def close(self):
         if self._h:
             lib().mp_search_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _Borrowed(Search):
+    """A search handle owned by a Multi (stats only; never destroyed here)."""
+
+    def __init__(self, h):
+        self._h = h
+
+    def close(self):
+        self._h = c_void_p()
+
+
+class Multi:
+    """One process, several devices (mp_multi_*): owned ranges of one sequence set, one per
+    device, searched in parallel and gathered into devices[0] over RCCL."""
+
+    def __init__(self, devices, tables):
+        self.devices = [int(d) for d in devices]
+        self.tables = list(tables)  # kept alive with the handle
+        self._h = c_void_p()
+        devs = (c_int32 * len(self.devices))(*self.devices)
+        hs = (c_void_p * len(self.tables))(*[tb._h for tb in self.tables])
+        check(lib().mp_multi_create(len(self.devices), devs, hs, ctypes.byref(self._h)))
+
+    def genome(self, lengths):
+        self.lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        check(lib().mp_multi_genome(self._h, len(self.lengths), ptr(self.lengths)))
+
+    def put(self, seq: int, data):
+        buf = np.ascontiguousarray(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data,
+                                   dtype=np.uint8)
+        check(lib().mp_multi_put(self._h, seq, ptr(buf), buf.size))
+
+    def seal(self):
+        check(lib().mp_multi_seal(self._h))
+
+    def run(self) -> int:
+        n = c_uint64(0)
+        check(lib().mp_multi_run(self._h, ctypes.byref(n)))
+        return n.value
+
+    def fetch(self, n: int) -> np.ndarray:
+        out = np.empty(n, dtype=HIT_DTYPE)
+        check(lib().mp_multi_fetch(self._h, ptr(out), n))
+        return out
+
+    def device(self, i: int):
+        """(search handle of device i, its owned range, last gather ms)."""
+        s, r, g = c_void_p(), MPRange(), c_float()
+        check(lib().mp_multi_device_search(self._h, i, ctypes.byref(s), ctypes.byref(r), ctypes.byref(g)))
+        return _Borrowed(s), (r.seq_begin, r.seq_end, r.k_begin, r.k_end), g.value
+
+    def close(self):
+        if self._h:
+            lib().mp_multi_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * 128)()
+    check(lib().mp_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """One rank of a process-per-GPU job (mp_comm_*): RCCL inside the library; the
+    128-byte unique id is shared by the caller (e.g. over torch.distributed)."""
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int):
+        self._h = c_void_p()
+        self.rank, self.nranks = rank, nranks
+        b = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().mp_comm_create(b, nranks, rank, device, ctypes.byref(self._h)))
+
+    def gather_hits(self, search: Search, dev_out: int, cap: int, seq_shift: int = 0, stream=None) -> int:
+        """Every rank's last-run hits into dev_out on rank 0, rank order; returns the total."""
+        n = c_uint64(0)
+        rc = lib().mp_comm_gather_hits(self._h, search._h, seq_shift, c_void_p(dev_out), cap, ctypes.byref(n),
+                                       c_void_p(stream or 0))
+        self.last_total = n.value  # set on MP_E_CAP too: the capacity rank 0 needs
+        check(rc)
+        return n.value
+
+    def close(self):
+        if self._h:
+            lib().mp_comm_destroy(self._h)
             self._h = c_void_p()
 
     def __del__(self):

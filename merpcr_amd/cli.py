@@ -89,6 +89,9 @@ def create_parser() -> argparse.ArgumentParser:
     p.add_argument("-v", "--version", action="version", version="merPCR version 1.0.0")
     p.add_argument("--debug", action="store_true", help="Enable debug logging")
     p.add_argument("--device", type=int, default=None, help="HIP device index (default: 0)")
+    p.add_argument("--gpus", type=_bounded("gpus_type", 1, None, "GPUs must be > 0, got {v}"), default=1,
+                   help="search on this many GPUs (devices --device, --device+1, ...): the sequences' "
+                        "positions are split among them and the hits gathered over RCCL")
     p.add_argument("--emulate-chunks", action="store_true",
                    help="with -T > 1, reproduce the reference's per-chunk output (duplicate overlap "
                         "hits) instead of the exact single-chunk result")
@@ -104,7 +107,8 @@ def main(argv: List[str] = None) -> int:
                      three_prime_match=args.three_prime_match, iupac_mode=args.iupac,
                      default_pcr_size=args.default_pcr_size, threads=args.threads,
                      max_sts_line_length=args.max_sts_line_length, device=args.device,
-                     emulate_chunks=args.emulate_chunks)
+                     emulate_chunks=args.emulate_chunks,
+                     devices=[(args.device or 0) + i for i in range(args.gpus)] if args.gpus > 1 else None)
         if not eng.load_sts_file(args.sts_file):
             logger.error(f"Failed to load STS file: {args.sts_file}")
             return 1

@@ -68,7 +68,8 @@ class MerPCR:
                  three_prime_match: int = DEFAULT_THREE_PRIME_MATCH,
                  iupac_mode: int = DEFAULT_IUPAC_MODE, default_pcr_size: int = DEFAULT_PCR_SIZE,
                  threads: int = DEFAULT_THREADS, max_sts_line_length: int = 1022,
-                 device: Optional[int] = None, emulate_chunks: bool = False):
+                 device: Optional[int] = None, emulate_chunks: bool = False,
+                 devices: Optional[Sequence[int]] = None):
         self.wordsize = wordsize
         self.margin = margin
         self.mismatches = mismatches
@@ -77,7 +78,14 @@ class MerPCR:
         self.default_pcr_size = default_pcr_size
         self.threads = threads
         self.max_sts_line_length = max_sts_line_length
-        self.device = 0 if device is None else int(device)
+        # devices: several GPUs of this process share every search (owned-range sharding,
+        # RCCL gather; MerPCR(devices=[0, 1, ...]) or the CLI's --gpus N); device is the first
+        if devices:
+            self.devices = [int(d) for d in devices]
+            self.device = self.devices[0]
+        else:
+            self.device = 0 if device is None else int(device)
+            self.devices = [self.device]
         # threads > 1: reproduce the reference's per-chunk output (duplicated overlap
         # hits, chunk-local record ends) instead of the exact T=1 result
         self.emulate_chunks = bool(emulate_chunks)
@@ -98,6 +106,9 @@ class MerPCR:
         self._dev_search = None
         self._dev_search_key = None
         self._dev_genome_dev = None
+        self._extra_tables: Dict[int, object] = {}
+        self._multi = None
+        self._multi_key = None
 
         self._init_lookup_tables()
         self._validate_parameters()
@@ -371,7 +382,22 @@ class MerPCR:
         if self._dev_table is None or self._dev_table_sig != sig:
             self._dev_table = _native.Table(self._params(), self.device, *self._table_arrays())
             self._dev_table_sig = sig
+            self._extra_tables = {}
         return self._dev_table
+
+    def device_tables(self) -> list:
+        """One seed table per entry of self.devices (a repeated device shares its table)."""
+        from .. import _native
+        first = self.device_table()
+        out = []
+        for d in self.devices:
+            if d == self.device:
+                out.append(first)
+                continue
+            if d not in self._extra_tables:
+                self._extra_tables[d] = _native.Table(self._params(), d, *self._table_arrays())
+            out.append(self._extra_tables[d])
+        return out
 
     def encode_sequences(self, sequences: Sequence[str]) -> List[np.ndarray]:
         """Device bytes of each sequence, in the coordinates of ``seq.upper()``.
@@ -460,7 +486,42 @@ class MerPCR:
             self._dev_search_key = key
         return self._dev_genome, self._dev_search
 
+    def _search_multi(self, data: Sequence[np.ndarray]) -> np.ndarray:
+        """Several devices: owned (sequence, k) ranges of equal base count, one per device,
+        searched in parallel and gathered into devices[0] (mp_multi_*, RCCL)."""
+        from .. import _native
+        tables = self.device_tables()
+        key = (tuple(self.devices), tuple(id(tb) for tb in tables), tuple(sorted(self.search_options.items())))
+        if self._multi is None or self._multi_key != key:
+            if self._multi is not None:
+                self._multi.close()
+            self._multi = _native.Multi(self.devices, tables)
+            self._multi_key = key
+            self._multi_opts_pending = bool(self.search_options)
+        m = self._multi
+        m.genome([len(d) for d in data])
+        if self._multi_opts_pending:  # the per-device searches exist once the genome is laid out
+            for i in range(len(self.devices)):
+                m.device(i)[0].set_options(**self.search_options)
+            self._multi_opts_pending = False
+        for i, d in enumerate(data):
+            if len(d):
+                m.put(i, d)
+        m.seal()
+        t0 = time.time()
+        n = m.run()
+        hits = m.fetch(n)
+        per = []
+        for i in range(len(self.devices)):
+            s, rng, gms = m.device(i)
+            per.append(dict(s.last_stats(), owned=rng))
+        self.last_search_stats = dict(wall_s=time.time() - t0, hits=n, gather_ms=gms, devices=per,
+                                      scan_ms=max(p["scan_ms"] for p in per), regrowths=0)
+        return hits
+
     def _search_device(self, data: Sequence[np.ndarray]) -> np.ndarray:
+        if len(self.devices) > 1:
+            return self._search_multi(data)
         genome, search = self._device_search([len(d) for d in data])
         for i, d in enumerate(data):
             if len(d):

@@ -109,6 +109,7 @@ struct Table {
     uint32_t n_rec = 0;
     uint64_t n_keys = 0, max_bucket = 0, dev_bytes = 0;
     uint32_t max_hash_off = 0;
+    uint64_t max_reach = 0;   // max(size) + M: bases past an amplicon start any compare reads
     int filt_direct = 1;
     uint32_t filt_log2 = 0;   // log2(filter bits)
     int lds_exact = 0;        // LDS prefilter is the exact 4^W bitmap (W <= 10)
@@ -120,6 +121,10 @@ struct Table {
     uint2* rk = nullptr;          // W <= 13: rank bitmap
     Entry* dents = nullptr;       // W <= 13: bucket heads by key rank
     uint2* dents8 = nullptr;      // W <= 13: 8-B heads {primer-1 bases W..W+15, rec | (l1-W)<<26 | full<<31}
+    uint64_t* rkf = nullptr;      // W <= 13: filtered rank groups, one u64 per 16 keys (see kRkf*)
+    uint32_t rkf_rb = 0;          // rank prefix bits in an rkf group
+    uint32_t rkf_fw = 0;          // bits per filter field (2 fields per group)
+    uint32_t rkf_F = 0;           // primer-1 bases W..W+F-1 a filter field holds (0: no filter)
     uint2* binfo = nullptr;       // W <= kDenseMaxW: per key rank {first padded entry, records}
     uint16_t* dfilt = nullptr;    // W <= kDenseMaxW: 2-B filter word per padded entry (kDenseAlways...)
     uint2* dgrp = nullptr;        // W <= kDenseMaxW: per 32 keys {inline-bucket bits, first oct | any escape << 31}
@@ -300,6 +305,17 @@ __host__ __device__ __forceinline__ uint32_t lds_block_mask(uint32_t x, uint32_t
     if (k >= 2) m |= 1u << ((x >> shw) & 31u);
     return m;
 }
+
+// Filtered rank groups (rkf), the ranked drain's level-2 table: one u64 per 16 consecutive
+// keys of the exact 4^W presence bitmap -- bits 0-15 presence, then the rank prefix (rkf_rb
+// bits), then two filter fields of rkf_fw bits for the group's first two present keys: a
+// flag (top bit of the field) and, for a bucket of one record seeded at its primer start and
+// plain over bases W..W+F-1, those F bases (2-bit, base W on top).  The level-2 probe that
+// confirms a seed thus also carries a filter: a seed window whose bases W..W+F-1 differ from
+// them in more than N positions cannot match primer 1 (each counted position is a real
+// mismatch), so the drain skips its bucket head without loading it.
+constexpr uint32_t kRkfKeys = 16;
+__host__ __device__ __forceinline__ uint32_t rkf_field_flag(uint32_t fw) { return 1u << (fw - 1); }
 
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {
     return d == 0 ? 0u : (d < 0 ? (uint32_t)(-2 * d - 1) : (uint32_t)(2 * d));

@@ -1,0 +1,402 @@
+// Multi-GPU search: one genome's (sequence, k) space split into owned ranges, one range
+// per device, and the per-device sorted hit lists gathered over RCCL (xGMI) into one list.
+//
+// every window position is independent and owned ranges are contiguous in
+// (sequence, k), so the rank-ordered concatenation of the per-device sorted lists is the
+// reference's output order (engine.py:434, T=1 semantics); boundary tests inside each
+// device use the true sequence lengths (the whole layout is known to every device), so
+// the union is exactly the single-device result.  The reference's own parallelism is
+// the -T ProcessPool fan-out over chunks of one record (engine.py:386-422); this replaces
+// it.
+//
+// Two forms:
+//   * mp_multi_*: one process drives several devices, one host thread per device for the
+//     pack and the search, then one grouped ncclSend/ncclRecv gatherv into devices[0]
+//     (ncclCommInitAll over distinct devices; a repeated device -- tests on one GPU --
+//     is gathered by device copies instead, as RCCL admits one rank per device).
+//   * mp_comm_*: one process per GPU (torchrun / MPI style): the caller shares the RCCL
+//     unique id out of band; every rank's last search result is gathered to rank 0.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "mp_internal.h"
+
+namespace mp {
+
+#define MP_NCCL_CHECK(expr)                                                              \
+    do {                                                                                 \
+        ncclResult_t _r = (expr);                                                        \
+        if (_r != ncclSuccess)                                                           \
+            return ::mp::fail(MP_E_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+// seq += shift[segment] for the gathered hits of each rank (contig shards of a larger
+// record set: each rank numbers its sequences from 0)
+__global__ void shift_seq_kernel(mp_hit* __restrict__ h, uint64_t n, uint32_t shift) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) h[i].seq += shift;
+}
+
+struct Multi {
+    std::vector<int> dev;
+    std::vector<Table*> tab;
+    std::vector<Genome*> gen;
+    std::vector<Search*> srch;
+    std::vector<hipStream_t> st;
+    std::vector<ncclComm_t> comm;   // empty when a device repeats
+    std::vector<mp_range> rng;      // owned range per device
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> need;  // per device, per sequence: bases packed
+    std::vector<uint64_t> counts;
+    std::vector<uint64_t> len;
+    mp_hit* all = nullptr;          // gathered hits on dev[0]
+    uint64_t all_cap = 0, n_all = 0;
+    float gather_ms = 0.f;
+};
+
+static void free_multi(Multi* m) {
+    if (!m) return;
+    for (auto c : m->comm) ncclCommDestroy(c);
+    for (size_t i = 0; i < m->dev.size(); ++i) {
+        hipSetDevice(m->dev[i]);
+        if (m->srch[i]) mp_search_destroy(m->srch[i]);
+        if (m->gen[i]) mp_genome_destroy(m->gen[i]);
+        if (m->st[i]) hipStreamDestroy(m->st[i]);
+    }
+    if (m->all) {
+        hipSetDevice(m->dev[0]);
+        hipFree(m->all);
+    }
+    delete m;
+}
+
+// Owned (sequence, k) ranges of equal base count, in order; the last ends at the genome's end.
+static void split_ranges(const std::vector<uint64_t>& len, uint32_t parts, std::vector<mp_range>& out) {
+    uint64_t total = 0;
+    for (auto l : len) total += l;
+    const uint32_t n_seq = (uint32_t)len.size();
+    out.assign(parts, mp_range{0, 0, 0, 0});
+    uint32_t q = 0;
+    uint64_t before = 0;  // bases of sequences < q
+    mp_range cur{0, 0, 0, 0};
+    for (uint32_t p = 0; p < parts; ++p) {
+        out[p].seq_begin = cur.seq_begin;
+        out[p].k_begin = cur.k_begin;
+        if (p + 1 == parts) {
+            out[p].seq_end = n_seq;
+            out[p].k_end = 0;
+            break;
+        }
+        const uint64_t cut = total * (p + 1) / parts;  // global base index of the cut
+        while (q < n_seq && before + len[q] <= cut) {
+            before += len[q];
+            ++q;
+        }
+        out[p].seq_end = q;
+        out[p].k_end = q < n_seq ? cut - before : 0;
+        cur.seq_begin = q;
+        cur.k_begin = out[p].k_end;
+    }
+}
+
+// Run fn(d) for every device in a host thread of its own; the first failure is re-raised
+// on the calling thread (error messages are thread-local).
+template <class F>
+static int per_device(uint32_t nd, F&& fn) {
+    std::vector<int> rc(nd, MP_OK);
+    std::vector<std::string> msg(nd);
+    std::vector<std::thread> th;
+    for (uint32_t d = 0; d < nd; ++d)
+        th.emplace_back([&, d] {
+            rc[d] = fn(d);
+            if (rc[d]) msg[d] = mp_last_error();
+        });
+    for (auto& x : th) x.join();
+    for (uint32_t d = 0; d < nd; ++d)
+        if (rc[d]) return fail(rc[d], msg[d]);
+    return MP_OK;
+}
+
+static int multi_layout(Multi* m, uint32_t n_seq, const uint64_t* seq_len) {
+    const uint32_t nd = (uint32_t)m->dev.size();
+    m->len.assign(seq_len, seq_len + n_seq);
+    split_ranges(m->len, nd, m->rng);
+    m->need.assign(nd, std::vector<std::pair<uint64_t, uint64_t>>(n_seq, {0, 0}));
+    for (uint32_t d = 0; d < nd; ++d) {
+        const mp_range& r = m->rng[d];
+        const uint64_t halo = m->tab[d]->max_reach + 64;  // bases past an owned k any compare reads
+        for (uint32_t q = r.seq_begin; q < n_seq && q <= r.seq_end; ++q) {
+            const uint64_t lo = q == r.seq_begin ? r.k_begin : 0;
+            const uint64_t hi = q == r.seq_end ? r.k_end : m->len[q];
+            if (hi <= lo) continue;
+            const uint64_t a = lo & ~63ull;
+            uint64_t b = std::min<uint64_t>(m->len[q], hi + halo + m->tab[d]->max_hash_off);
+            if (b < m->len[q]) b = std::min<uint64_t>(m->len[q], round_up(b, 64));
+            m->need[d][q] = {a, b};
+        }
+    }
+    // one thread per device: (re)lay every device's genome out on its own buffers
+    return per_device(nd, [&](uint32_t d) -> int {
+        if (hipSetDevice(m->dev[d]) != hipSuccess) return fail(MP_E_HIP, "hipSetDevice failed");
+        if (m->gen[d]) return mp_genome_reset(m->gen[d], n_seq, seq_len);
+        void* g = nullptr;
+        int rc = mp_genome_create(m->dev[d], n_seq, seq_len, &g);
+        m->gen[d] = (Genome*)g;
+        if (rc) return rc;
+        void* s = nullptr;
+        rc = mp_search_create(m->tab[d], m->gen[d], &s);
+        m->srch[d] = (Search*)s;
+        return rc;
+    });
+}
+
+}  // namespace mp
+
+using namespace mp;
+
+MP_EXPORT int mp_multi_create(uint32_t n_dev, const int32_t* devices, void* const* tables, void** out) {
+    if (!out || !n_dev || !devices || !tables) return fail(MP_E_ARG, "mp_multi_create: null pointer or no device");
+    *out = nullptr;
+    Multi* m = new Multi();
+    m->dev.assign(devices, devices + n_dev);
+    m->tab.resize(n_dev);
+    m->gen.assign(n_dev, nullptr);
+    m->srch.assign(n_dev, nullptr);
+    m->st.assign(n_dev, nullptr);
+    m->counts.assign(n_dev, 0);
+    int rc = MP_OK;
+    for (uint32_t d = 0; d < n_dev && !rc; ++d) {
+        m->tab[d] = (Table*)tables[d];
+        if (!m->tab[d]) rc = fail(MP_E_ARG, "mp_multi_create: null table");
+        else if (m->tab[d]->device != m->dev[d]) rc = fail(MP_E_ARG, "mp_multi_create: table i must live on devices[i]");
+        else if (hipSetDevice(m->dev[d]) != hipSuccess || hipStreamCreateWithFlags(&m->st[d], hipStreamNonBlocking) != hipSuccess)
+            rc = fail(MP_E_HIP, "mp_multi_create: stream creation failed");
+    }
+    if (!rc) {
+        std::vector<int> sorted(m->dev);
+        std::sort(sorted.begin(), sorted.end());
+        const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+        if (distinct) {
+            m->comm.resize(n_dev);
+            const ncclResult_t r = ncclCommInitAll(m->comm.data(), (int)n_dev, m->dev.data());
+            if (r != ncclSuccess) {
+                m->comm.clear();
+                rc = fail(MP_E_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+            }
+        }
+    }
+    if (rc) {
+        free_multi(m);
+        return rc;
+    }
+    *out = m;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_multi_genome(void* multi, uint32_t n_seq, const uint64_t* seq_len) {
+    Multi* m = (Multi*)multi;
+    if (!m || (n_seq && !seq_len)) return fail(MP_E_ARG, "mp_multi_genome: null pointer");
+    return multi_layout(m, n_seq, seq_len);
+}
+
+MP_EXPORT int mp_multi_put(void* multi, uint32_t seq, const uint8_t* host_bytes, uint64_t nbytes) {
+    Multi* m = (Multi*)multi;
+    if (!m || (nbytes && !host_bytes)) return fail(MP_E_ARG, "mp_multi_put: null pointer");
+    if (seq >= m->len.size()) return fail(MP_E_ARG, "mp_multi_put: sequence index out of range");
+    if (nbytes != m->len[seq]) return fail(MP_E_ARG, "mp_multi_put: pass the whole sequence");
+    return per_device((uint32_t)m->dev.size(), [&](uint32_t d) -> int {
+        const auto [a, b] = m->need[d][seq];  // each device packs the part its owned range reads
+        return b > a ? mp_genome_put(m->gen[d], seq, a, host_bytes + a, b - a, m->st[d]) : MP_OK;
+    });
+}
+
+MP_EXPORT int mp_multi_seal(void* multi) {
+    Multi* m = (Multi*)multi;
+    if (!m) return fail(MP_E_ARG, "mp_multi_seal: null multi");
+    return per_device((uint32_t)m->dev.size(), [&](uint32_t d) { return mp_genome_seal(m->gen[d], m->st[d]); });
+}
+
+MP_EXPORT int mp_multi_run(void* multi, uint64_t* n_hits) {
+    Multi* m = (Multi*)multi;
+    if (!m) return fail(MP_E_ARG, "mp_multi_run: null multi");
+    if (!m->gen[0]) return fail(MP_E_STATE, "mp_multi_run: no genome (call mp_multi_genome)");
+    const uint32_t nd = (uint32_t)m->dev.size();
+    if (n_hits) *n_hits = 0;
+    const int rc = per_device(nd, [&](uint32_t d) { return mp_search_run(m->srch[d], &m->rng[d], m->st[d], &m->counts[d]); });
+    if (rc) return rc;
+    uint64_t total = 0;
+    for (auto c : m->counts) total += c;
+    MP_HIP_CHECK(hipSetDevice(m->dev[0]));
+    if (total > m->all_cap) {
+        hipFree(m->all);
+        m->all = nullptr;
+        m->all_cap = 0;
+        const uint64_t cap = total + total / 4 + 1024;
+        MP_HIP_CHECK(hipMalloc(&m->all, cap * sizeof(mp_hit)));
+        m->all_cap = cap;
+    }
+    hipEvent_t e0, e1;
+    MP_HIP_CHECK(hipEventCreate(&e0));
+    MP_HIP_CHECK(hipEventCreate(&e1));
+    MP_HIP_CHECK(hipEventRecord(e0, m->st[0]));
+    uint64_t off = 0;
+    if (!m->comm.empty()) {
+        // gatherv over RCCL: devices[0] receives every device's sorted list at its offset
+        MP_NCCL_CHECK(ncclGroupStart());
+        for (uint32_t d = 0; d < nd; ++d) {
+            const size_t bytes = m->counts[d] * sizeof(mp_hit);
+            if (bytes) {
+                MP_NCCL_CHECK(ncclRecv(m->all + off, bytes, ncclUint8, (int)d, m->comm[0], m->st[0]));
+                MP_NCCL_CHECK(ncclSend(m->srch[d]->out, bytes, ncclUint8, 0, m->comm[d], m->st[d]));
+            }
+            off += m->counts[d];
+        }
+        MP_NCCL_CHECK(ncclGroupEnd());
+        for (uint32_t d = 1; d < nd; ++d) {
+            MP_HIP_CHECK(hipSetDevice(m->dev[d]));
+            MP_HIP_CHECK(hipStreamSynchronize(m->st[d]));
+        }
+        MP_HIP_CHECK(hipSetDevice(m->dev[0]));
+    } else {
+        for (uint32_t d = 0; d < nd; ++d) {  // a repeated device: peer / local copies
+            const size_t bytes = m->counts[d] * sizeof(mp_hit);
+            if (bytes)
+                MP_HIP_CHECK(hipMemcpyPeerAsync(m->all + off, m->dev[0], m->srch[d]->out, m->dev[d], bytes, m->st[0]));
+            off += m->counts[d];
+        }
+    }
+    MP_HIP_CHECK(hipEventRecord(e1, m->st[0]));
+    MP_HIP_CHECK(hipStreamSynchronize(m->st[0]));
+    MP_HIP_CHECK(hipEventElapsedTime(&m->gather_ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    m->n_all = total;
+    if (n_hits) *n_hits = total;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_multi_fetch(void* multi, mp_hit* out, uint64_t cap) {
+    Multi* m = (Multi*)multi;
+    if (!m || (m->n_all && !out)) return fail(MP_E_ARG, "mp_multi_fetch: null pointer");
+    if (cap < m->n_all) return fail(MP_E_CAP, "mp_multi_fetch: output buffer too small");
+    if (!m->n_all) return MP_OK;
+    MP_HIP_CHECK(hipSetDevice(m->dev[0]));
+    MP_HIP_CHECK(hipMemcpyAsync(out, m->all, m->n_all * sizeof(mp_hit), hipMemcpyDeviceToHost, m->st[0]));
+    MP_HIP_CHECK(hipStreamSynchronize(m->st[0]));
+    return MP_OK;
+}
+
+MP_EXPORT int mp_multi_device_search(void* multi, uint32_t i, void** search, mp_range* owned, float* gather_ms) {
+    Multi* m = (Multi*)multi;
+    if (!m || i >= m->dev.size()) return fail(MP_E_ARG, "mp_multi_device_search: bad index");
+    if (search) *search = m->srch[i];
+    if (owned) *owned = i < m->rng.size() ? m->rng[i] : mp_range{0, 0, 0, 0};
+    if (gather_ms) *gather_ms = m->gather_ms;
+    return MP_OK;
+}
+
+MP_EXPORT void mp_multi_destroy(void* multi) { free_multi((Multi*)multi); }
+
+// ---------------------------------------------------------------- process per GPU
+namespace mp {
+struct Comm {
+    ncclComm_t c = nullptr;
+    int rank = 0, nranks = 1, device = 0;
+    uint64_t* d_meta = nullptr;  // nranks x {count, seq shift, capacity}
+    std::vector<uint64_t> meta;
+};
+}  // namespace mp
+
+static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id is 128 bytes");
+
+MP_EXPORT int mp_comm_unique_id(uint8_t* id) {
+    if (!id) return fail(MP_E_ARG, "mp_comm_unique_id: null pointer");
+    ncclUniqueId u;
+    MP_NCCL_CHECK(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return MP_OK;
+}
+
+MP_EXPORT int mp_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, void** out) {
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return fail(MP_E_ARG, "mp_comm_create: bad argument");
+    *out = nullptr;
+    MP_HIP_CHECK(hipSetDevice(device));
+    Comm* c = new Comm();
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device = device;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    ncclResult_t r = ncclCommInitRank(&c->c, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return fail(MP_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    if (hipMalloc(&c->d_meta, (size_t)nranks * 3 * sizeof(uint64_t)) != hipSuccess) {
+        ncclCommDestroy(c->c);
+        delete c;
+        return fail(MP_E_NOMEM, "mp_comm_create: allocation failed");
+    }
+    c->meta.assign((size_t)nranks * 3, 0);
+    *out = c;
+    return MP_OK;
+}
+
+// Gatherv of every rank's last-run hits (mp_search_run on `search`) to rank 0, in rank
+// order, into dev_out (rank 0's device, cap entries).  Each rank names the shift of its
+// sequence indices (its first record in the caller's global numbering).  Collective:
+// every rank calls it; *n_total = all ranks' hits on every rank; MP_E_CAP on every rank
+// when rank 0's cap is too small (nothing is sent then).
+MP_EXPORT int mp_comm_gather_hits(void* comm, void* search, uint32_t seq_shift, mp_hit* dev_out, uint64_t cap,
+                                  uint64_t* n_total, void* stream) {
+    Comm* c = (Comm*)comm;
+    Search* s = (Search*)search;
+    if (!c || !s || !n_total || (c->rank == 0 && cap && !dev_out)) return fail(MP_E_ARG, "mp_comm_gather_hits: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    MP_HIP_CHECK(hipSetDevice(c->device));
+    const uint64_t mine[3] = {s->n_hits, seq_shift, cap};
+    MP_HIP_CHECK(hipMemcpyAsync(c->d_meta + (size_t)c->rank * 3, mine, sizeof(mine), hipMemcpyHostToDevice, st));
+    MP_NCCL_CHECK(ncclAllGather(c->d_meta + (size_t)c->rank * 3, c->d_meta, 3, ncclUint64, c->c, st));
+    MP_HIP_CHECK(hipMemcpyAsync(c->meta.data(), c->d_meta, c->meta.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    MP_HIP_CHECK(hipStreamSynchronize(st));
+    uint64_t total = 0;
+    for (int r = 0; r < c->nranks; ++r) total += c->meta[(size_t)r * 3];
+    *n_total = total;
+    if (total > c->meta[2]) return fail(MP_E_CAP, "mp_comm_gather_hits: rank 0 buffer too small");
+    MP_NCCL_CHECK(ncclGroupStart());
+    uint64_t off = 0;
+    for (int r = 0; r < c->nranks; ++r) {
+        const size_t bytes = c->meta[(size_t)r * 3] * sizeof(mp_hit);
+        if (bytes) {
+            if (c->rank == 0) MP_NCCL_CHECK(ncclRecv(dev_out + off, bytes, ncclUint8, r, c->c, st));
+            if (c->rank == r) MP_NCCL_CHECK(ncclSend(s->out, bytes, ncclUint8, 0, c->c, st));
+        }
+        off += c->meta[(size_t)r * 3];
+    }
+    MP_NCCL_CHECK(ncclGroupEnd());
+    if (c->rank == 0) {
+        off = 0;
+        for (int r = 0; r < c->nranks; ++r) {
+            const uint64_t n = c->meta[(size_t)r * 3];
+            const uint32_t sh = (uint32_t)c->meta[(size_t)r * 3 + 1];
+            if (n && sh) {
+                hipLaunchKernelGGL(shift_seq_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, dev_out + off, n, sh);
+                MP_HIP_CHECK(hipGetLastError());
+            }
+            off += n;
+        }
+    }
+    return MP_OK;
+}
+
+MP_EXPORT void mp_comm_destroy(void* comm) {
+    Comm* c = (Comm*)comm;
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipFree(c->d_meta);
+    if (c->c) ncclCommDestroy(c->c);
+    delete c;
+}

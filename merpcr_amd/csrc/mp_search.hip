@@ -1078,7 +1078,9 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
     __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane) {
         if (stride) return ss + stride;
         if (ss + 1 < end) return ss + 1;
-        const uint32_t st = lo + (nw + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending)) * (uint32_t)kSChunk;
+        // lane 0 holds the claimed counter value: broadcast from lane 0 explicitly (called
+        // wave-uniformly, but readfirstlane would read another lane under divergence)
+        const uint32_t st = lo + (nw + (uint32_t)__shfl((int)pending, 0, 64)) * (uint32_t)kSChunk;
         if (st >= hi) {
             end = 0;
             return n_supers;

@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->rkf); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -182,6 +182,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 break;
             }
             t->max_hash_off = std::max(t->max_hash_off, d.hash_off);
+            t->max_reach = std::max<uint64_t>(t->max_reach, (uint64_t)d.size + (uint64_t)p.margin);
             d.p1_pl = (uint32_t)(planes.size() / 4);
             build_planes(primer1 + a1, d.l1, p.iupac_mode, planes);
             d.p2_pl = (uint32_t)(planes.size() / 4);
@@ -261,6 +262,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         std::vector<uint2> dgrp;
         std::vector<uint32_t> dgesc;
         std::vector<uint2> dents8;
+        std::vector<uint64_t> rkf;
         std::vector<Slot> slots;
         if (t->filt_direct) {
             // rank bitmap over the exact 4^W presence bitmap; heads in key order
@@ -379,6 +381,39 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             // few full heads (multi-record buckets, IUPAC/long/inner-seed primers): the ranked
             // drain tests only compact heads and defers every full-head bucket to tail_kernel
             t->defer_full = n_full * 20 < (uint64_t)nb;
+            // filtered rank groups (kRkfKeys keys per u64) for the deferring drain
+            if (W >= 10) {
+                uint32_t rb = 1;
+                while ((1ull << rb) <= (uint64_t)nb) ++rb;
+                const uint32_t fw = (48u - std::min(rb, 46u)) / 2u;
+                const uint32_t F = std::min<uint32_t>(std::min<uint32_t>((fw - 1u) / 2u, (32u - std::min(rb, 32u)) / 2u), 8u);
+                t->rkf_rb = rb;
+                t->rkf_fw = fw;
+                t->rkf_F = F >= 2 ? F : 0u;
+                const uint64_t nkeys = 1ull << (2 * W);
+                rkf.assign(std::max<uint64_t>(nkeys / kRkfKeys, 1), 0ull);
+                uint32_t acc = 0;
+                for (uint64_t g = 0; g < rkf.size(); ++g) {
+                    const uint32_t pres = (uint32_t)((filt[g >> 1] >> ((g & 1) * 16)) & 0xFFFFu);
+                    uint64_t w = (uint64_t)pres | ((uint64_t)acc << 16);
+                    uint32_t j = 0;
+                    for (uint32_t bit = 0; bit < 16 && j < 2 && t->rkf_F; ++bit) {
+                        if (!((pres >> bit) & 1u)) continue;
+                        const uint32_t k = (uint32_t)(g * kRkfKeys + bit);
+                        const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
+                        const uint2 h = dents8[rank];
+                        uint32_t field = 0;
+                        // compact head (single record, seeded at its primer start, plain, <= W + 16
+                        // bases) carrying at least F bases after the seed
+                        if (!(h.y & kHead8Full) && ((h.y >> kHead8RecBits) & 31u) >= t->rkf_F)
+                            field = rkf_field_flag(fw) | (h.x >> (32u - 2u * t->rkf_F));
+                        w |= (uint64_t)field << (16u + rb + j * fw);
+                        ++j;
+                    }
+                    rkf[g] = w;
+                    acc += (uint32_t)__builtin_popcount(pres);
+                }
+            }
             filt.assign(1, 0);
         } else {
             uint32_t lg = 6;
@@ -411,6 +446,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->rk, rk.data(), rk.size(), &bytes))) break;
         if ((rc = upload(&t->dents, dents.data(), dents.size(), &bytes))) break;
         if ((rc = upload(&t->dents8, dents8.data(), dents8.size(), &bytes))) break;
+        if ((rc = upload(&t->rkf, rkf.data(), rkf.size(), &bytes))) break;
         if ((rc = upload(&t->binfo, binfo.data(), binfo.size(), &bytes))) break;
         if ((rc = upload(&t->dfilt, dfilt.data(), dfilt.size(), &bytes))) break;
         if ((rc = upload(&t->dgrp, dgrp.data(), dgrp.size(), &bytes))) break;

@@ -12,9 +12,11 @@ back by pickling.  Here one process drives one GPU (torch.distributed, backend
   union of the ranks' hits is exactly the single-GPU hit list.
 * Owned ranges are ordered and hit order never crosses a range boundary, so the
   rank-ordered concatenation of per-rank sorted lists is the global order.
-  ``gather_hits`` is a gatherv: an all_gather of per-rank counts, then one
-  point-to-point transfer per rank into rank 0's buffer.  There is no other
-  data-path collective.
+  The gatherv of the GPU path lives in the library (``native_comm`` ->
+  mp_comm_gather_hits: an RCCL all-gather of the counts, then one grouped
+  ncclSend/ncclRecv per rank into rank 0's buffer); ``gather_hits`` is the same
+  exchange over torch.distributed, for gloo (CPU tests, ranks sharing one GPU,
+  which RCCL does not admit).  There is no other data-path collective.
 * Contig sharding (``contig_shards``): each rank holds only its own whole
   records (a contiguous run of the file's records, balanced by bases) and
   scans them completely; ``gather_hits(..., seq_base=first record)`` shifts
@@ -65,6 +67,19 @@ def contig_shards(lengths: Sequence[int], world: int) -> List[Tuple[int, int]]:
         cuts.append(min(max(c, cuts[-1]), len(lens)))
     cuts.append(len(lens))
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+def native_comm(device: int, group=None):
+    """This rank's RCCL communicator inside libmerpcr_hip (mp_comm_create), for the
+    process-per-GPU layout: rank 0 makes the 128-byte unique id, torch.distributed (any
+    backend, e.g. gloo) carries it to the other ranks -- plumbing only; the hit gather
+    itself (mp_comm_gather_hits) is a grouped ncclSend/ncclRecv over xGMI."""
+    import torch.distributed as dist
+    from ._native import Comm, comm_unique_id
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    obj = [comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return Comm(obj[0], world, rank, device)
 
 
 def gather_hits(local, n_local: int, group=None, dst: int = 0, seq_base: int = 0) -> Optional[object]:

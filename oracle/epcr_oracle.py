@@ -69,7 +69,9 @@ def hash_word(primer: str, W: int) -> Tuple[int, int]:
     Restates ``MerPCR._hash_value`` (core/engine.py:331-355): the primer is
     upper-cased, the first offset whose W characters all have a 2-bit code is
     chosen, and the value packs the first base into the most significant bits.
-    (-1, 0) when the primer is shorter than W or has no such window.
+    (-1, 0) when the primer is shorter than W or has no such window.  Like the
+    reference's ``self.scode[ord(base)]`` (a 256-entry list, engine.py:345), a
+    character beyond U+00FF raises IndexError when the loop reaches it.
     """
     p = primer.upper()
     if len(p) < W:
@@ -77,6 +79,8 @@ def hash_word(primer: str, W: int) -> Tuple[int, int]:
     for off in range(len(p) - W + 1):
         v = 0
         for ch in p[off:off + W]:
+            if ord(ch) > 0xFF:
+                raise IndexError("list index out of range")
             c = _BASE2.get(ch)
             if c is None:
                 break
@@ -319,6 +323,9 @@ def scan_sequence(seq: str, table: OracleTable, p: dict) -> List[Tuple[int, int,
     out: List[Tuple[int, int, int]] = []
     if n <= W:
         return out
+    if not s.isascii() and max(map(ord, s)) > 0xFF:
+        # engine.py:472/497 look every base up in the 256-entry scode list
+        raise IndexError("list index out of range")
     mask = (1 << (2 * W)) - 1
     h = 0
     last_bad = -1  # index of the last non-ACGTU character seen
@@ -397,6 +404,14 @@ def search_lines(records: Sequence[Tuple[str, str]], table: OracleTable, p: dict
             r = table.records[ri]
             lines.append(f"{label}\t{k + 1}..{pos2 + 1}\t{r.sts_id}\t{r.alias}\t({r.direct})")
     return lines
+
+
+def scan_chunk(task) -> List[Tuple[int, int, int]]:
+    """One ProcessPool work item of the reference's -T N execution model
+    (engine.py:412-422: each chunk is scanned as a sequence of its own by a worker
+    process that receives the pickled table); hits shifted to record coordinates."""
+    seq, off, table, p = task
+    return [(k + off, pos2 + off, ri) for k, pos2, ri in scan_sequence(seq, table, p)]
 
 
 def params(**kw) -> dict:

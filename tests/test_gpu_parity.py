@@ -463,3 +463,180 @@ def test_latin1_primer_character_first_search():
     assert len(exp) == 1
     assert _device_lines(eng, recs) == exp
     assert _device_lines(eng, recs) == exp
+
+
+def _multi_case(W, n_sts, seed):
+    """A multi-record synthetic genome (N runs, planted amplicons) and its STS text."""
+    from merpcr_amd import synth
+    sts = synth.make_sts(n_sts, seed=seed, W=W)
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    glen = 2_000_000
+    g = acgt[rng.integers(0, 4, glen)].copy()
+    for _ in range(20):
+        a = int(rng.integers(0, glen - 3000))
+        g[a:a + int(rng.integers(50, 3000))] = ord("N")
+    amps, starts = synth.amplicons(sts, glen, seed, 1, 50, W)
+    for amp, st in zip(amps, starts):
+        if st + len(amp) <= glen:
+            g[st:st + len(amp)] = np.frombuffer(amp, dtype=np.uint8)
+    s = g.tobytes().decode("ascii")
+    seqs = [s[:700_001], s[700_001:700_300], "", s[700_300:1_500_000], s[1_500_000:]]
+    return sts.text(), seqs
+
+
+@pytest.mark.parametrize("W,n_sts,opts", [(8, 3000, {}), (10, 3000, {}), (11, 6000, {}),
+                                          (11, 6000, dict(tails="inline")), (11, 6000, dict(defer=False))])
+def test_sharded_ranges_all_paths(W, n_sts, opts):
+    """Owned (seq, k) ranges partition the hit list exactly through every scan path:
+    dense_kernel (W=8), the exact-LDS scan (W=10), the ranked drain with full-head deferral
+    to tail_kernel (W=11 default), inline tails, no deferral; cuts inside super-steps and
+    next to records' seed offsets (k + hash_offset straddling a cut)."""
+    from merpcr_amd import _native
+    sts_text, seqs = _multi_case(W, n_sts, 30 + W)
+    eng = MerPCR(wordsize=W, mismatches=1)
+    eng.search_options = opts
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    data = eng.encode_sequences(seqs)
+    genome = _native.Genome(0, [len(d) for d in data])
+    for i, d in enumerate(data):
+        if len(d):
+            genome.put(i, d)
+    genome.seal()
+    s = _native.Search(eng.device_table(), genome)
+    if opts:
+        s.set_options(**opts)
+    whole = s.fetch(s.run())
+    assert len(whole) > 100
+    # cuts: mid super-step, at a hit's k, one and W-1 bases after a hit's k (its seed window
+    # lies across the cut), record boundaries
+    k0 = int(whole["pos1"][len(whole) // 3])
+    q0 = int(whole["seq"][len(whole) // 3])
+    k1 = int(whole["pos1"][2 * len(whole) // 3])
+    q1 = int(whole["seq"][2 * len(whole) // 3])
+    cuts = sorted({(0, 0), (0, 17_001), (q0, k0), (q0, k0 + 1), (q1, k1 + W - 1), (1, 100), (3, 0),
+                   (3, 333_333), (len(seqs), 0)})
+    parts = [s.fetch(s.run((a, b, ka, kb))) for (a, ka), (b, kb) in zip(cuts[:-1], cuts[1:])]
+    cat = np.concatenate(parts)
+    assert np.array_equal(cat, whole)
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0]])
+def test_multi_device_engine_matches_single(devices):
+    """MerPCR(devices=[...]) / CLI --gpus: owned ranges over the devices, each packing only
+    its share of the genome, gathered into devices[0]; identical to one device.  (One GPU
+    here: a repeated device takes the device-copy gather, RCCL admitting one rank per GPU.)"""
+    sts_text, seqs = _multi_case(11, 6000, 41)
+    recs = [FASTARecord(defline=f">m{i}", sequence=s) for i, s in enumerate(seqs)]
+    single = MerPCR(wordsize=11, mismatches=1)
+    multi = MerPCR(wordsize=11, mismatches=1, devices=devices)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(single, sts_text, td)
+        assert _load_sts(multi, sts_text, td)
+    exp = _device_lines(single, recs)
+    assert len(exp) > 100
+    assert _device_lines(multi, recs) == exp
+    assert _device_lines(multi, recs[1:]) == _device_lines(single, recs[1:])  # re-laid out, same handles
+    assert len(multi.last_search_stats["devices"]) == len(devices)
+
+
+def test_multi_rccl_gather_one_device():
+    """mp_multi over one device: the RCCL communicator path (ncclCommInitAll, grouped
+    ncclSend/ncclRecv to itself) gathers the hit list."""
+    from merpcr_amd import _native
+    sts_text, seqs = _multi_case(11, 3000, 43)
+    eng = MerPCR(wordsize=11, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    data = eng.encode_sequences(seqs)
+    exp = eng.find_hits([FASTARecord(defline=f">m{i}", sequence=s) for i, s in enumerate(seqs)])
+    m = _native.Multi([0], [eng.device_table()])
+    m.genome([len(d) for d in data])
+    for i, d in enumerate(data):
+        if len(d):
+            m.put(i, d)
+    m.seal()
+    got = m.fetch(m.run())
+    assert len(exp) > 100 and got.tobytes() == exp.tobytes()
+    m.close()
+
+
+def test_comm_gather_single_rank():
+    """mp_comm_* with one rank: unique id -> communicator -> gather into a device buffer."""
+    import torch
+    from merpcr_amd import _native
+    sts_text, seqs = _multi_case(10, 3000, 44)
+    eng = MerPCR(wordsize=10, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    exp = eng.find_hits([FASTARecord(defline=f">m{i}", sequence=s) for i, s in enumerate(seqs)])
+    comm = _native.Comm(_native.comm_unique_id(), 1, 0, 0)
+    out = torch.empty(len(exp) * 24 + 24, dtype=torch.uint8, device="cuda:0")
+    search = eng._dev_search
+    n = comm.gather_hits(search, out.data_ptr(), len(exp) + 1, seq_shift=3)
+    torch.cuda.synchronize()
+    got = np.frombuffer(out[:n * 24].cpu().numpy().tobytes(), dtype=exp.dtype)
+    assert n == len(exp) and np.array_equal(got["seq"], exp["seq"] + 3)
+    assert np.array_equal(got["pos1"], exp["pos1"]) and np.array_equal(got["rec"], exp["rec"])
+    with pytest.raises(_native.NativeError):  # rank 0's buffer too small: MP_E_CAP, nothing sent
+        comm.gather_hits(search, out.data_ptr(), 1)
+    assert comm.last_total == len(exp)
+    comm.close()
+
+
+def _two_rank_worker(rank, world, port, sts_text, seqs, q):
+    import torch
+    import torch.distributed as dist
+    from merpcr_amd import _native
+    from merpcr_amd.dist import as_hits, gather_hits, shard_ranges
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = MerPCR(wordsize=11, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    data = eng.encode_sequences(seqs)
+    genome = _native.Genome(0, [len(d) for d in data])
+    for i, d in enumerate(data):
+        if len(d):
+            genome.put(i, d)
+    genome.seal()
+    s = _native.Search(eng.device_table(), genome)
+    rng = shard_ranges([len(d) for d in data], world)[rank]
+    mine = s.fetch(s.run(rng))  # the HIP path on this rank's owned range
+    buf = torch.from_numpy(np.frombuffer(mine.tobytes() + b"\0" * 24, dtype=np.uint8).copy())
+    got = gather_hits(buf, len(mine))
+    if rank == 0:
+        q.put(as_hits(got).tobytes())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_on_one_gpu():
+    """Two processes on cuda:0, each searching its owned range with the HIP path, gathered
+    over torch.distributed (gloo: RCCL does not admit two ranks on one GPU); the gathered
+    list equals the whole-genome HIP list and the C oracle's."""
+    import socket
+    import torch.multiprocessing as tmp
+    from oracle import c_oracle as C
+    sts_text, seqs = _multi_case(11, 3000, 45)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, sts_text, seqs, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    eng = MerPCR(wordsize=11, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    whole = eng.find_hits([FASTARecord(defline=f">m{i}", sequence=x) for i, x in enumerate(seqs)])
+    table = O.load_sts_lines(sts_text.splitlines(True), 11, 240)
+    ref = C.search(table, [np.frombuffer(x.encode(), dtype=np.uint8) for x in seqs], O.params(wordsize=11, mismatches=1), 8)
+    assert len(whole) > 100 and got == whole.tobytes() == ref.tobytes()
+    assert all(p.exitcode == 0 for p in procs)

@@ -120,3 +120,15 @@ def test_chunked_corpus():
         for t, exp in case["by_threads"].items():
             lines = O.search_lines(recs, table, O.params(**params), threads=int(t))
             assert lines == exp["output"].splitlines(), (case["name"], t)
+
+
+def test_oracle_hash_index_error_kats():
+    """The oracle's hash restates the reference's IndexError for characters beyond U+00FF
+    (errors.json.gz, generated by the reference)."""
+    from oracle import epcr_oracle as O
+    for p, W, exp in load_golden("errors.json.gz")["hash"]:
+        try:
+            got = list(O.hash_word(p, W))
+        except IndexError:
+            got = "IndexError"
+        assert got == exp, (p, W)
