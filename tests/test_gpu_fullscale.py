@@ -1,0 +1,64 @@
+"""GPU parity at the benchmark configs' full table scale.
+
+The bench configs c3/c4/c5 use 100k-STS tables (200k records: 195k distinct keys at
+W=11, 62k at W=8 with a mean fan-out of 3.2 records per key).  Here the real tables
+go through the default kernels over a genome prefix the C oracle scans in seconds
+(c3/c4: 40 Mbp, c5: 12 Mbp), generated exactly as bench.py does (synth.py: N runs,
+soft-masking, every STS planted in both orientations, densely here), and the hit
+lists must be byte-identical.  The table regime -- seed fan-out, prefilter pass rate,
+bucket tails, full-head deferral, dense_kernel's escape buckets -- is the full-size
+one; only the genome is shorter.
+"""
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from merpcr_amd import MerPCR, _native, synth
+from oracle import c_oracle as C
+from oracle import epcr_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+_THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+@pytest.mark.parametrize("name,total,records", [("c3", 40_000_000, 3), ("c4", 40_000_000, 3),
+                                                ("c5", 12_000_000, 2)])
+def test_full_table_prefix_vs_c_oracle(name, total, records):
+    import torch
+    cfg = synth.CONFIGS[name]
+    sts = synth.make_sts(cfg["n_sts"], W=cfg["W"], iupac=cfg["iupac"])
+    eng = MerPCR(wordsize=cfg["W"], margin=cfg["M"], mismatches=cfg["N"], iupac_mode=cfg["I"])
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "c.sts")
+        with open(p, "w") as fh:
+            fh.write(sts.text())
+        assert eng.load_sts_file(p)
+    assert len(eng.sts_records) == 2 * cfg["n_sts"]
+    table = eng.device_table()
+    dev = torch.device("cuda", 0)
+    names, lens, buf, offs, planted = synth.build_genome_torch(
+        total, records, sts, seed=1, N=cfg["N"], M=cfg["M"], W=cfg["W"], nrun=cfg["nrun"], device=dev)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+    genome = _native.Genome(0, lens)
+    for r, n in enumerate(lens):
+        genome.put_device(r, buf.data_ptr() + int(offs[r]), n, stream=stream)
+    genome.seal(stream)
+    search = _native.Search(table, genome)
+    got = search.fetch(search.run(None, stream))
+    stats = search.last_stats()
+    host = buf.cpu().numpy()
+    seqs = [host[int(offs[r]):int(offs[r]) + lens[r]] for r in range(len(lens))]
+    otable = O.load_sts_lines(sts.text().splitlines(True), cfg["W"], 240)
+    prm = O.params(wordsize=cfg["W"], mismatches=cfg["N"], margin=cfg["M"], iupac_mode=cfg["I"])
+    ref = C.search(otable, seqs, prm, _THREADS)
+    search.close()
+    genome.close()
+    assert planted > 10_000 and len(ref) > planted // 2, (planted, len(ref))
+    assert stats["windows"] >= 0.9 * total
+    assert len(got) == len(ref), (len(got), len(ref), stats)
+    assert got.tobytes() == ref.tobytes()
