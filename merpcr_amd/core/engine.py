@@ -415,6 +415,16 @@ class MerPCR:
             out.append(self._codes.sequence_bytes(s))
         return out
 
+    def encode_records(self, fasta_records: Sequence[FASTARecord]) -> List[np.ndarray]:
+        """encode_sequences of the records' sequences; a record from the native FASTA
+        reader hands over its ASCII bytes as they are (no str round trip)."""
+        out = []
+        for r in fasta_records:
+            raw = _raw_ascii(r)
+            out.append(np.frombuffer(raw, dtype=np.uint8) if raw is not None else
+                       self.encode_sequences([r.sequence])[0])
+        return out
+
     def chunk_plan(self, seq_len: int) -> List[Tuple[int, int]]:
         """(offset, length) of each chunk the reference's search scans for a record of
         seq_len bases (engine.py:380-410): T = threads for records of >= 100 kbp, reduced
@@ -441,7 +451,7 @@ class MerPCR:
         (engine.py:412-434) -- overlap hits then appear once per chunk, as in the
         reference's multi-process output."""
         self.device_table()  # registers the primers' non-ASCII codes before the genome is encoded
-        return self._hits_of(self.encode_sequences([r.sequence for r in fasta_records]))
+        return self._hits_of(self.encode_records(fasta_records))
 
     def _hits_of(self, data: List[np.ndarray]) -> np.ndarray:
         if not (self.emulate_chunks and self.threads > 1):
@@ -578,13 +588,13 @@ class MerPCR:
             data, err = [], None
             for r in recs:
                 try:
-                    data.extend(self.encode_sequences([r.sequence]))
+                    data.extend(self.encode_records([r]))
                 except IndexError as e:
                     err = e
                     break
             n_ok = len(data)
             if self.threads > 1 and not self.emulate_chunks and any(
-                    len(self.chunk_plan(len(r.sequence))) > 1 for r in recs[:n_ok]):
+                    len(self.chunk_plan(_seq_len(r))) > 1 for r in recs[:n_ok]):
                 logger.warning("threads > 1: hits are reported once, as with -T 1 (the reference's "
                                "multi-process chunking repeats hits inside chunk overlaps; "
                                "emulate_chunks=True reproduces that output)")
@@ -596,8 +606,8 @@ class MerPCR:
             line_end = np.cumsum(per)
             pos = 0
             for i, rec in enumerate(recs[:n_ok]):
-                logger.info(f"Processing sequence: {rec.label} ({len(rec.sequence)} bp)")
-                self._log_thread_plan(len(rec.sequence))
+                logger.info(f"Processing sequence: {rec.label} ({_seq_len(rec)} bp)")
+                self._log_thread_plan(_seq_len(rec))
                 if per[i]:
                     stop = int(ends[line_end[i] - 1])
                     output.write(text[pos:stop].decode("utf-8"))
@@ -605,8 +615,8 @@ class MerPCR:
                     total += int(per[i])
             if err is not None:
                 rec = recs[n_ok]
-                logger.info(f"Processing sequence: {rec.label} ({len(rec.sequence)} bp)")
-                self._log_thread_plan(len(rec.sequence))
+                logger.info(f"Processing sequence: {rec.label} ({_seq_len(rec)} bp)")
+                self._log_thread_plan(_seq_len(rec))
                 raise err
         finally:
             if to_file:
@@ -626,6 +636,16 @@ class MerPCR:
             h.pos2 += thread_data.offset
             thread_data.hits.append(h)
         return thread_data
+
+
+def _raw_ascii(rec):
+    f = getattr(rec, "raw_ascii", None)
+    return f() if f is not None else None
+
+
+def _seq_len(rec) -> int:
+    raw = _raw_ascii(rec)
+    return len(raw) if raw is not None else len(rec.sequence)
 
 
 def _hit_dtype():

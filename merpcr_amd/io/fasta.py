@@ -41,6 +41,46 @@ def filter_line(line: str) -> str:
     return _DROP.sub("", line)
 
 
+class ReaderRecord(FASTARecord):
+    """A FASTARecord from the native reader: the sequence stays the reader's filtered UTF-8
+    bytes, and the str the reference's API exposes is built on first access.  The device
+    path (MerPCR.search / find_hits) encodes ASCII bytes directly, so the CLI never pays
+    the bytes -> str -> bytes round trip (about 1.4 s per Gbp)."""
+
+    def __init__(self, defline: str, raw: bytes):
+        self._raw = raw
+        self._str = None
+        super().__init__(defline=defline, sequence=None)
+
+    @property
+    def sequence(self) -> str:
+        if self._str is None:
+            self._str = self._raw.decode("utf-8")
+        return self._str
+
+    @sequence.setter
+    def sequence(self, value):
+        if value is not None:  # assigned by the caller: the bytes no longer describe it
+            self._str = value
+            self._raw = None
+
+    def __eq__(self, other):  # equal to a plain FASTARecord with the same fields
+        if isinstance(other, FASTARecord):
+            return (self.defline, self.sequence, self.label) == (other.defline, other.sequence, other.label)
+        return NotImplemented
+
+    __hash__ = None
+
+    def __repr__(self):
+        return f"FASTARecord(defline={self.defline!r}, sequence={self.sequence!r}, label={self.label!r})"
+
+    def raw_ascii(self):
+        """The sequence as ASCII bytes without building the str, or None."""
+        if self._str is None and self._raw is not None and self._raw.isascii():
+            return self._raw
+        return None
+
+
 class FASTALoader:
     """Loads FASTA files into FASTARecord lists (reference: io/fasta.py:15-71)."""
 
@@ -56,7 +96,7 @@ class FASTALoader:
         logger.info(f"Reading FASTA file: {filename}")
         records = []
         for defline, seq in _native.fasta_read(filename, _chunk_bytes):
-            records.append(FASTARecord(defline=defline, sequence=seq.decode("utf-8")))
+            records.append(ReaderRecord(defline, seq))
         logger.info(f"Loaded {len(records)} sequences in {time.time() - start:.2f} seconds")
         return records
 

@@ -105,3 +105,25 @@ def test_missing_and_empty(tmp_path):
     p = tmp_path / "empty.fa"
     p.write_bytes(b"")
     assert FASTALoader.load_file(str(p)) == []
+
+
+def test_reader_records_keep_bytes(tmp_path):
+    """Records from the native reader equal the Python loop's FASTARecords; ASCII sequences
+    reach the engine's encoder as the reader's bytes (no str round trip), and a record with
+    U+017F or a reassigned sequence goes through the str path."""
+    import numpy as np
+    from merpcr_amd import FASTARecord, MerPCR
+    p = tmp_path / "r.fa"
+    p.write_text(">a one\nACGTacgtNN\n>b\nACſGT\n>c\n\n", encoding="utf-8")
+    got = FASTALoader.load_file(str(p))
+    exp = FASTALoader.load_file_py(str(p))
+    assert got == exp and exp == got
+    assert [repr(r) for r in got] == [repr(FASTARecord(r.defline, r.sequence, r.label)) for r in exp]
+    got = FASTALoader.load_file(str(p))
+    assert got[0].raw_ascii() == b"ACGTacgtNN" and got[1].raw_ascii() is None
+    eng = MerPCR()
+    enc = eng.encode_records(got)
+    ref = eng.encode_sequences([r.sequence for r in exp])
+    assert all(np.array_equal(x, y) for x, y in zip(enc, ref))
+    got[0].sequence = "TTTT"
+    assert got[0].raw_ascii() is None and np.array_equal(eng.encode_records(got[:1])[0], np.frombuffer(b"TTTT", np.uint8))
