@@ -132,6 +132,8 @@ struct Table {
     Entry* dents_pad = nullptr;   // W <= kDenseMaxW: ents with every bucket padded to a multiple of 4
     uint32_t dense_F = 0;         // bases after the seed the filter words hold
     uint32_t dense_M = 0;         // their mismatch mask in both halves of a 32-bit word pair
+    uint16_t* dsum = nullptr;     // W <= kDenseSumMaxW, N <= 1: per-key summary (see kDenseSumMaxW)
+    int dsum_mode = 0;            // 0: none, 1: N = 0 form, 2: N = 1 form
     Slot* slots = nullptr;        // W >= 14
     Entry* ents = nullptr;
     DevRec* recs = nullptr;
@@ -281,6 +283,17 @@ constexpr uint32_t kDenseMaxW = 9;
 constexpr uint32_t kDenseAlways = 1u;   // entry not filterable (seed inside the primer, short or IUPAC primer)
 constexpr uint32_t kDensePad = 2u;      // spare slot of an oct
 constexpr uint32_t kDenseMaxF = 7;
+// Per-key summary (W <= kDenseSumMaxW, N <= 1; 16 bits per key, staged in LDS beside the
+// bucket index): a window's oct is loaded only when some record of its key could pass the
+// filter.  N = 0: bit dsum_hash4(all F bases) of each record.  N = 1: F bases split into
+// A (first FA = ceil(F/2)) and B (last F - FA); a window within one mismatch of a record
+// matches it exactly on A or on B (pigeonhole), so bits dsum_hash3(A) and 8 + dsum_hash3(B)
+// are set per record and the window needs one of its two bits.  A hashed bit can only make
+// a window pass that the exact rule rejects, never the reverse.  Buckets the filter cannot
+// carry (escape) have every bit set.
+constexpr uint32_t kDenseSumMaxW = 8;
+__host__ __device__ __forceinline__ uint32_t dsum_hash3(uint32_t v) { return (v ^ (v >> 3) ^ (v >> 6)) & 7u; }
+__host__ __device__ __forceinline__ uint32_t dsum_hash4(uint32_t v) { return (v ^ (v >> 4) ^ (v >> 8) ^ (v >> 12)) & 15u; }
 constexpr uint32_t kDenseOct = 8;
 
 // LDS prefilter bit of a seed key.  Exact (bit = key) when 4^W fits (W <= 10);

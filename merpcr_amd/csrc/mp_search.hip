@@ -60,6 +60,9 @@ struct ScanArgs {
     const uint32_t* dgesc;  // W <= kDenseMaxW: per-32-key escape bits
     const Entry* dents_pad; // W <= kDenseMaxW: Entry per padded entry
     uint32_t dense_M;       // filter mismatch mask
+    const uint16_t* dsum;   // W <= kDenseSumMaxW, N <= 1: per-key summary of the filter bases
+    int dsum_mode;          // 0: none, 1: N = 0 form, 2: N = 1 form
+    uint32_t dense_F;       // filter bases per word
     int defer_full;         // ranked drain: full-head buckets go whole to tail_kernel
     const uint32_t* lfilt;
     const Slot* slots;
@@ -1332,16 +1335,60 @@ __device__ __forceinline__ void dense_full_tests(const ScanArgs& a, uint64_t pm,
     }
 }
 
+// Filter pass bits of one oct (slot 2j in the low half of word j, 2j+1 in the high half;
+// bit j of the result = slot j) against the window's bases W..W+F-1 in both halves of gg:
+// set where at most N of the F bases differ.  Per word: one mismatch bit per base (the low
+// bit of its 2-bit slot), the lowest set bit cleared N times by a packed 16-bit decrement,
+// then a packed minimum with 1 leaves 1 in each half that still holds a mismatch -- seven
+// VALU per two records, where a popcount and compare per half took twelve.
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min1(uint32_t v) {  // per 16-bit half: min(half, 1)
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(v), "v"(0x00010001u));
+    return r;
+}
+template <int kN>  // N when 0..2 (straight-line), -1: the run-time N
+__device__ __forceinline__ uint32_t oct_pass8(const uint4 q, uint32_t gg, uint32_t fmask, int N) {
+    const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+    uint32_t nz = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t x = gg ^ wv[j];
+        u16x2 d = __builtin_bit_cast(u16x2, (x | (x >> 1)) & fmask);
+        if constexpr (kN >= 0) {
+#pragma unroll
+            for (int t = 0; t < kN; ++t) d &= d - (u16x2)(1);
+        } else {
+            for (int t = 0; t < N; ++t) d &= d - (u16x2)(1);
+        }
+        nz |= pk_min1(__builtin_bit_cast(uint32_t, d)) << (2 * j);
+    }
+    const uint32_t p = ~nz;
+    return (p & 0x55u) | ((p >> 15) & 0xAAu);
+}
+// Spare slots of an oct (kDensePad set in the word's half).
+__device__ __forceinline__ uint32_t oct_spares(const uint4 q) {
+    const uint32_t m = kDensePad | (kDensePad << 16);
+    return (uint32_t)__popc((q.x & m) | ((q.y & m) << 1) | ((q.z & m) << 2) | ((q.w & m) << 3));
+}
+
+template <int kN>
 __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     extern __shared__ uint2 s_grp[];
     const uint32_t W = (uint32_t)a.W;
     const uint32_t ngrp = max(1u, (1u << (2 * W)) / 32);
     uint32_t* s_esc = reinterpret_cast<uint32_t*>(s_grp + ngrp);
+    uint32_t* s_sum = s_esc + ngrp;  // dsum_mode: 16-bit summary per key, two per word
     for (uint32_t i = threadIdx.x; i < ngrp; i += kDenseBlock) {
         s_grp[i] = a.dgrp[i];
         s_esc[i] = a.dgesc[i];
     }
+    if (a.dsum_mode) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.dsum);
+        for (uint32_t i = threadIdx.x; i < (1u << (2 * W)) / 2; i += kDenseBlock) s_sum[i] = src[i];
+    }
     __syncthreads();
+    const uint32_t sumF = a.dense_F, sumFB = sumF / 2;
 
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -1424,7 +1471,17 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
                 const uint32_t bq = h & 31u;
                 const uint32_t wb = 31u - (TB + (uint32_t)T);
                 const bool ok = (okm >> wb) & 1u;
-                const bool inl = ok && ((L.x >> bq) & 1u);
+                bool inl = ok && ((L.x >> bq) & 1u);
+                if (a.dsum_mode) {  // the key's summary: no record can pass -> no oct load
+                    const uint32_t sm = s_sum[h >> 1] >> ((h & 1u) << 4);
+                    const uint32_t key = r ? __builtin_amdgcn_alignbit(dh, dl, 32u - r) : dh;
+                    const uint32_t gf = (key << (2 * W)) >> (32u - 2u * sumF);  // bases W..W+F-1
+                    const uint32_t sb = a.dsum_mode == 1
+                                            ? sm >> dsum_hash4(gf)
+                                            : (sm >> dsum_hash3(gf >> (2u * sumFB))) |
+                                                  (sm >> (8u + dsum_hash3(gf & ((1u << (2u * sumFB)) - 1u))));
+                    inl = inl && ((sb & 1u) || ((slowm >> wb) & 1u));
+                }
                 if ((int32_t)L.y < 0 && ok)  // the group holds a key of more than eight records
                     escm |= ((s_esc[h >> 5] >> bq) & 1u) << wb;
                 live |= (uint32_t)inl << T;
@@ -1441,20 +1498,10 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
                 const uint32_t gg = gwin | (gwin << 16);
                 const bool lv = (live >> T) & 1u;
                 const bool sl = (slowm >> (31u - (TB + (uint32_t)T))) & 1u;
-                const uint32_t wv[4] = {q[T].x, q[T].y, q[T].z, q[T].w};
-                uint32_t pbits = 0;
-#pragma unroll
-                for (int h2 = 0; h2 < 4; ++h2) {
-                    const uint32_t x = gg ^ wv[h2];
-                    const uint32_t d = (x | (x >> 1)) & fmask;
-                    pbits |= ((uint32_t)((uint32_t)__popc(d & 0xFFFFu) <= N) << (2 * h2)) |
-                             ((uint32_t)((uint32_t)__popc(d >> 16) <= N) << (2 * h2 + 1));
-                }
-                // spare slots (pad bit) pass with slot 0 and are skipped by the full test
-                const uint32_t spare = (wv[0] & 0x20002u) | ((wv[1] & 0x20002u) >> 1) |
-                                       ((wv[2] & 0x20002u) << 1) | ((wv[3] & 0x20002u) << 2);
+                const uint32_t pbits = oct_pass8<kN>(q[T], gg, fmask, (int)N);
                 pm |= (uint64_t)(lv ? (sl ? 0xFFu : pbits) : 0u) << (8 * T);
-                ncand += lv ? 8u - (uint32_t)__popc(spare) : 0u;
+                // spare slots (pad bit) pass with slot 0 and are skipped by the full test
+                ncand += lv ? 8u - oct_spares(q[T]) : 0u;
             }
             if (__any(pm != 0)) dense_full_tests(a, pm, s_grp, 0u, TB, pb, w0, w1, iv, sbase, n, owned, sp.seq, lane, C);
         }
@@ -1775,8 +1822,13 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
                              ? (uint32_t)occ : 5u;
         s->dense_lds = (sizeof(uint2) + sizeof(uint32_t)) *
                        std::max<size_t>(1, ((size_t)1 << (2 * std::min<int>(t->prm.wordsize, kDenseMaxW))) / 32);
+        if (t->dsum_mode) s->dense_lds += sizeof(uint16_t) * ((size_t)1 << (2 * t->prm.wordsize));
+        if (s->dense_lds > 64 * 1024)
+            for (const void* k : {(const void*)dense_kernel<0>, (const void*)dense_kernel<1>,
+                                  (const void*)dense_kernel<2>, (const void*)dense_kernel<-1>})
+                (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->dense_lds);
         occ = 0;
-        s->dense_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dense_kernel, kDenseBlock, s->dense_lds) ==
+        s->dense_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dense_kernel<1>, kDenseBlock, s->dense_lds) ==
                                hipSuccess && occ > 0) ? (uint32_t)occ : 1u;
         if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
             hipEventCreate(&s->ev2) != hipSuccess || hipEventCreate(&s->ev3) != hipSuccess ||
@@ -1868,6 +1920,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.seq_base = g->d_base; a.seq_len = g->d_len;
     a.spans = s->spans; a.n_spans = n_real_spans;
     a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
+    a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
     a.defer_full = t->defer_full && !s->opt.no_defer;
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
@@ -1913,7 +1966,10 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             if (dense) {
                 const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
                                                                     (uint64_t)s->n_cu * (uint64_t)dense_per_cu);
-                hipLaunchKernelGGL(dense_kernel, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
+                if (a.N == 0) hipLaunchKernelGGL(dense_kernel<0>, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
+                else if (a.N == 1) hipLaunchKernelGGL(dense_kernel<1>, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
+                else if (a.N == 2) hipLaunchKernelGGL(dense_kernel<2>, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
+                else hipLaunchKernelGGL(dense_kernel<-1>, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
             } else if (inl) {
                 if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
                 else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);

@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->rkf); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->rkf); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -261,6 +261,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         std::vector<Entry> dents_pad;
         std::vector<uint2> dgrp;
         std::vector<uint32_t> dgesc;
+        std::vector<uint16_t> dsum;
         std::vector<uint2> dents8;
         std::vector<uint64_t> rkf;
         std::vector<Slot> slots;
@@ -361,6 +362,24 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                         for (uint32_t j = bcount[b]; j < kDenseOct; ++j)
                             dfilt[qfirst[b] + j] = (uint16_t)(dfilt[qfirst[b]] | kDensePad);
                 }
+                // per-key summary of the inline buckets' filter bases
+                if (W <= kDenseSumMaxW && p.mismatches <= 1 && F >= (p.mismatches ? 2u : 1u)) {
+                    t->dsum_mode = p.mismatches ? 2 : 1;
+                    const uint32_t FB = F / 2, fbm = (1u << (2 * FB)) - 1u;
+                    dsum.assign(nkeys, 0);
+                    for (uint32_t k = 0; k < nkeys; ++k) {
+                        const uint32_t b = by_key[k];
+                        if (b == 0xFFFFFFFFu) continue;
+                        if (!inline_ok(b)) { dsum[k] = 0xFFFFu; continue; }
+                        uint32_t sm = 0;
+                        for (uint32_t j = 0; j < bcount[b]; ++j) {
+                            const uint32_t gf = (uint32_t)dfilt[qfirst[b] + j] >> (16 - 2 * F);  // F bases
+                            if (p.mismatches == 0) sm |= 1u << dsum_hash4(gf);
+                            else sm |= (1u << dsum_hash3(gf >> (2 * FB))) | (1u << (8 + dsum_hash3(gf & fbm)));
+                        }
+                        dsum[k] = (uint16_t)sm;
+                    }
+                }
             }
             uint64_t n_full = 0;
             for (uint32_t b = 0; b < nb; ++b) {
@@ -451,6 +470,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->dfilt, dfilt.data(), dfilt.size(), &bytes))) break;
         if ((rc = upload(&t->dgrp, dgrp.data(), dgrp.size(), &bytes))) break;
         if ((rc = upload(&t->dgesc, dgesc.data(), dgesc.size(), &bytes))) break;
+        if ((rc = upload(&t->dsum, dsum.data(), dsum.size(), &bytes))) break;
         if ((rc = upload(&t->dents_pad, dents_pad.data(), dents_pad.size(), &bytes))) break;
         if ((rc = upload(&t->ents, ents.data(), ents.size(), &bytes))) break;
         if ((rc = upload(&t->recs, recs.data(), recs.size(), &bytes))) break;
