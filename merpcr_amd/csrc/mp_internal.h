@@ -121,6 +121,8 @@ struct Table {
     uint2* rk = nullptr;          // W <= 13: rank bitmap
     Entry* dents = nullptr;       // W <= 13: bucket heads by key rank
     uint2* dents8 = nullptr;      // W <= 13: 8-B heads {primer-1 bases W..W+15, rec | (l1-W)<<26 | full<<31}
+    uint4* dents16 = nullptr;     // h16: 16-B heads {bases W..W+15, plain bits, never bits, as dents8.y}
+    int h16 = 0;                  // many heads need plain/never masks (IUPAC primers): 16-B heads
     uint64_t* rkf = nullptr;      // W <= 13: filtered rank groups, one u64 per 16 keys (see kRkf*)
     uint32_t rkf_rb = 0;          // rank prefix bits in an rkf group
     uint32_t rkf_fw = 0;          // bits per filter field (2 fields per group)
@@ -222,7 +224,7 @@ __device__ __forceinline__ uint64_t ext1(const uint64_t* __restrict__ p, uint64_
 }
 
 // Spaced mask (bit 62-2i) for primer-chunk positions i < b, 0 <= b <= 32.
-__device__ __forceinline__ uint64_t sp_lt(int b) {
+__host__ __device__ __forceinline__ uint64_t sp_lt(int b) {
     return b <= 0 ? 0ull : (b >= 32 ? kEven : (kEven & (~0ull << (64 - 2 * b))));
 }
 

@@ -54,6 +54,7 @@ struct ScanArgs {
     const uint2* rk;        // W <= 13: rank bitmap
     const Entry* dents;     // W <= 13: bucket heads by rank
     const uint2* dents8;    // W <= 13: 8-B heads
+    const uint4* dents16;   // W <= 13, Table::h16: 16-B heads (primers with IUPAC bases after the seed)
     const uint2* binfo;     // W <= kDenseMaxW: bucket {first padded entry, records} by key rank
     const uint16_t* dfilt;  // W <= kDenseMaxW: filter word per padded entry
     const uint2* dgrp;      // W <= kDenseMaxW: per-32-key bucket index
@@ -684,6 +685,21 @@ __device__ __forceinline__ Entry head8_entry(const uint2 c, uint32_t h, uint32_t
     return e;
 }
 
+// Entry of a 16-B head (kHead8Full clear in .w): the seed key h supplies primer-1 bases
+// [0, W) (plain), .x bases W..W+15, .y / .z their plain / never bits (bit 30-2j).
+__device__ __forceinline__ Entry head16_entry(const uint4 c, uint32_t h, uint32_t W) {
+    Entry e;
+    const uint32_t L = (c.w >> kHead8RecBits) & 31u;
+    e.code = ((uint64_t)h << (64 - 2 * W)) | ((uint64_t)c.x << (32 - 2 * W));
+    e.rec = c.w & ((1u << kHead8RecBits) - 1u);
+    e.hash_off = 0;
+    e.l1 = (uint16_t)(W + L);
+    e.pmask = sp_lt((int)W) | ((uint64_t)c.y << (32 - 2 * W)) | ((uint64_t)c.z << (33 - 2 * W));
+    e.xstart = 0;
+    e.count = 1;
+    return e;
+}
+
 // Bucket head of seed key h (W <= 13: rank of h in the exact bitmap; above: slot).
 template <int kMode>
 __device__ __forceinline__ bool bucket_head(const ScanArgs& a, uint32_t h, Entry& e0) {
@@ -810,10 +826,15 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
 // full head sends its whole bucket to tail_kernel (its first entry is in the head's low
 // word), so the drain never reads a 32-B Entry.  Compact heads whose primer span holds a
 // genome exception base take the general candidate test (rare: all lanes must call).
+// kH16: 16-B heads (Table::h16) -- .x bases W..W+15, .y plain bits, .z never bits, .w the
+// 8-B head's second word; a position that is neither (an IUPAC base under I=1) is skipped,
+// so the count is a lower bound and the survivor is not exact.
+template <bool kH16>
 __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
-                                              bool l, uint32_t p, const uint2 c, uint64_t G, uint32_t x, int lane,
+                                              bool l, uint32_t p, const uint4 c4, uint64_t G, uint32_t x, int lane,
                                               uint32_t& ncand, SurvChunk& C, SurvChunk& TC) {
     const uint32_t W = (uint32_t)a.W;
+    const uint2 c = make_uint2(c4.x, c4.w);  // the 8-B head's words
     const bool full = l && (c.y & kHead8Full);
     const uint32_t L = (c.y >> kHead8RecBits) & 31u;  // l1 - W
     const uint32_t l1 = W + L;
@@ -825,14 +846,23 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
     const uint32_t g = (uint32_t)((G << (2u * W)) >> 32);
     const uint32_t xx = g ^ c.x;
     const uint32_t inm = L >= 16u ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (2u * L));
-    const uint32_t d = (xx | (xx >> 1)) & 0x55555555u & inm;
+    uint32_t d;
+    bool exact = true;
+    if constexpr (kH16) {
+        d = (((xx | (xx >> 1)) & c4.y) | c4.z) & 0x55555555u & inm;
+        exact = ((c4.y | c4.z) & 0x55555555u & inm) == (0x55555555u & inm);
+    } else {
+        d = (xx | (xx >> 1)) & 0x55555555u & inm;
+    }
     const int32_t p0 = (int32_t)L - a.X;  // protected: relative positions >= L - X
     const uint32_t prot = p0 <= 0 ? inm : (p0 >= 16 ? 0u : inm & (0xFFFFFFFFu >> (2 * p0)));
     bool surv = act && !(d & prot) && __popc(d) <= a.N;
-    bool exact = true;
     ncand += act;
     if (__any(general)) {
-        const Entry e = head8_entry(c, (uint32_t)(G >> (64u - 2u * W)), W);
+        const uint32_t hk = (uint32_t)(G >> (64u - 2u * W));
+        Entry e;
+        if constexpr (kH16) e = head16_entry(c4, hk, W);
+        else e = head8_entry(c, hk, W);
         uint32_t k2 = 0;
         bool ex2 = false;
         const bool s2 = candidate(a, R, sbase, n, general, p, e, ncand, k2, G, x, true, ex2);
@@ -866,7 +896,7 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
 
 // drain_seeds for the ranked queue (kMode 1, 1): the head comes straight from the
 // queued key rank -- one dependent load (the 8-B head) per seed instead of two.
-template <bool kInline, bool kDefer>
+template <bool kInline, bool kDefer, bool kH16 = false>
 __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
                                              uint32_t qn, int lane, uint32_t& ncand, WaveLds& L,
                                              SurvChunk& C, SurvChunk& TC) {
@@ -877,6 +907,17 @@ __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs&
         const uint32_t pa = R.base + (la ? (uint32_t)L.rq.q[ea] : 0u);
         const uint32_t pb = R.base + (lb ? (uint32_t)L.rq.q[eb] : 0u);
         const uint32_t qa = la ? L.rq.r[ea] : 0u, qb = lb ? L.rq.r[eb] : 0u;
+        if constexpr (kH16) {  // deferring drain over 16-B heads
+            const uint4 ca = a.dents16[qa];
+            const uint4 cb = a.dents16[qb];
+            uint64_t Ga, Gb;
+            uint32_t xa, xb;
+            window_from_regs(a, R, sbase, pa, true, Ga, xa);
+            window_from_regs(a, R, sbase, pb, true, Gb, xb);
+            drain_compact<true>(a, R, sbase, n, la, pa, ca, Ga, xa, lane, ncand, C, TC);
+            if (b + 64 < qn) drain_compact<true>(a, R, sbase, n, lb, pb, cb, Gb, xb, lane, ncand, C, TC);
+            continue;
+        }
         const uint2 ca = a.dents8[qa];
         const uint2 cb = a.dents8[qb];
         uint64_t Ga, Gb;
@@ -884,8 +925,9 @@ __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs&
         window_from_regs(a, R, sbase, pa, true, Ga, xa);
         window_from_regs(a, R, sbase, pb, true, Gb, xb);
         if constexpr (kDefer) {  // compact heads tested here, full-head buckets to tail_kernel
-            drain_compact(a, R, sbase, n, la, pa, ca, Ga, xa, lane, ncand, C, TC);
-            if (b + 64 < qn) drain_compact(a, R, sbase, n, lb, pb, cb, Gb, xb, lane, ncand, C, TC);
+            drain_compact<false>(a, R, sbase, n, la, pa, make_uint4(ca.x, 0u, 0u, ca.y), Ga, xa, lane, ncand, C, TC);
+            if (b + 64 < qn)
+                drain_compact<false>(a, R, sbase, n, lb, pb, make_uint4(cb.x, 0u, 0u, cb.y), Gb, xb, lane, ncand, C, TC);
             continue;
         }
         const uint32_t ha = (uint32_t)(Ga >> shw), hb = (uint32_t)(Gb >> shw);
@@ -1094,7 +1136,7 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
     }
 };
 
-template <int kMode, bool kInline, int kK = 1, bool kDefer = false>
+template <int kMode, bool kInline, int kK = 1, bool kDefer = false, bool kH16 = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
@@ -1234,7 +1276,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     }
                 }
                 wave_sync();
-                if (qn) drain_ranked<kInline, kDefer>(a, R, sbase, n, qn, lane, ncand, L, C, TC);
+                if (qn) drain_ranked<kInline, kDefer, kH16>(a, R, sbase, n, qn, lane, ncand, L, C, TC);
                 wave_sync();
                 r0 += kSeedQR;
             } while (r0 < tot);
@@ -1922,7 +1964,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
     a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
     a.defer_full = t->defer_full && !s->opt.no_defer;
-    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.lfilt = t->lfilt;
+    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
     a.planes = t->planes; a.pchars = t->pchars;
@@ -1977,8 +2019,12 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
                 else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
             } else {
                 if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h16)
+                    hipLaunchKernelGGL((scan_kernel<1, false, 2, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
                 else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
                     hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct && a.defer_full && t->h16)
+                    hipLaunchKernelGGL((scan_kernel<1, false, 1, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
                 else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);
                 else if (t->filt_direct && a.defer_full)
                     hipLaunchKernelGGL((scan_kernel<1, false, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);

@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->rkf); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->rkf); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -263,6 +263,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         std::vector<uint32_t> dgesc;
         std::vector<uint16_t> dsum;
         std::vector<uint2> dents8;
+        std::vector<uint4> dents16;
         std::vector<uint64_t> rkf;
         std::vector<Slot> slots;
         if (t->filt_direct) {
@@ -381,6 +382,30 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                     }
                 }
             }
+            // 16-B form of a single-record head seeded at its primer start, plain over the
+            // seed, at most W + 16 bases: bases W..W+15 with their plain / never bits (an IUPAC
+            // base under I=1 is neither); {0, 0, 0, kHead8Full} when the record does not fit
+            auto entry16 = [&](const Entry& e) {
+                const uint64_t seed = sp_lt((int)W);
+                const bool fits = e.count == 1 && e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 16 &&
+                                  e.rec < (1u << kHead8RecBits) && (e.pmask & seed) == seed &&
+                                  ((e.pmask >> 1) & seed) == 0;
+                if (!fits) return make_uint4(0u, 0u, 0u, kHead8Full);
+                return make_uint4((uint32_t)((e.code << (2 * W)) >> 32),
+                                  (uint32_t)(((e.pmask & kEven) << (2 * W)) >> 32),
+                                  (uint32_t)((((e.pmask >> 1) & kEven) << (2 * W)) >> 32),
+                                  e.rec | ((uint32_t)(e.l1 - W) << kHead8RecBits));
+            };
+            uint64_t n_full8 = 0, n_full16 = 0;
+            for (uint32_t b = 0; b < nb; ++b) {
+                const Entry& e = ents[boff[b]];
+                n_full8 += (e.count != 1 || (entry8(e).y & kHead8Full)) ? 1u : 0u;
+                n_full16 += (entry16(e).w & kHead8Full) ? 1u : 0u;
+            }
+            // 16-B heads when they make the deferring drain possible (full heads under 5%) and
+            // the 8-B heads do not (c4: 10% IUPAC primer bases)
+            t->h16 = W >= 10 && n_full16 * 20 < (uint64_t)nb && n_full8 * 20 >= (uint64_t)nb;
+            if (t->h16) dents16.resize(std::max<uint32_t>(nb, 1));
             uint64_t n_full = 0;
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint32_t k = bkey[b];
@@ -393,7 +418,14 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                 if (dents8[rank].y & kHead8Full) {
                     dents8[rank].x = boff[b];
                     dents8[rank].y = kHead8Full | head8_filter(b);
-                    ++n_full;
+                    if (!t->h16) ++n_full;
+                }
+                if (t->h16) {
+                    dents16[rank] = entry16(e);
+                    if (dents16[rank].w & kHead8Full) {
+                        dents16[rank] = make_uint4(boff[b], 0u, 0u, kHead8Full | head8_filter(b));
+                        ++n_full;
+                    }
                 }
                 if (W <= kDenseMaxW) binfo[rank] = make_uint2(qfirst[b], bcount[b]);
             }
@@ -465,6 +497,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->rk, rk.data(), rk.size(), &bytes))) break;
         if ((rc = upload(&t->dents, dents.data(), dents.size(), &bytes))) break;
         if ((rc = upload(&t->dents8, dents8.data(), dents8.size(), &bytes))) break;
+        if ((rc = upload(&t->dents16, dents16.data(), dents16.size(), &bytes))) break;
         if ((rc = upload(&t->rkf, rkf.data(), rkf.size(), &bytes))) break;
         if ((rc = upload(&t->binfo, binfo.data(), binfo.size(), &bytes))) break;
         if ((rc = upload(&t->dfilt, dfilt.data(), dfilt.size(), &bytes))) break;

@@ -249,6 +249,7 @@ def test_cli_threads_emulation(tmp_path):
 @pytest.mark.parametrize("tails", ["auto", "inline", "kernel"])
 @pytest.mark.parametrize("W,n_sts,glen,N,I,iupac", [(8, 4000, 3_000_000, 1, 0, 0.0), (9, 6000, 2_000_000, 2, 1, 0.1),
                                                     (11, 20000, 4_000_000, 1, 1, 0.1),
+                                                    (11, 20000, 4_000_000, 2, 0, 0.1),  # 16-B heads, never bits
                                                     (12, 40000, 4_000_000, 1, 0, 0.0)])  # > 65536 keys: 2-bit LDS filter
 def test_dense_tables_vs_c_oracle(tails, W, n_sts, glen, N, I, iupac):
     """Larger tables (multi-record buckets everywhere at W=8) through the default kernels
