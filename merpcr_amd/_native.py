@@ -133,6 +133,30 @@ def _sig(lib):
     lib.mp_format_hits.argtypes = [P, c_uint64, P, P, c_uint32, P, P, c_uint32, P, c_uint64, u64p]
 
 
+def _share_hip_runtime():
+    """One HIP runtime per process.  A PyTorch-ROCm wheel bundles its own libamdhip64
+    (soname libamdhip64.so.7, the same as /opt/rocm's), which libtorch_hip finds by file
+    name.  If this library loaded /opt/rocm's copy first, a later `import torch` would map
+    the second copy and its device init would fail ("No HIP GPUs are available").  So when
+    torch is installed its runtime is mapped first (by path, RTLD_GLOBAL, without importing
+    torch); libmerpcr_hip's NEEDED libamdhip64.so.7 then resolves to it, and torch later
+    finds the same file already mapped."""
+    import importlib.util
+    if os.environ.get("MERPCR_SYSTEM_HIP") == "1":
+        return
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+            return
+
+
 def lib():
     """The loaded library; raises if it has not been built."""
     global _lib
@@ -141,6 +165,7 @@ def lib():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "(the MI355X engine has no CPU fallback)")
+        _share_hip_runtime()
         l = ctypes.CDLL(LIB_PATH)
         _sig(l)
         if l.mp_abi_version() != 1:

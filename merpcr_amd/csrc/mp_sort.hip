@@ -48,219 +48,6 @@ __global__ void unpack_keys(const uint64_t* __restrict__ key, uint64_t n, unsign
     lo[i] = (((k & ((1ull << low_bits) - 1ull)) >> try_bits) << 32) | (k & ((1ull << try_bits) - 1ull));
 }
 
-// ---------------------------------------------------------------- device-count bucket sort
-// The common case (the order key fits 64 bits) sorts without the host knowing the hit
-// count: it is read from counters[0] on the device, so the sort follows pair_kernel on
-// the stream with no host round trip.  Keys are bucketed by their top bits (global k:
-// hits spread over the genome), counted, scattered, and each bucket is ranked in LDS by
-// one workgroup that writes the decoded mp_hit records straight to the output.  A bucket
-// larger than kSortCap (hits piled on a few positions, e.g. a dense repeat) sets
-// counters[kSortOverflow]; the host then sorts with rocPRIM instead.
-constexpr uint32_t kSortCap = 2048;
-constexpr unsigned kMaxBucketBits = 16;
-
-// Raw hits arrive in runs of one bucket (a survivor's tries, a wave's batch of nearby
-// survivors; IUPAC primers over N runs pile thousands on a few positions).  Same-address
-// atomics serialise at the L2, so each wave collapses its runs of equal buckets: the run
-// head adds the run length once and hands the base to the run's other lanes.
-__device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint32_t& head, uint32_t& len) {
-    const uint32_t prev = (uint32_t)__shfl_up((int)b, 1, 64);
-    const uint64_t heads = __ballot(on && (lane == 0 || prev != b));
-    const uint64_t upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
-    head = upto ? 63u - (uint32_t)__clzll(upto) : 0u;  // this lane's run head
-    const uint64_t above = heads & ~((2ull << lane) - 1ull);
-    const uint64_t onm = __ballot(on);
-    const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1u : 64u - (uint32_t)__clzll(onm);
-    len = end - (uint32_t)lane;  // meaningful on heads only
-}
-
-__global__ void bucket_hist(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
-                            const unsigned long long* __restrict__ counters, uint64_t cap, unsigned try_bits,
-                            unsigned low_bits, unsigned shift, uint64_t* __restrict__ keys, uint32_t* __restrict__ cnt) {
-    const uint64_t n = counters[0] < cap ? counters[0] : cap;
-    const int lane = threadIdx.x & 63;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
-        const uint64_t i = base + (uint64_t)lane;  // wave-uniform loop: the ballots see every lane
-        const bool on = i < n;
-        uint32_t b = 0xFFFFFFFFu;
-        if (on) {
-            const uint64_t l = lo[i];
-            const uint64_t key = (hi[i] << low_bits) | ((l >> 32) << try_bits) | (l & 0xFFFFFFFFull);
-            keys[i] = key;
-            b = (uint32_t)(key >> shift);
-        }
-        uint32_t head, len;
-        bucket_runs(b, on, lane, head, len);
-        if (on && head == (uint32_t)lane) atomicAdd(&cnt[b], len);
-    }
-}
-
-// exclusive scan of the bucket counts (one 1024-thread workgroup, <= 64 buckets per
-// thread held in registers: one load round trip); cursor = offset
-__global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restrict__ cnt, uint32_t nb,
-                                                       uint32_t* __restrict__ off, uint32_t* __restrict__ cursor) {
-    __shared__ uint32_t s_part[1024];
-    const uint32_t per = (nb + 1023) / 1024;  // <= 64 (nb <= 2^16)
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t v[64];
-    uint32_t sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 64; ++j) {
-        v[j] = j < per && b0 + j < nb ? cnt[b0 + j] : 0u;
-        sum += v[j];
-    }
-    s_part[threadIdx.x] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t x = threadIdx.x >= o ? s_part[threadIdx.x - o] : 0u;
-        __syncthreads();
-        s_part[threadIdx.x] += x;
-        __syncthreads();
-    }
-    uint32_t run = s_part[threadIdx.x] - sum;
-#pragma unroll
-    for (uint32_t j = 0; j < 64; ++j) {
-        if (j < per && b0 + j < nb) {
-            off[b0 + j] = run;
-            cursor[b0 + j] = run;
-        }
-        run += v[j];
-    }
-    if (threadIdx.x == 1023) off[nb] = s_part[1023];
-}
-
-__global__ void bucket_scatter(const uint64_t* __restrict__ keys, const unsigned long long* __restrict__ counters,
-                               uint64_t cap, unsigned shift, uint32_t* __restrict__ cursor, uint64_t* __restrict__ out) {
-    const uint64_t n = counters[0] < cap ? counters[0] : cap;
-    const int lane = threadIdx.x & 63;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
-        const uint64_t i = base + (uint64_t)lane;
-        const bool on = i < n;
-        const uint64_t key = on ? keys[i] : 0ull;
-        const uint32_t b = on ? (uint32_t)(key >> shift) : 0xFFFFFFFFu;
-        uint32_t head, len;
-        bucket_runs(b, on, lane, head, len);
-        uint32_t pos = 0;
-        if (on && head == (uint32_t)lane) pos = atomicAdd(&cursor[b], len);
-        pos = (uint32_t)__shfl((int)pos, (int)head, 64) + ((uint32_t)lane - head);
-        if (on) out[pos] = key;
-    }
-}
-
-// One workgroup per bucket: the keys (unique: one hit per (k, record, try)) are ranked by
-// counting the smaller ones, and each is decoded as decode_kernel does.
-__global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
-                                                          unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
-                                                          const uint64_t* __restrict__ seq_len, uint32_t n_seq,
-                                                          const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
-                                                          mp_hit* __restrict__ out, unsigned long long* __restrict__ counters) {
-    __shared__ uint64_t s_k[kSortCap];
-    const uint32_t start = off[blockIdx.x], m = off[blockIdx.x + 1] - start;
-    if (m == 0) return;
-    if (m > kSortCap) {
-        if (threadIdx.x == 0) atomicOr(&counters[kSortOverflow], 1ull);
-        return;
-    }
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
-    const bool small = m <= 256;  // rank by counting; larger buckets: bitonic sort in LDS
-    if (!small) {
-        uint32_t P = 512;
-        while (P < m) P <<= 1;
-        for (uint32_t i = m + threadIdx.x; i < P; i += blockDim.x) s_k[i] = ~0ull;
-        __syncthreads();
-        for (uint32_t k = 2; k <= P; k <<= 1) {
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-                    const uint32_t ij = i ^ j;
-                    if (ij > i) {
-                        const uint64_t x = s_k[i], y = s_k[ij];
-                        if ((x > y) == ((i & k) == 0)) {
-                            s_k[i] = y;
-                            s_k[ij] = x;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-        const uint64_t key = s_k[i];
-        uint32_t r = i;
-        if (small) {
-            r = 0;
-            for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
-        }
-        const uint64_t gk = key >> low_bits;
-        const uint32_t rank = (uint32_t)((key & ((1ull << low_bits) - 1ull)) >> try_bits);
-        const uint32_t tr = (uint32_t)(key & ((1ull << try_bits) - 1ull));
-        uint32_t a = 0, b = n_seq;  // last sequence with base <= gk
-        while (b - a > 1) {
-            const uint32_t mid = (a + b) >> 1;
-            if (seq_base[mid] <= gk) a = mid;
-            else b = mid;
-        }
-        const uint64_t k = gk - seq_base[a];
-        const uint32_t rec = inv_rank[rank];
-        const uint64_t len = seq_len[a];
-        const uint64_t size = recs[rec].size;
-        const uint64_t e = size > len - k ? len - k : size;
-        mp_hit h;
-        h.pos1 = k;
-        h.pos2 = (uint64_t)((int64_t)(k + e) - 1 + try_offset(tr));
-        h.seq = a;
-        h.rec = rec;
-        out[start + r] = h;
-    }
-}
-
-bool sort_hits_device_ok(const Search* s) {
-    const unsigned hi_bits = bits_for(s->genome->total);
-    const unsigned try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
-    return hi_bits + s->table->rank_bits + try_bits <= 64 && s->opt.sort == MP_SORT_AUTO;
-}
-
-int alloc_sort_buckets(Search* s) {
-    if (!s->bucket) MP_HIP_CHECK(hipMalloc(&s->bucket, (3ull << kMaxBucketBits) * 4 + 16));
-    return MP_OK;
-}
-
-int sort_hits_device(Search* s, hipStream_t st) {
-    const unsigned hi_bits = bits_for(s->genome->total);
-    const unsigned try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
-    const unsigned low_bits = s->table->rank_bits + try_bits;
-    const unsigned key_bits = hi_bits + low_bits;
-    // ~32 hits per bucket at the buffer's capacity (the count is not known on the host)
-    unsigned bb = bits_for(s->cap / 32);
-    bb = std::min(std::max(bb, 6u), kMaxBucketBits);
-    if (s->opt.sort_bucket_bits > 0) bb = std::min((unsigned)s->opt.sort_bucket_bits, kMaxBucketBits);
-    bb = std::min(bb, key_bits);
-    const unsigned shift = key_bits - bb;
-    const uint32_t nb = 1u << bb;
-    const int arc = alloc_sort_buckets(s);
-    if (arc) return arc;
-    uint32_t* cnt = s->bucket;
-    uint32_t* off = cnt + (1u << kMaxBucketBits);
-    uint32_t* cursor = off + (1u << kMaxBucketBits) + 1;
-    MP_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)nb * 4, st));
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((s->cap + 255) / 256, 2048);
-    hipLaunchKernelGGL(bucket_hist, dim3(grid), dim3(256), 0, st, s->keys, s->keys + s->cap, s->counters, s->cap,
-                       try_bits, low_bits, shift, s->tmp_lo, cnt);
-    MP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, cnt, nb, off, cursor);
-    MP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, s->counters, s->cap, shift, cursor,
-                       s->tmp_hi);
-    MP_HIP_CHECK(hipGetLastError());
-    const Genome* g = s->genome;
-    hipLaunchKernelGGL(bucket_sort_decode, dim3(nb), dim3(256), 0, st, s->tmp_hi, off, try_bits, low_bits, g->d_base,
-                       g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->counters);
-    MP_HIP_CHECK(hipGetLastError());
-    return MP_OK;
-}
 
 int sort_hits(Search* s, uint64_t n, hipStream_t st) {
     if (n < 2) return MP_OK;

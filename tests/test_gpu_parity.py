@@ -51,6 +51,20 @@ def test_library_loaded_and_device_visible():
     assert _native.device_count() >= 1
 
 
+def test_search_then_torch_in_one_process():
+    """A search before `import torch` leaves torch's device init working: the process
+    maps one HIP runtime (_native._share_hip_runtime)."""
+    import subprocess
+    import sys
+    code = ("import __graft_entry__ as g; g.smoke(); import torch; "
+            "x = torch.ones(4, device='cuda:0'); assert float(x.sum()) == 4.0; "
+            "maps = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}; "
+            "assert len(maps) == 1, maps; print('one runtime', maps)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_bundled_kat():
     g = load_golden("bundled.json.gz")
     for case in g["cases"]:
