@@ -134,6 +134,9 @@ typedef struct mp_search_options {
     uint64_t hit_cap;           /* initial raw-hit list capacity (entries); 0 = default */
     uint64_t surv_cap;          /* initial fingerprint-survivor list capacity; 0 = default */
     uint64_t tail_cap;          /* initial bucket-tail reference list capacity; 0 = default */
+    int32_t no_rank_filter;     /* 1: level-2 probes read the plain rank bitmap, without the
+                                   filtered rank groups' primer-base filter */
+    int32_t reserved;
 } mp_search_options;
 /* Replace the handle's options (reallocating the lists to the given capacities). */
 int mp_search_set_options(void* search, const mp_search_options* opt);

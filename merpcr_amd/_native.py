@@ -59,7 +59,8 @@ MP_SORT = {"auto": 0, "radix64": 1, "radix128": 2}
 class MPSearchOptions(ctypes.Structure):
     _fields_ = [("tails", c_int32), ("no_defer", c_int32), ("no_dense", c_int32), ("sort", c_int32),
                 ("sort_bucket_bits", c_int32), ("pair_blocks_per_cu", c_int32),
-                ("hit_cap", c_uint64), ("surv_cap", c_uint64), ("tail_cap", c_uint64)]
+                ("hit_cap", c_uint64), ("surv_cap", c_uint64), ("tail_cap", c_uint64),
+                ("no_rank_filter", c_int32), ("reserved", c_int32)]
 
 
 HIT_DTYPE = np.dtype([("pos1", "<u8"), ("pos2", "<u8"), ("seq", "<u4"), ("rec", "<u4")])
@@ -278,11 +279,12 @@ class Search:
         check(lib().mp_search_create(table._h, genome._h, ctypes.byref(self._h)))
 
     def set_options(self, tails="auto", defer=True, dense=True, sort="auto", sort_bucket_bits=0,
-                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0):
+                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True):
         """Kernel-path selection and initial list capacities (mp_search_set_options);
         the defaults are the library's automatic choices."""
         o = MPSearchOptions(MP_TAILS[tails], 0 if defer else 1, 0 if dense else 1, MP_SORT[sort],
-                            sort_bucket_bits, pair_blocks_per_cu, hit_cap, surv_cap, tail_cap)
+                            sort_bucket_bits, pair_blocks_per_cu, hit_cap, surv_cap, tail_cap,
+                            0 if rank_filter else 1, 0)
         check(lib().mp_search_set_options(self._h, ctypes.byref(o)))
 
     def regrowths(self) -> int:

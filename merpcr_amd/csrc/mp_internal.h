@@ -123,10 +123,8 @@ struct Table {
     uint2* dents8 = nullptr;      // W <= 13: 8-B heads {primer-1 bases W..W+15, rec | (l1-W)<<26 | full<<31}
     uint4* dents16 = nullptr;     // h16: 16-B heads {bases W..W+15, plain bits, never bits, as dents8.y}
     int h16 = 0;                  // many heads need plain/never masks (IUPAC primers): 16-B heads
-    uint64_t* rkf = nullptr;      // W <= 13: filtered rank groups, one u64 per 16 keys (see kRkf*)
-    uint32_t rkf_rb = 0;          // rank prefix bits in an rkf group
-    uint32_t rkf_fw = 0;          // bits per filter field (2 fields per group)
-    uint32_t rkf_F = 0;           // primer-1 bases W..W+F-1 a filter field holds (0: no filter)
+    uint64_t* kgrp = nullptr;     // W 11..13: key groups, one u64 per 16 keys (see kKgrpKeys)
+    uint32_t kgrp_F = 0;          // primer-1 bases W..W+F-1 a key-group field holds (0: no key groups)
     uint2* binfo = nullptr;       // W <= kDenseMaxW: per key rank {first padded entry, records}
     uint16_t* dfilt = nullptr;    // W <= kDenseMaxW: 2-B filter word per padded entry (kDenseAlways...)
     uint2* dgrp = nullptr;        // W <= kDenseMaxW: per 32 keys {inline-bucket bits, first oct | any escape << 31}
@@ -321,16 +319,18 @@ __host__ __device__ __forceinline__ uint32_t lds_block_mask(uint32_t x, uint32_t
     return m;
 }
 
-// Filtered rank groups (rkf), the ranked drain's level-2 table: one u64 per 16 consecutive
-// keys of the exact 4^W presence bitmap -- bits 0-15 presence, then the rank prefix (rkf_rb
-// bits), then two filter fields of rkf_fw bits for the group's first two present keys: a
-// flag (top bit of the field) and, for a bucket of one record seeded at its primer start and
-// plain over bases W..W+F-1, those F bases (2-bit, base W on top).  The level-2 probe that
-// confirms a seed thus also carries a filter: a seed window whose bases W..W+F-1 differ from
-// them in more than N positions cannot match primer 1 (each counted position is a real
-// mismatch), so the drain skips its bucket head without loading it.
-constexpr uint32_t kRkfKeys = 16;
-__host__ __device__ __forceinline__ uint32_t rkf_field_flag(uint32_t fw) { return 1u << (fw - 1); }
+// Key groups (kgrp), the level-2 table of the scan for W 11..13 under I = 0: one u64 per 16
+// consecutive keys of the exact 4^W presence bitmap -- bits 0-15 presence, then three 16-bit
+// fields for the group's first three present keys.  A field with its top bit set belongs to a
+// key whose bucket is one record seeded at its primer start and plain (the 8-B compact head)
+// and holds that primer's bases W..W+F-1 (2-bit, base W on top, in the low 2F bits).  The
+// probe that confirms a seed thus also filters it: a window whose bases there differ in more
+// than N positions cannot be a survivor (each counted position is a real mismatch under
+// I = 0; a genome exception base reads as 'A' and can only hide one), so the seed ends at
+// the probe.  Other seeds leave as key references for tail_kernel.
+constexpr uint32_t kKgrpKeys = 16;
+constexpr uint32_t kKgrpFields = 3;
+constexpr uint32_t kKgrpFlag = 0x8000u;
 
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {
     return d == 0 ? 0u : (d < 0 ? (uint32_t)(-2 * d - 1) : (uint32_t)(2 * d));

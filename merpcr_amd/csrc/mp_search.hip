@@ -52,6 +52,8 @@ struct ScanArgs {
     const uint32_t* filt;   // W >= 14: hashed presence filter
     uint32_t filt_log2;
     const uint2* rk;        // W <= 13: rank bitmap
+    const uint2* kgrp;      // W 11..13, I = 0: key groups (u64 per 16 keys, see kKgrpKeys)
+    uint32_t kgrp_F;
     const Entry* dents;     // W <= 13: bucket heads by rank
     const uint2* dents8;    // W <= 13: 8-B heads
     const uint4* dents16;   // W <= 13, Table::h16: 16-B heads (primers with IUPAC bases after the seed)
@@ -1078,6 +1080,33 @@ __device__ __forceinline__ uint32_t kmer_dyn(uint32_t d0, uint32_t d1, uint32_t 
     return r ? __builtin_amdgcn_alignbit(hi, lo, 32u - r) : hi;
 }
 
+// The same over the lane's 64 bases (d3: bases 48..63), p in [0, 48).
+__device__ __forceinline__ uint32_t kmer_dyn4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t p) {
+    const uint32_t hi = p < 16 ? d0 : (p < 32 ? d1 : d2), lo = p < 16 ? d1 : (p < 32 ? d2 : d3);
+    const uint32_t r = 2u * (p & 15u);
+    return r ? __builtin_amdgcn_alignbit(hi, lo, 32u - r) : hi;
+}
+
+// Bucket-tail reference of a seed that passed the key groups (kRkf scan): no bucket field;
+// tail_kernel finds the bucket from the seed window's key.
+constexpr uint32_t kKeyRef = 0x80000000u;
+
+// Level-2 probe of the key groups (kRkf, Table::kgrp): presence of the window's key and, for
+// the group's first three present keys with a compact head, primer-1 bases W..W+F-1 (see
+// kKgrpKeys).  `xb`: the window's bases [2, 18) (base 2 on top).  True = the seed goes on.
+__device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t key, uint32_t xb, uint32_t W) {
+    const uint32_t bit = key & 15u;
+    if (!((rw.x >> bit) & 1u)) return false;
+    const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
+    if (j >= kKgrpFields) return true;
+    const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
+    if (!(field & kKgrpFlag)) return true;
+    const uint32_t F2 = 2u * a.kgrp_F;
+    const uint32_t g = (xb << (2u * W - 4u)) >> (32u - F2);
+    const uint32_t x = (g ^ field) & ((1u << F2) - 1u);
+    return __popc((x | (x >> 1)) & 0x55555555u) <= a.N;
+}
+
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
 // ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
 // The next super-step's plane words are loaded before the current one is processed.
@@ -1136,7 +1165,7 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
     }
 };
 
-template <int kMode, bool kInline, int kK = 1, bool kDefer = false, bool kH16 = false>
+template <int kMode, bool kInline, int kK = 1, bool kDefer = false, bool kH16 = false, bool kRkf = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
@@ -1227,8 +1256,14 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         const uint32_t i = (uint32_t)__clz(m);
                         m &= ~(0x80000000u >> i);
                         if (qi - r0 < kSeedQR) {
-                            L.rq.r[qi - r0] = kmer_dyn(d0, d1, d2, i) >> shw;
-                            L.rq.q[qi - r0] = (uint16_t)((uint32_t)lane * kLanePos + i);
+                            if constexpr (kRkf) {  // bases [i + 2, i + 18) and, above the offset, bases i, i + 1
+                                L.rq.r[qi - r0] = kmer_dyn4(d0, d1, d2, (uint32_t)R.w1, i + 2u);
+                                L.rq.q[qi - r0] = (uint16_t)(((uint32_t)lane * kLanePos + i) |
+                                                             ((kmer_dyn(d0, d1, d2, i) >> 28) << 11));
+                            } else {
+                                L.rq.r[qi - r0] = kmer_dyn(d0, d1, d2, i) >> shw;
+                                L.rq.q[qi - r0] = (uint16_t)((uint32_t)lane * kLanePos + i);
+                            }
                         }
                         ++qi;
                     }
@@ -1248,7 +1283,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         const bool v = e < nr;
                         pk[q] = v ? L.rq.r[e] : 0u;
                         po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
-                        rw[q] = a.rk[v ? (pk[q] >> 5) : 0u];
+                        if constexpr (kRkf) {
+                            const uint32_t key = ((po[q] >> 11) << (2u * W - 4u)) | (pk[q] >> (36u - 2u * W));
+                            rw[q] = a.kgrp[v ? (key >> 4) : 0u];
+                        } else {
+                            rw[q] = a.rk[v ? (pk[q] >> 5) : 0u];
+                        }
                     }
                 }
                 if (first) {  // the next super-step's words, issued after this step's probes
@@ -1259,18 +1299,56 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     }
                 }
                 wave_sync();  // every list entry is in registers before the seeds overwrite it
+                if constexpr (kRkf) {
+                    // the few seeds that pass the key groups (c3: 4% of seeds) leave as key
+                    // references for tail_kernel, with their window, exception bits and bases
+                    // left: compacted into the list, then one pass of window shuffles per 64
+                    uint32_t qn = 0;
+#pragma unroll
+                    for (int q = 0; q < kP; ++q) {
+                        if ((uint32_t)q * 64u < nr) {
+                            const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
+                            const uint32_t key = ((po[q] >> 11) << (2u * W - 4u)) | (pk[q] >> (36u - 2u * W));
+                            const bool hit = e < nr && kgrp_pass(a, rw[q], key, pk[q], W);
+                            const uint64_t hm = __ballot(hit);
+                            if (hit) L.rq.q[qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint16_t)(po[q] & 0x7FFu);
+                            qn += (uint32_t)__popcll(hm);
+                        }
+                    }
+                    wave_sync();
+                    for (uint32_t b = 0; b < qn; b += 64) {
+                        const uint32_t e = b + (uint32_t)lane;
+                        const bool on = e < qn;
+                        const uint32_t p = R.base + (on ? (uint32_t)L.rq.q[e] : 0u);
+                        uint64_t G;
+                        uint32_t x;
+                        window_from_regs(a, R, sbase, p, true, G, x);
+                        const uint64_t gp = sbase + p;
+                        append_chunked<2>(&a.counters[4], a.tails, a.tails_cap, on,
+                                          make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), kKeyRef, R.seq), lane, TC,
+                                          make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
+                    }
+                    wave_sync();  // the next round rewrites the list
+                    r0 += kSeedQR;
+                    continue;
+                }
                 uint32_t qn = 0;
 #pragma unroll
                 for (int q = 0; q < kP; ++q) {
                     if ((uint32_t)q * 64u < nr) {
                         const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
-                        const uint32_t bq = pk[q] & 31u;
-                        const bool hit = e < nr && ((rw[q].x >> bq) & 1u);
+                        bool hit;
+                        uint32_t rank;
+                        {
+                            const uint32_t bq = pk[q] & 31u;
+                            hit = e < nr && ((rw[q].x >> bq) & 1u);
+                            rank = rw[q].y + (uint32_t)__popc(rw[q].x & ((1u << bq) - 1u));
+                        }
                         const uint64_t hm = __ballot(hit);
                         if (hit) {
                             const uint32_t at = qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
-                            L.rq.q[at] = (uint16_t)po[q];
-                            L.rq.r[at] = rw[q].y + (uint32_t)__popc(rw[q].x & ((1u << bq) - 1u));
+                            L.rq.q[at] = (uint16_t)(po[q] & 0x7FFu);
+                            L.rq.r[at] = rank;
                         }
                         qn += (uint32_t)__popcll(hm);
                     }
@@ -1598,6 +1676,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
 // returning atomic: one per wave-iteration would serialise on the single list counter
 // (returning atomics on one address: ~88 per microsecond, MI355X_MICROARCH.md).
 constexpr uint32_t kTailBuf = 512;
+static_assert(kKeyRef == 0x80000000u, "key references: bucket field 2^31 (ents indices are below)");
 __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32_t& n_sh,
                                            unsigned long long& base_sh) {
     __syncthreads();
@@ -1633,10 +1712,39 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
             const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
             const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
             const uint32_t rem = w.w;                                    // bases from the seed to the end
-            Entry e = a.ents[v.z];                                       // its count = tail length
+            uint32_t first = v.z;
+            Entry e;
+            if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
+                const uint32_t W = (uint32_t)a.W;
+                const uint32_t h = (uint32_t)(Gs >> (64u - 2u * W));
+                const uint2 rw = a.rk[h >> 5];
+                const uint2 c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
+                if (c.y & kHead8Full) {
+                    first = c.x;  // the bucket's first entry
+                    if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
+                        const uint32_t cnt = ((c.y >> 28) & 3u) + 1u;
+                        const uint32_t F = head8_filt_bases(cnt);
+                        const uint32_t fm = (1u << (2u * F)) - 1u;
+                        const uint32_t gf = (uint32_t)((Gs << (2u * W)) >> (64u - 2u * F));
+                        const uint32_t xf = w.z & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
+                        bool any = xf != 0u;
+                        for (uint32_t j = 0; j < cnt; ++j) {
+                            const uint32_t xj = gf ^ ((c.y >> (2u * F * j)) & fm);
+                            any = any || __popc((xj | (xj >> 1)) & 0x55555555u) <= a.N;
+                        }
+                        if (!any) first = 0xFFFFFFFFu;
+                    }
+                    if (first != 0xFFFFFFFFu) e = a.ents[first];
+                    else e.count = 0;
+                } else {
+                    e = head8_entry(c, h, W);
+                }
+            } else {
+                e = a.ents[first];                                       // its count = tail length
+            }
             const uint32_t cnt = e.count;
             for (uint32_t j = 0; j < cnt; ++j) {
-                if (j) e = a.ents[v.z + j];
+                if (j) e = a.ents[first + j];
                 const uint64_t gk = gp - e.hash_off;
                 if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) continue;  // k + l1 > n / not owned
                 uint64_t G = Gs;
@@ -1964,6 +2072,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
     a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
     a.defer_full = t->defer_full && !s->opt.no_defer;
+    a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F;
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
@@ -1987,6 +2096,10 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     if (s->opt.tails == MP_TAILS_KERNEL) inl = false;
     // W <= kDenseMaxW: dense_kernel (bucket index in LDS, filter-word octs)
     const bool dense = (uint32_t)t->prm.wordsize <= kDenseMaxW && !s->opt.no_dense;
+    // level-2 filter of the filtered rank groups: I = 0 (the 2-bit mismatch count is then a
+    // lower bound), compact 8-B heads (not h16)
+    const bool rkf = t->kgrp_F >= 2 && !t->h16 && a.I == 0 && !s->opt.no_rank_filter && t->filt_direct &&
+                     !t->lds_exact && a.W >= 11 && a.W <= 13;
     const size_t dense_lds = s->dense_lds;
     const uint32_t dense_per_cu = s->dense_per_cu;
     // A list that overflowed is grown and its producers rerun: the scan (and tail_kernel)
@@ -2021,8 +2134,12 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
                 if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
                 else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h16)
                     hipLaunchKernelGGL((scan_kernel<1, false, 2, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct && t->lds_k == 2 && a.defer_full && rkf)
+                    hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
                 else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
                     hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
+                else if (t->filt_direct && a.defer_full && rkf)
+                    hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
                 else if (t->filt_direct && a.defer_full && t->h16)
                     hipLaunchKernelGGL((scan_kernel<1, false, 1, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
                 else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);

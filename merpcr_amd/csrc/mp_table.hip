@@ -32,7 +32,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->rkf); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->kgrp); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
     delete t;
@@ -264,7 +264,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         std::vector<uint16_t> dsum;
         std::vector<uint2> dents8;
         std::vector<uint4> dents16;
-        std::vector<uint64_t> rkf;
+        std::vector<uint64_t> kgrp;
         std::vector<Slot> slots;
         if (t->filt_direct) {
             // rank bitmap over the exact 4^W presence bitmap; heads in key order
@@ -432,37 +432,29 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             // few full heads (multi-record buckets, IUPAC/long/inner-seed primers): the ranked
             // drain tests only compact heads and defers every full-head bucket to tail_kernel
             t->defer_full = n_full * 20 < (uint64_t)nb;
-            // filtered rank groups (kRkfKeys keys per u64) for the deferring drain
-            if (W >= 10) {
-                uint32_t rb = 1;
-                while ((1ull << rb) <= (uint64_t)nb) ++rb;
-                const uint32_t fw = (48u - std::min(rb, 46u)) / 2u;
-                const uint32_t F = std::min<uint32_t>(std::min<uint32_t>((fw - 1u) / 2u, (32u - std::min(rb, 32u)) / 2u), 8u);
-                t->rkf_rb = rb;
-                t->rkf_fw = fw;
-                t->rkf_F = F >= 2 ? F : 0u;
+            // key groups (kKgrpKeys keys per u64) for the scan's level-2 probe: the list entry
+            // of window i carries bases [i, i + 18), so F <= 18 - W, and a field holds <= 7 bases
+            if (W >= 11 && W <= 13) {
+                const uint32_t F = std::min<uint32_t>(7u, 18u - W);
+                t->kgrp_F = F;
                 const uint64_t nkeys = 1ull << (2 * W);
-                rkf.assign(std::max<uint64_t>(nkeys / kRkfKeys, 1), 0ull);
-                uint32_t acc = 0;
-                for (uint64_t g = 0; g < rkf.size(); ++g) {
+                kgrp.assign(nkeys / kKgrpKeys, 0ull);
+                for (uint64_t g = 0; g < kgrp.size(); ++g) {
                     const uint32_t pres = (uint32_t)((filt[g >> 1] >> ((g & 1) * 16)) & 0xFFFFu);
-                    uint64_t w = (uint64_t)pres | ((uint64_t)acc << 16);
+                    uint64_t w = pres;
                     uint32_t j = 0;
-                    for (uint32_t bit = 0; bit < 16 && j < 2 && t->rkf_F; ++bit) {
+                    for (uint32_t bit = 0; bit < 16 && j < kKgrpFields; ++bit) {
                         if (!((pres >> bit) & 1u)) continue;
-                        const uint32_t k = (uint32_t)(g * kRkfKeys + bit);
+                        const uint32_t k = (uint32_t)(g * kKgrpKeys + bit);
                         const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
                         const uint2 h = dents8[rank];
-                        uint32_t field = 0;
                         // compact head (single record, seeded at its primer start, plain, <= W + 16
                         // bases) carrying at least F bases after the seed
-                        if (!(h.y & kHead8Full) && ((h.y >> kHead8RecBits) & 31u) >= t->rkf_F)
-                            field = rkf_field_flag(fw) | (h.x >> (32u - 2u * t->rkf_F));
-                        w |= (uint64_t)field << (16u + rb + j * fw);
+                        if (!(h.y & kHead8Full) && ((h.y >> kHead8RecBits) & 31u) >= F)
+                            w |= (uint64_t)(kKgrpFlag | (h.x >> (32u - 2u * F))) << (16u + 16u * j);
                         ++j;
                     }
-                    rkf[g] = w;
-                    acc += (uint32_t)__builtin_popcount(pres);
+                    kgrp[g] = w;
                 }
             }
             filt.assign(1, 0);
@@ -498,7 +490,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         if ((rc = upload(&t->dents, dents.data(), dents.size(), &bytes))) break;
         if ((rc = upload(&t->dents8, dents8.data(), dents8.size(), &bytes))) break;
         if ((rc = upload(&t->dents16, dents16.data(), dents16.size(), &bytes))) break;
-        if ((rc = upload(&t->rkf, rkf.data(), rkf.size(), &bytes))) break;
+        if ((rc = upload(&t->kgrp, kgrp.data(), kgrp.size(), &bytes))) break;
         if ((rc = upload(&t->binfo, binfo.data(), binfo.size(), &bytes))) break;
         if ((rc = upload(&t->dfilt, dfilt.data(), dfilt.size(), &bytes))) break;
         if ((rc = upload(&t->dgrp, dgrp.data(), dgrp.size(), &bytes))) break;

@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,4,5")
+    ap.add_argument("--variants", default="0", help="0 = product, n = MP_ABLATE=n, NAME=VAL[+...] = defines, opt:name=val[,...] = search options")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--steps", type=int, default=3)
@@ -31,7 +31,7 @@ def main():
     for v in variants:
         # 0 = product; n = MP_ABLATE=n; nt = non-temporal genome
         # stream; NAME=VAL[+NAME=VAL...] = those defines
-        if v == "0":
+        if v == "0" or v.startswith("opt:"):
             defs = ()
         elif v == "nt":
             defs = ("MP_NT_STREAM=1",)
@@ -40,7 +40,7 @@ def main():
         else:
             defs = (f"MP_ABLATE={int(v)}",)
         tag = "".join(ch if ch.isalnum() else "_" for ch in v)
-        path = _build.LIB if v == "0" else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{tag}.so")
+        path = _build.LIB if not defs else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{tag}.so")
         libs[v] = _build.build_native(defines=defs, lib=path)
     if args.build_only:
         return
@@ -70,6 +70,12 @@ def main():
             genome.put_device(r, buf.data_ptr() + int(offs[r]), n)
         genome.seal()
         s = _native.Search(table, genome)
+        if v.startswith("opt:"):  # opt:name=int[,name=int...]: mp_search_set_options on the product library
+            kw = {}
+            for item in v[4:].split(","):
+                k, val = item.split("=")
+                kw[k] = val if k in ("tails", "sort") else int(val)
+            s.set_options(**kw)
         from merpcr_amd.dist import shard_ranges
         rng = shard_ranges(lens, args.shard_of)[0] if args.shard_of > 1 else None
         s.run(rng)
