@@ -1091,19 +1091,26 @@ __device__ __forceinline__ uint32_t kmer_dyn4(uint32_t d0, uint32_t d1, uint32_t
 // tail_kernel finds the bucket from the seed window's key.
 constexpr uint32_t kKeyRef = 0x80000000u;
 
+// 32-bit funnel of bases p..p+15 of a lane's 48 bases (A, B, C = bases 0-15, 16-31,
+// 32-47), p in [0, 48); bases past 47 read as 0.
+__device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, uint32_t p) {
+    const uint32_t hi = p < 16u ? A : (p < 32u ? B : C);
+    const uint32_t lo = p < 16u ? B : (p < 32u ? C : 0u);
+    return (uint32_t)(((((uint64_t)hi << 32) | lo) << (2u * (p & 15u))) >> 32);
+}
+
 // Level-2 probe of the key groups (kRkf, Table::kgrp): presence of the window's key and, for
 // the group's first three present keys with a compact head, primer-1 bases W..W+F-1 (see
-// kKgrpKeys).  `xb`: the window's bases [2, 18) (base 2 on top).  True = the seed goes on.
-__device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t key, uint32_t xb, uint32_t W) {
-    const uint32_t bit = key & 15u;
+// kKgrpKeys).  `pk`: the window's bases W..W+F-1 << 4 | the key's low 4 bits.  True = the
+// seed goes on.
+__device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
+    const uint32_t bit = pk & 15u;
     if (!((rw.x >> bit) & 1u)) return false;
     const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
     if (j >= kKgrpFields) return true;
     const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
     if (!(field & kKgrpFlag)) return true;
-    const uint32_t F2 = 2u * a.kgrp_F;
-    const uint32_t g = (xb << (2u * W - 4u)) >> (32u - F2);
-    const uint32_t x = (g ^ field) & ((1u << F2) - 1u);
+    const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
     return __popc((x | (x >> 1)) & 0x55555555u) <= a.N;
 }
 
@@ -1244,6 +1251,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // pass -- full lanes, all passes' rank-word loads in flight together -- and the
             // seeds are compacted back into the same arrays as {offset, rank}
             const uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
+#if defined(MP_ABLATE) && MP_ABLATE == 1  // timing only: level 1 alone
+            ncand += (uint32_t)__popc(rem);
+            if (nx < n_supers) { locate(nx); words(nx, nw0, nw1, niv); }
+            ss = nx;
+            continue;
+#endif
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
@@ -1256,10 +1269,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         const uint32_t i = (uint32_t)__clz(m);
                         m &= ~(0x80000000u >> i);
                         if (qi - r0 < kSeedQR) {
-                            if constexpr (kRkf) {  // bases [i + 2, i + 18) and, above the offset, bases i, i + 1
-                                L.rq.r[qi - r0] = kmer_dyn4(d0, d1, d2, (uint32_t)R.w1, i + 2u);
-                                L.rq.q[qi - r0] = (uint16_t)(((uint32_t)lane * kLanePos + i) |
-                                                             ((kmer_dyn(d0, d1, d2, i) >> 28) << 11));
+                            if constexpr (kRkf) {  // the offset only: the probe shuffles the window from its lane
+                                L.rq.q[qi - r0] = (uint16_t)((uint32_t)lane * kLanePos + i);
                             } else {
                                 L.rq.r[qi - r0] = kmer_dyn(d0, d1, d2, i) >> shw;
                                 L.rq.q[qi - r0] = (uint16_t)((uint32_t)lane * kLanePos + i);
@@ -1270,6 +1281,13 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                 }
                 wave_sync();
                 const uint32_t nr = min(tot - r0, kSeedQR);
+#if defined(MP_ABLATE) && MP_ABLATE == 2  // timing only: level 1 and the list
+                if (first) { first = false; if (nx < n_supers) { locate(nx); words(nx, nw0, nw1, niv); } }
+                ncand += (uint32_t)L.rq.r[lane] & 1u;
+                wave_sync();
+                r0 += kSeedQR;
+                continue;
+#endif
                 constexpr int kP = (kSeedQR + 63) / 64;
                 uint32_t pk[kP], po[kP];
                 uint2 rw[kP];
@@ -1281,12 +1299,21 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     rw[q] = make_uint2(0u, 0u);
                     if ((uint32_t)q * 64u < nr) {
                         const bool v = e < nr;
-                        pk[q] = v ? L.rq.r[e] : 0u;
-                        po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
                         if constexpr (kRkf) {
-                            const uint32_t key = ((po[q] >> 11) << (2u * W - 4u)) | (pk[q] >> (36u - 2u * W));
+                            // bases [i, i + W + F) of window i of lane src: three shuffles of the
+                            // lane's 48 bases; pk = the F filter bases << 4 | the key's low 4 bits
+                            po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
+                            const int sa = (int)((po[q] >> 5) << 2);
+                            const uint32_t A = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d0);
+                            const uint32_t B = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d1);
+                            const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d2);
+                            const uint32_t i = po[q] & 31u;
+                            const uint32_t key = funnel3(A, B, C, i) >> shw;
+                            pk[q] = ((funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F)) << 4) | (key & 15u);
                             rw[q] = a.kgrp[v ? (key >> 4) : 0u];
                         } else {
+                            pk[q] = v ? L.rq.r[e] : 0u;
+                            po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
                             rw[q] = a.rk[v ? (pk[q] >> 5) : 0u];
                         }
                     }
@@ -1299,6 +1326,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     }
                 }
                 wave_sync();  // every list entry is in registers before the seeds overwrite it
+#if defined(MP_ABLATE) && MP_ABLATE == 3  // timing only: level 1, the list and the level-2 loads
+                for (int q = 0; q < kP; ++q) ncand += rw[q].x & 1u;
+                r0 += kSeedQR;
+                continue;
+#endif
                 if constexpr (kRkf) {
                     // the few seeds that pass the key groups (c3: 4% of seeds) leave as key
                     // references for tail_kernel, with their window, exception bits and bases
@@ -1308,10 +1340,9 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     for (int q = 0; q < kP; ++q) {
                         if ((uint32_t)q * 64u < nr) {
                             const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
-                            const uint32_t key = ((po[q] >> 11) << (2u * W - 4u)) | (pk[q] >> (36u - 2u * W));
-                            const bool hit = e < nr && kgrp_pass(a, rw[q], key, pk[q], W);
+                            const bool hit = e < nr && kgrp_pass(a, rw[q], pk[q]);
                             const uint64_t hm = __ballot(hit);
-                            if (hit) L.rq.q[qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint16_t)(po[q] & 0x7FFu);
+                            if (hit) L.rq.q[qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint16_t)po[q];
                             qn += (uint32_t)__popcll(hm);
                         }
                     }

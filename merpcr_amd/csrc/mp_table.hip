@@ -432,10 +432,11 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             // few full heads (multi-record buckets, IUPAC/long/inner-seed primers): the ranked
             // drain tests only compact heads and defers every full-head bucket to tail_kernel
             t->defer_full = n_full * 20 < (uint64_t)nb;
-            // key groups (kKgrpKeys keys per u64) for the scan's level-2 probe: the list entry
-            // of window i carries bases [i, i + 18), so F <= 18 - W, and a field holds <= 7 bases
+            // key groups (kKgrpKeys keys per u64) for the scan's level-2 probe: it shuffles
+            // bases [i, i + 17) of window i from the owning lane (i < 32 of its 48), so
+            // F <= 17 - W, and a field holds <= 7 bases
             if (W >= 11 && W <= 13) {
-                const uint32_t F = std::min<uint32_t>(7u, 18u - W);
+                const uint32_t F = std::min<uint32_t>(7u, 17u - W);
                 t->kgrp_F = F;
                 const uint64_t nkeys = 1ull << (2 * W);
                 kgrp.assign(nkeys / kKgrpKeys, 0ull);
