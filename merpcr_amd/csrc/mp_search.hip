@@ -31,7 +31,7 @@
 // survivors per pair-check batch (lanes of the prologue); smaller batches spread the
 // per-survivor loop over more waves
 #ifndef MP_PBATCH
-#define MP_PBATCH 32
+#define MP_PBATCH 64
 #endif
 
 
@@ -104,7 +104,7 @@ constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;  // pair_kernel
 constexpr int kSchedBase = kPairQBase + 8 * kStatStride;  // scan super-step chunk counters, 8 x 256 B
 constexpr size_t kCounterBytes = (size_t)(kSchedBase + 8 * kStatStride) * 8;
 #ifndef MP_PDYN_BATCH
-#define MP_PDYN_BATCH 16
+#define MP_PDYN_BATCH 64
 #endif
 
 __device__ __forceinline__ void add_stats(const ScanArgs& a, uint32_t cand, uint32_t surv, int lane) {
@@ -375,9 +375,9 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
     // in parallel with the primer-1 compare, into the wave's LDS stage ([slot][lane], so
     // the writes are conflict-free), and phase 2 reads them from LDS instead of issuing
     // one dependent global round trip per survivor.
-    bool fast = false;
+    bool fast = false, clean = false;
+    const uint64_t P0l = gk + e - r.l2 - (uint32_t)lo;
     {
-        const uint64_t P0l = gk + e - r.l2 - (uint32_t)lo;
         const uint64_t lastl = P0l + (uint64_t)(lo + hi) + r.l2 - 1;
         const uint64_t w0 = P0l >> 5, e0 = P0l >> 6;
         const uint64_t wl = (lastl >> 5) + 1, el = (lastl >> 6) + 1;  // last words any try reads
@@ -385,8 +385,23 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         if (fast) {
 #pragma unroll
             for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[w0 + t] : 0ull;
+            // exception bits of the stretch [P0l, lastl] (at most 4 words of 64 bases)
+            uint64_t ew[kPE];
 #pragma unroll
-            for (int t = 0; t < kPE; ++t) pst[(kPW + t) * MP_PBATCH + lane] = e0 + t <= el ? a.gexc[e0 + t] : 0ull;
+            for (int t = 0; t < kPE; ++t) {
+                ew[t] = e0 + t <= el ? a.gexc[e0 + t] : 0ull;
+                pst[(kPW + t) * MP_PBATCH + lane] = ew[t];
+            }
+            const uint32_t f0 = (uint32_t)(P0l & 63), f1 = (uint32_t)(lastl - (e0 << 6));  // stretch bits in word order
+            uint64_t any = 0;
+#pragma unroll
+            for (int t = 0; t < kPE; ++t) {
+                const uint32_t b0 = 64u * (uint32_t)t, b1 = b0 + 63u;  // bases of word t, relative to e0 << 6
+                const uint32_t s0 = f0 > b0 ? f0 - b0 : 0u, s1 = f1 < b1 ? f1 - b0 : 63u;
+                if (f0 <= b1 && f1 >= b0)
+                    any |= ew[t] & ((~0ull >> s0) & ~(s1 >= 63u ? 0ull : (~0ull >> (s1 + 1u))));
+            }
+            clean = any == 0;
             const uint64_t* pp = a.planes + (uint64_t)r.p2_pl * 4;
 #pragma unroll
             for (int t = 0; t < 4; ++t) pst[(kPW + kPE + t) * MP_PBATCH + lane] = pp[t];
@@ -394,7 +409,53 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
     }
     wave_sync_lds();
     if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);
-    uint64_t todo = __ballot(keep);
+    // Lane-parallel tries: a survivor whose stretch holds no exception base takes its tries
+    // in its own lane -- a 32-base window slid one base per try through the staged words,
+    // primer 2 compared by XOR/popcount (plain) or the accept planes -- one wave-wide pass
+    // per try offset instead of one per survivor.
+    const bool lp = keep && fast && clean;
+    if (__any(lp)) {
+        const uint64_t* sj = pst + lane;
+        const uint64_t Q0 = sj[(kPW + kPE) * MP_PBATCH], Q1 = sj[(kPW + kPE + 1) * MP_PBATCH];
+        const uint64_t Q2 = sj[(kPW + kPE + 2) * MP_PBATCH], Q3 = sj[(kPW + kPE + 3) * MP_PBATCH];
+        const uint64_t in2 = sp_lt((int)r.l2);
+        const uint64_t two = (Q0 & Q1) | (Q0 & Q2) | (Q0 & Q3) | (Q1 & Q2) | (Q1 & Q3) | (Q2 & Q3);
+        const bool plain2 = two == 0 && ((Q0 | Q1 | Q2 | Q3) & in2) == in2;
+        const uint64_t code2 = ((Q1 | Q3) & kEven) | (((Q2 | Q3) & kEven) << 1);
+        const uint64_t prot2 = sp_lt(min(a.X, (int)r.l2));  // '-' strand: positions < X
+        // try t (d = t - lo) is in bounds for t in [ta, lo + hi] (engine.py:548-560: a
+        // non-positive offset needs the product to end past primer 1, and the window inside
+        // the sequence, which hi already guarantees)
+        const int64_t ta = smin64((int64_t)lo + 1, smax64(0, (int64_t)r.l1 + r.l2 + lo - (int64_t)e));
+        const int32_t tb = lp ? lo + hi : -1;
+        const uint32_t a5 = (uint32_t)(P0l & 31);
+        auto fun = [&](uint64_t x0, uint64_t x1) { return a5 ? (x0 << (2 * a5)) | (x1 >> (64 - 2 * a5)) : x0; };
+        uint64_t G = fun(sj[0], sj[MP_PBATCH]);
+        uint64_t F = fun(sj[MP_PBATCH], sj[2 * MP_PBATCH]);
+        int nw = 2;
+        const bool all_plain = __all(!lp || plain2);
+        for (int32_t t = 0; __any(t <= tb); ++t) {
+            uint64_t mm;
+            if (all_plain) {
+                const uint64_t x = G ^ code2;
+                mm = (x | (x >> 1)) & in2;
+            } else {
+                const uint64_t glo = G & kEven, ghi = (G >> 1) & kEven;
+                const uint64_t nlo = glo ^ kEven, nhi = ghi ^ kEven;
+                mm = ~((nhi & nlo & Q0) | (nhi & glo & Q1) | (ghi & nlo & Q2) | (ghi & glo & Q3)) & in2;
+            }
+            const bool hit = t >= ta && t <= tb && !(mm & prot2) && __popcll(mm) <= a.N;
+            stage_try_hit(a, S, lane, hit, gk, rk, t - lo);
+            G = (G << 2) | (F >> 62);
+            F <<= 2;
+            if ((t & 31) == 31) {  // the next 32 bases
+                const int w = min(nw, kPW - 2);
+                F = fun(sj[w * MP_PBATCH], sj[(w + 1) * MP_PBATCH]);
+                ++nw;
+            }
+        }
+    }
+    uint64_t todo = __ballot(keep && !lp);
     while (todo) {
         const int j = (int)__builtin_ctzll(todo);
         todo &= todo - 1;
@@ -1310,7 +1371,16 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                             const uint32_t i = po[q] & 31u;
                             const uint32_t key = funnel3(A, B, C, i) >> shw;
                             pk[q] = ((funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F)) << 4) | (key & 15u);
+#if defined(MP_ABLATE) && MP_ABLATE == 4  // timing only: level-2 loads coalesced
+                            rw[q] = a.kgrp[(uint32_t)lane + (key & 1u)];
+#elif defined(MP_ABLATE) && MP_ABLATE == 5  // timing only: non-temporal level-2 loads
+                            {
+                                const uint64_t t = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(a.kgrp) + (v ? (key >> 4) : 0u));
+                                rw[q] = make_uint2((uint32_t)t, (uint32_t)(t >> 32));
+                            }
+#else
                             rw[q] = a.kgrp[v ? (key >> 4) : 0u];
+#endif
                         } else {
                             pk[q] = v ? L.rq.r[e] : 0u;
                             po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
@@ -1326,7 +1396,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     }
                 }
                 wave_sync();  // every list entry is in registers before the seeds overwrite it
-#if defined(MP_ABLATE) && MP_ABLATE == 3  // timing only: level 1, the list and the level-2 loads
+#if defined(MP_ABLATE) && (MP_ABLATE == 3 || MP_ABLATE == 4)  // timing only: level 1, the list and the level-2 loads
                 for (int q = 0; q < kP; ++q) ncand += rw[q].x & 1u;
                 r0 += kSeedQR;
                 continue;
@@ -2182,7 +2252,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             MP_HIP_CHECK(hipGetLastError());
             MP_HIP_CHECK(hipEventRecord(s->evt, st));
             if (!dense && !inl && (t->max_bucket > 1 || a.defer_full)) {  // defer_full: single-record full heads too
-                hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 4), dim3(256), 0, st, a);
+                hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 8), dim3(256), 0, st, a);
                 MP_HIP_CHECK(hipGetLastError());
             }
         } else {  // hit list regrown: counters of the pair check and the sort only
