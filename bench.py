@@ -57,7 +57,8 @@ def host_cores() -> int:
 
 def pmc_profile(workload: str):
     """Newest committed PMC summary of this workload (profiles/<tag>_pmc.json next to the
-    bench line it was collected with), or (None, None)."""
+    bench line it was collected with; the highest round tag wins -- file times are those of
+    the checkout), or (None, None)."""
     import glob
     best = None
     for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")):
@@ -69,8 +70,8 @@ def pmc_profile(workload: str):
             d = json.load(open(f))
         except (OSError, ValueError, KeyError):
             continue
-        if "hbm_traffic_bytes_per_launch" in d and (best is None or os.path.getmtime(f) > best[0]):
-            best = (os.path.getmtime(f), d, tag)
+        if "hbm_traffic_bytes_per_launch" in d and (best is None or tag > best[0]):
+            best = (tag, d, tag)
     return (best[1], best[2]) if best else (None, None)
 
 
