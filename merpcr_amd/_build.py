@@ -16,6 +16,11 @@ SOURCES = ["mp_table.hip", "mp_genome.hip", "mp_search.hip", "mp_sort.hip", "mp_
            "mp_format.hip", "mp_sts.hip"]
 HEADERS = ["mp_internal.h", "mp_text.h", os.path.join("..", "..", "include", "merpcr_hip.h")]
 ARCH = os.environ.get("MERPCR_OFFLOAD_ARCH", "gfx950")
+# Per-source flags.  mp_search.hip aggregates its atomics by hand (lane 0 of a wave); the
+# compiler's atomic optimizer would add a readfirstlane of the returned value, i.e. a wait
+# for every older load right at the atomic -- in the pipelined scan that is the super-step
+# claim, which must not wait for the level-2 probes in flight.
+SOURCE_FLAGS = {"mp_search.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
 
 
 def hipcc() -> str:
@@ -50,7 +55,7 @@ def build_native(force: bool = False, verbose: bool = False, defines=(), lib: st
         op = os.path.join(LIBDIR, src.replace(".hip", tag + ".o"))
         objs.append(op)
         if force or _stale(op, [sp] + hdrs):
-            jobs.append([cc] + _flags() + ["-D" + d for d in defines] + ["-c", sp, "-o", op])
+            jobs.append([cc] + _flags() + SOURCE_FLAGS.get(src, []) + ["-D" + d for d in defines] + ["-c", sp, "-o", op])
     if jobs:
         with concurrent.futures.ThreadPoolExecutor(max_workers=min(4, len(jobs))) as ex:
             for cmd, res in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):

@@ -200,6 +200,9 @@ struct Search {
     uint32_t dense_per_cu = 0;   // resident dense_kernel blocks per CU
     size_t dense_lds = 0;        // dense_kernel dynamic LDS bytes
     uint64_t n_regrowths = 0;    // list regrowths over the handle's life (tests)
+    std::vector<SeqSpan> last_spans;        // spans on the device (a rerun of the same range uploads nothing)
+    unsigned long long* h_cnt = nullptr;    // pinned host copy of counters[0..8) (the run's one readback)
+    hipEvent_t evd = nullptr;               // the readback's completion (polled, not slept on)
 };
 
 // ---------------------------------------------------------------- device helpers

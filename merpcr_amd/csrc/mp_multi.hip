@@ -306,7 +306,8 @@ struct Comm {
     ncclComm_t c = nullptr;
     int rank = 0, nranks = 1, device = 0;
     uint64_t* d_meta = nullptr;  // nranks x {count, seq shift, capacity}
-    std::vector<uint64_t> meta;
+    uint64_t* h_meta = nullptr;  // pinned: this rank's 3 words, then the gathered nranks x 3
+    hipEvent_t ev = nullptr;     // the gathered counts' arrival (polled)
 };
 }  // namespace mp
 
@@ -335,12 +336,15 @@ MP_EXPORT int mp_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, in
         delete c;
         return fail(MP_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     }
-    if (hipMalloc(&c->d_meta, (size_t)nranks * 3 * sizeof(uint64_t)) != hipSuccess) {
+    if (hipMalloc(&c->d_meta, (size_t)nranks * 3 * sizeof(uint64_t)) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_meta, (size_t)(nranks + 1) * 3 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev, hipEventDisableTiming) != hipSuccess) {
+        hipFree(c->d_meta);
+        if (c->h_meta) hipHostFree(c->h_meta);
         ncclCommDestroy(c->c);
         delete c;
         return fail(MP_E_NOMEM, "mp_comm_create: allocation failed");
     }
-    c->meta.assign((size_t)nranks * 3, 0);
     *out = c;
     return MP_OK;
 }
@@ -357,31 +361,41 @@ MP_EXPORT int mp_comm_gather_hits(void* comm, void* search, uint32_t seq_shift, 
     if (!c || !s || !n_total || (c->rank == 0 && cap && !dev_out)) return fail(MP_E_ARG, "mp_comm_gather_hits: null pointer");
     hipStream_t st = (hipStream_t)stream;
     MP_HIP_CHECK(hipSetDevice(c->device));
-    const uint64_t mine[3] = {s->n_hits, seq_shift, cap};
-    MP_HIP_CHECK(hipMemcpyAsync(c->d_meta + (size_t)c->rank * 3, mine, sizeof(mine), hipMemcpyHostToDevice, st));
+    // pinned staging and a polled event: the counts exchange is on every step's critical path
+    uint64_t* mine = c->h_meta;
+    const uint64_t* meta = c->h_meta + 3;
+    mine[0] = s->n_hits;
+    mine[1] = seq_shift;
+    mine[2] = cap;
+    MP_HIP_CHECK(hipMemcpyAsync(c->d_meta + (size_t)c->rank * 3, mine, 3 * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     MP_NCCL_CHECK(ncclAllGather(c->d_meta + (size_t)c->rank * 3, c->d_meta, 3, ncclUint64, c->c, st));
-    MP_HIP_CHECK(hipMemcpyAsync(c->meta.data(), c->d_meta, c->meta.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    MP_HIP_CHECK(hipStreamSynchronize(st));
+    MP_HIP_CHECK(hipMemcpyAsync(c->h_meta + 3, c->d_meta, (size_t)c->nranks * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    MP_HIP_CHECK(hipEventRecord(c->ev, st));
+    for (;;) {
+        const hipError_t e = hipEventQuery(c->ev);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) MP_HIP_CHECK(e);
+    }
     uint64_t total = 0;
-    for (int r = 0; r < c->nranks; ++r) total += c->meta[(size_t)r * 3];
+    for (int r = 0; r < c->nranks; ++r) total += meta[(size_t)r * 3];
     *n_total = total;
-    if (total > c->meta[2]) return fail(MP_E_CAP, "mp_comm_gather_hits: rank 0 buffer too small");
+    if (total > meta[2]) return fail(MP_E_CAP, "mp_comm_gather_hits: rank 0 buffer too small");
     MP_NCCL_CHECK(ncclGroupStart());
     uint64_t off = 0;
     for (int r = 0; r < c->nranks; ++r) {
-        const size_t bytes = c->meta[(size_t)r * 3] * sizeof(mp_hit);
+        const size_t bytes = meta[(size_t)r * 3] * sizeof(mp_hit);
         if (bytes) {
             if (c->rank == 0) MP_NCCL_CHECK(ncclRecv(dev_out + off, bytes, ncclUint8, r, c->c, st));
             if (c->rank == r) MP_NCCL_CHECK(ncclSend(s->out, bytes, ncclUint8, 0, c->c, st));
         }
-        off += c->meta[(size_t)r * 3];
+        off += meta[(size_t)r * 3];
     }
     MP_NCCL_CHECK(ncclGroupEnd());
     if (c->rank == 0) {
         off = 0;
         for (int r = 0; r < c->nranks; ++r) {
-            const uint64_t n = c->meta[(size_t)r * 3];
-            const uint32_t sh = (uint32_t)c->meta[(size_t)r * 3 + 1];
+            const uint64_t n = meta[(size_t)r * 3];
+            const uint32_t sh = (uint32_t)meta[(size_t)r * 3 + 1];
             if (n && sh) {
                 hipLaunchKernelGGL(shift_seq_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, dev_out + off, n, sh);
                 MP_HIP_CHECK(hipGetLastError());
@@ -397,6 +411,8 @@ MP_EXPORT void mp_comm_destroy(void* comm) {
     if (!c) return;
     hipSetDevice(c->device);
     hipFree(c->d_meta);
+    if (c->h_meta) hipHostFree(c->h_meta);
+    if (c->ev) hipEventDestroy(c->ev);
     if (c->c) ncclCommDestroy(c->c);
     delete c;
 }

@@ -31,8 +31,12 @@ def main():
     for v in variants:
         # 0 = product; n = MP_ABLATE=n; nt = non-temporal genome
         # stream; NAME=VAL[+NAME=VAL...] = those defines
+        flags = None
         if v == "0" or v.startswith("opt:"):
             defs = ()
+        elif v == "atomopt":  # the compiler's atomic optimizer back on for mp_search.hip
+            defs = ("MP_ATOMOPT=1",)
+            flags = {}
         elif v == "nt":
             defs = ("MP_NT_STREAM=1",)
         elif "=" in v:
@@ -41,7 +45,11 @@ def main():
             defs = (f"MP_ABLATE={int(v)}",)
         tag = "".join(ch if ch.isalnum() else "_" for ch in v)
         path = _build.LIB if not defs else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{tag}.so")
+        saved = _build.SOURCE_FLAGS
+        if flags is not None:
+            _build.SOURCE_FLAGS = flags
         libs[v] = _build.build_native(defines=defs, lib=path)
+        _build.SOURCE_FLAGS = saved
     if args.build_only:
         return
     import ctypes
