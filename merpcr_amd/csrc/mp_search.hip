@@ -107,6 +107,9 @@ constexpr size_t kCounterBytes = (size_t)(kSchedBase + 8 * kStatStride) * 8;
 #ifndef MP_PDYN_BATCH
 #define MP_PDYN_BATCH 64
 #endif
+#ifndef MP_PAIR_MINB
+#define MP_PAIR_MINB 4
+#endif
 
 __device__ __forceinline__ void add_stats(const ScanArgs& a, uint32_t cand, uint32_t surv, int lane) {
 #pragma unroll
@@ -1889,10 +1892,12 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
 // already exact, then the amplicon pair-check with lanes over the offsets.
 // Persistent: each wave strides over the survivor list (empty slots skipped) and stages
 // its hits in LDS.
-#ifndef MP_PAIR_OCC
-#define MP_PAIR_OCC 6  // measured: 6 blocks/CU beat 1 and 8 (c3 pair 0.41 -> 0.37 ms, c4 1.30 -> 1.19 ms)
-#endif
-__global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
+// One 1024-thread block per CU: the LDS stages (9.2 KB per wave) allow 16 waves per CU in
+// any block shape, and the block's hits leave with one returning atomic on the hit counter
+// (256 per launch instead of 1,024 with 4-wave blocks; c4 pair 0.743 -> 0.714 ms).
+constexpr int kPairWaves = 16;
+constexpr int kPairBlock = kPairWaves * 64;
+__global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
     if (blockIdx.x == 0 && threadIdx.x < 64) {  // statistics of the scan / tail kernels (add_stats)
         unsigned long long c = a.counters[kStatBase + threadIdx.x * kStatStride];
@@ -1908,15 +1913,15 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
             a.counters[3] = v;
         }
     }
-    __shared__ HitStage s_st[4];
-    __shared__ uint64_t s_pst[4][kPSlots * MP_PBATCH];
+    __shared__ HitStage s_st[kPairWaves];
+    __shared__ uint64_t s_pst[kPairWaves][kPSlots * MP_PBATCH];
     const int lane = threadIdx.x & 63;
     HitStage& S = s_st[threadIdx.x >> 6];
     if (lane == 0) S.n = 0;
     wave_sync_lds();
     // survivors per wave batch: up to MP_PBATCH, fewer when the list is short, so that
     // every resident wave gets work (a batch is checked one survivor at a time)
-    const uint64_t waves = (uint64_t)gridDim.x * 4;
+    const uint64_t waves = (uint64_t)gridDim.x * kPairWaves;
     // equal rounds for every wave: the fewest rounds of at most MP_PBATCH, then the batch
     // that spreads n_surv evenly over them (32 per batch would leave 1/3 of the waves
     // one round short on c3 while the kernel waits for the rest)
@@ -1928,13 +1933,15 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
     // (blocks x, x+8, ...) owns 1/8 of the batches: its waves take one batch each, then
     // pull the rest from the XCD's own counter (8 counters 256 B apart, ~1.3k atomics each).
     {
-        const uint32_t db = (uint32_t)umax64(4, umin64(MP_PDYN_BATCH, (n_surv + waves - 1) / waves));
+        // at least MP_PAIR_MINB survivors per batch (c2, 30k survivors: minimum 4, 16, 32, 64
+        // -> 0.049, 0.047, 0.050, 0.057 ms)
+        const uint32_t db = (uint32_t)umax64(MP_PAIR_MINB, umin64(MP_PDYN_BATCH, (n_surv + waves - 1) / waves));
         const uint64_t nbat = (n_surv + db - 1) / db;
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
         const uint64_t lo_b = nbat * x / g, hi_b = nbat * (x + 1) / g;
-        const uint64_t nw_x = (uint64_t)((gridDim.x - x + g - 1u) / g) * 4u;  // waves of this group
-        uint64_t bi = lo_b + (uint64_t)(blockIdx.x / g) * 4u + (threadIdx.x >> 6);
+        const uint64_t nw_x = (uint64_t)((gridDim.x - x + g - 1u) / g) * kPairWaves;  // waves of this group
+        uint64_t bi = lo_b + (uint64_t)(blockIdx.x / g) * kPairWaves + (threadIdx.x >> 6);
         const uint64_t nw_d = nw_x;
         while (bi < hi_b) {
             pair_check_batch(a, bi * db, n_surv, db, lane, S, s_pst[threadIdx.x >> 6]);
@@ -1944,12 +1951,13 @@ __global__ __launch_bounds__(256, MP_PAIR_OCC) void pair_kernel(ScanArgs a) {
         }
     }
     (void)stride;
-    // the block's four stages leave with one returning atomic: one per wave at the end of
-    // the kernel would serialise ~5k atomics on the hit counter (~88 per microsecond)
+    // the block's stages leave with one returning atomic: one per wave at the end of the
+    // kernel would serialise ~4k atomics on the hit counter (~88 per microsecond)
     __syncthreads();
     __shared__ unsigned long long s_base;
     if (threadIdx.x == 0) {
-        const uint32_t tot = s_st[0].n + s_st[1].n + s_st[2].n + s_st[3].n;
+        uint32_t tot = 0;
+        for (int q = 0; q < kPairWaves; ++q) tot += s_st[q].n;
         s_base = tot ? atomicAdd(&a.counters[0], (unsigned long long)tot) : 0ull;
     }
     __syncthreads();
@@ -2086,8 +2094,8 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
             s->n_cu <= 0)
             s->n_cu = 256;
         int occ = 0;  // persistent pair check: every resident block slot once
-        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel, 256, 0) == hipSuccess && occ > 0)
-                             ? (uint32_t)occ : 5u;
+        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel, kPairBlock, 0) == hipSuccess && occ > 0)
+                             ? (uint32_t)occ : 1u;
         s->dense_lds = (sizeof(uint2) + sizeof(uint32_t)) *
                        std::max<size_t>(1, ((size_t)1 << (2 * std::min<int>(t->prm.wordsize, kDenseMaxW))) / 32);
         if (t->dsum_mode) s->dense_lds += sizeof(uint16_t) * ((size_t)1 << (2 * t->prm.wordsize));
@@ -2294,7 +2302,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         MP_HIP_CHECK(hipEventRecord(s->ev1, st));
         const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
                                                                : s->pair_per_cu;
-        hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
         MP_HIP_CHECK(hipEventRecord(s->ev2, st));
         if (dev_sort) {  // hit order on the device count: no host round trip before the sort
