@@ -1191,29 +1191,39 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
 #ifndef MP_SCHUNK
 #define MP_SCHUNK 8
 #endif
-constexpr uint64_t kSChunk = MP_SCHUNK;
+constexpr uint32_t kSChunk = MP_SCHUNK;
+// Short scans (under kSChunkShort super-steps per wave, e.g. one rank's eighth of c3) take
+// chunks of 4: the last chunks then even out sooner (1/8 of c3: scan 0.354 ms static, 0.335
+// in chunks of 8, 0.323 in chunks of 4; full c3 is best with 8).  Only scans under
+// MP_SCHED_MIN super-steps per wave keep the static order.
+constexpr uint32_t kSChunkShort = 128;
+#ifndef MP_SCHED_MIN
+#define MP_SCHED_MIN 4u
+#endif
 struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives beside the scan's registers
     uint32_t lo, hi, nw, end;  // XCD group range, waves of the group, end of the current chunk
     uint32_t pending;          // lane 0: counter value claimed for the next chunk
     uint32_t stride;           // 0: dynamic; else the static round-robin stride
+    uint32_t chunk;            // super-steps per claim
     unsigned int* ctr;
     __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint64_t n_supers, int w, int kW, int lane) {
         // short scans (under 64 super-steps per wave, e.g. c2) keep the static order: their
         // per-wave totals average out and the claims would only add latency
         const uint32_t waves = gridDim.x * (uint32_t)kW;
-        if (n_supers < (uint64_t)waves * 64u) {
+        if (n_supers < (uint64_t)waves * MP_SCHED_MIN) {
             stride = waves;
             return (uint64_t)blockIdx.x * (uint64_t)kW + (uint64_t)w;
         }
         stride = 0;
+        chunk = n_supers < (uint64_t)waves * kSChunkShort ? 4u : kSChunk;
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
         ctr = reinterpret_cast<unsigned int*>(counters + kSchedBase + x * kStatStride);
         lo = (uint32_t)(n_supers * x / g);
         hi = (uint32_t)(n_supers * (x + 1) / g);
         nw = ((gridDim.x - x + g - 1u) / g) * (uint32_t)kW;
-        const uint32_t st = lo + ((blockIdx.x / g) * (uint32_t)kW + (uint32_t)w) * (uint32_t)kSChunk;
-        end = min(st + (uint32_t)kSChunk, hi);
+        const uint32_t st = lo + ((blockIdx.x / g) * (uint32_t)kW + (uint32_t)w) * chunk;
+        end = min(st + chunk, hi);
         claim(lane);
         return st < hi ? st : n_supers;
     }
@@ -1226,12 +1236,12 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         if (ss + 1 < end) return ss + 1;
         // lane 0 holds the claimed counter value: broadcast from lane 0 explicitly (called
         // wave-uniformly, but readfirstlane would read another lane under divergence)
-        const uint32_t st = lo + (nw + (uint32_t)__shfl((int)pending, 0, 64)) * (uint32_t)kSChunk;
+        const uint32_t st = lo + (nw + (uint32_t)__shfl((int)pending, 0, 64)) * chunk;
         if (st >= hi) {
             end = 0;
             return n_supers;
         }
-        end = min(st + (uint32_t)kSChunk, hi);
+        end = min(st + chunk, hi);
         claim(lane);
         return st;
     }
@@ -1786,7 +1796,11 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
 // Survivors of a tail_kernel block collect in LDS and leave in batches with one
 // returning atomic: one per wave-iteration would serialise on the single list counter
 // (returning atomics on one address: ~88 per microsecond, MI355X_MICROARCH.md).
-constexpr uint32_t kTailBuf = 512;
+// 1024-thread blocks, two per CU: each block's survivors leave with one returning atomic on
+// the survivor counter per flush, and those serialise at one address (~11 ns each), so
+// 512 blocks where 2,048 smaller ones spent ~20 us on them at the kernel's end.
+constexpr uint32_t kTailBlock = 1024;
+constexpr uint32_t kTailBuf = 2048;
 static_assert(kKeyRef == 0x80000000u, "key references: bucket field 2^31 (ents indices are below)");
 __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32_t& n_sh,
                                            unsigned long long& base_sh) {
@@ -1801,7 +1815,7 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
+__global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     __shared__ uint4 s_buf[kTailBuf];
     __shared__ uint32_t s_n;
     __shared__ unsigned long long s_base;
@@ -1811,8 +1825,8 @@ __global__ __launch_bounds__(256) void tail_kernel(ScanArgs a) {
     const uint64_t n_refs = umin64(a.counters[4], a.tails_cap);
     const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
     uint32_t ncand = 0, nsurv = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t b = (uint64_t)blockIdx.x * 256; b < n_refs; b += stride) {  // block-uniform
+    const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
+    for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride) {  // block-uniform
         const uint64_t i = b + threadIdx.x;
         uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
         if (i < n_refs) {
@@ -2289,7 +2303,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             MP_HIP_CHECK(hipGetLastError());
             MP_HIP_CHECK(hipEventRecord(s->evt, st));
             if (!dense && !inl && (t->max_bucket > 1 || a.defer_full)) {  // defer_full: single-record full heads too
-                hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 8), dim3(256), 0, st, a);
+                hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, a);
                 MP_HIP_CHECK(hipGetLastError());
             }
         } else {  // hit list regrown: counters of the pair check and the sort only
