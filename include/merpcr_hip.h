@@ -205,14 +205,22 @@ void mp_comm_destroy(void* comm);
  * before the first header dropped.  The caller handles the reference's empty-file
  * case (fasta.py:31-33) before calling.  Records stay owned by the handle. */
 int mp_fasta_load(const char* path, void** fasta_out);
-/* Same, reading the file in chunks of `chunk_bytes` (0 = 64 MiB): tests use small chunks
- * to put read seams inside lines, UTF-8 sequences and CR/LF pairs. */
+/* Same rules over the memory-mapped file on `threads` host threads (0 = every CPU the
+ * process may use; mp_fasta_load's choice): UTF-8 validation, header lines and the
+ * filter each split over the threads.  An unmappable file falls back to the streaming
+ * reader below. */
+int mp_fasta_load_parallel(const char* path, int32_t threads, void** fasta_out);
+/* The streaming reader, one thread, reading the file in chunks of `chunk_bytes` (0 = 64
+ * MiB): tests use small chunks to put read seams inside lines, UTF-8 sequences and CR/LF
+ * pairs. */
 int mp_fasta_load_chunked(const char* path, uint64_t chunk_bytes, void** fasta_out);
 /* Number of records and total filtered sequence bytes. */
 int mp_fasta_info(void* fasta, uint64_t* n_records, uint64_t* total_bytes);
 /* Borrowed pointers to record i's defline (UTF-8, with '>') and filtered sequence. */
 int mp_fasta_record(void* fasta, uint64_t i, const uint8_t** defline, uint64_t* defline_len,
                     const uint8_t** seq, uint64_t* seq_len);
+/* 1 when record i's filtered sequence is ASCII (no U+017F), else 0. */
+int mp_fasta_record_ascii(void* fasta, uint64_t i, int32_t* ascii);
 void mp_fasta_destroy(void* fasta);
 
 /* ---- STS file (replaces MerPCR.load_sts_file and helpers, engine.py:193-359) --

@@ -36,7 +36,7 @@ EXPORTS = (
     "mp_multi_create", "mp_multi_genome", "mp_multi_put", "mp_multi_seal", "mp_multi_run", "mp_multi_fetch",
     "mp_multi_device_search", "mp_multi_destroy",
     "mp_comm_unique_id", "mp_comm_create", "mp_comm_gather_hits", "mp_comm_destroy",
-    "mp_fasta_load", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record", "mp_fasta_destroy",
+    "mp_fasta_load", "mp_fasta_load_parallel", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record_ascii", "mp_fasta_record", "mp_fasta_destroy",
     "mp_format_hits",
     "mp_sts_parse", "mp_sts_info", "mp_sts_arrays", "mp_sts_destroy",
 )
@@ -122,6 +122,8 @@ def _sig(lib):
     lib.mp_comm_destroy.restype = None
     lib.mp_fasta_load.argtypes = [c_char_p, POINTER(c_void_p)]
     lib.mp_fasta_load_chunked.argtypes = [c_char_p, c_uint64, POINTER(c_void_p)]
+    lib.mp_fasta_load_parallel.argtypes = [c_char_p, c_int32, POINTER(c_void_p)]
+    lib.mp_fasta_record_ascii.argtypes = [c_void_p, c_uint64, POINTER(c_int32)]
     lib.mp_fasta_info.argtypes = [P, u64p, u64p]
     lib.mp_fasta_record.argtypes = [P, c_uint64, POINTER(c_void_p), u64p, POINTER(c_void_p), u64p]
     lib.mp_fasta_destroy.argtypes = [P]
@@ -480,29 +482,58 @@ def sts_parse(path: str, wordsize: int, default_pcr_size: int):
         lib().mp_sts_destroy(h)
 
 
-def fasta_read(path: str, chunk_bytes: int = 0):
-    """Read a FASTA file natively (mp_fasta_load_chunked); returns [(defline, sequence bytes)].
+def fasta_read(path: str, chunk_bytes: int = 0, threads: int = 0, with_ascii: bool = False):
+    """Read a FASTA file natively; returns [(defline, sequence bytes)].
 
     Raises UnicodeDecodeError for invalid UTF-8, as the reference's text-mode read does.
-    chunk_bytes (tests) sets the read size; 0 = the library default.
+    Default: the parallel whole-file reader (mp_fasta_load_parallel, `threads` host threads,
+    0 = every usable CPU).  chunk_bytes > 0 (tests): the streaming reader with that read size.
+    Sequences are views of the reader's buffers (freed with the last view); with_ascii adds
+    each record's "ASCII only" flag as a third field.
     """
     h = c_void_p()
-    rc = lib().mp_fasta_load_chunked(os.fsencode(path), chunk_bytes, ctypes.byref(h))
+    if chunk_bytes:
+        rc = lib().mp_fasta_load_chunked(os.fsencode(path), chunk_bytes, ctypes.byref(h))
+    else:
+        rc = lib().mp_fasta_load_parallel(os.fsencode(path), threads, ctypes.byref(h))
     _decode_error(rc)
     check(rc)
-    try:
-        n, total = c_uint64(), c_uint64()
-        check(lib().mp_fasta_info(h, ctypes.byref(n), ctypes.byref(total)))
-        out = []
-        dp, dl, sp, sl = c_void_p(), c_uint64(), c_void_p(), c_uint64()
-        for i in range(n.value):
-            check(lib().mp_fasta_record(h, i, ctypes.byref(dp), ctypes.byref(dl), ctypes.byref(sp), ctypes.byref(sl)))
-            d = ctypes.string_at(dp, dl.value).decode("utf-8")
-            seq = ctypes.string_at(sp, sl.value) if sl.value else b""
+    owner = _FastaHandle(h)
+    n, total = c_uint64(), c_uint64()
+    check(lib().mp_fasta_info(h, ctypes.byref(n), ctypes.byref(total)))
+    out = []
+    dp, dl, sp, sl = c_void_p(), c_uint64(), c_void_p(), c_uint64()
+    for i in range(n.value):
+        check(lib().mp_fasta_record(h, i, ctypes.byref(dp), ctypes.byref(dl), ctypes.byref(sp), ctypes.byref(sl)))
+        d = ctypes.string_at(dp, dl.value).decode("utf-8")
+        if sl.value:  # the reader's buffer itself (no copy); the view keeps the handle alive
+            arr = (ctypes.c_uint8 * sl.value).from_address(sp.value)
+            arr._owner = owner
+            seq = memoryview(arr).cast("B")
+        else:
+            seq = b""
+        if with_ascii:
+            asc = c_int32()
+            check(lib().mp_fasta_record_ascii(h, i, ctypes.byref(asc)))
+            out.append((d, seq, bool(asc.value)))
+        else:
             out.append((d, seq))
-        return out
-    finally:
-        lib().mp_fasta_destroy(h)
+    return out
+
+
+class _FastaHandle:
+    """Owns an mp_fasta handle; record views made by fasta_read reference it."""
+
+    def __init__(self, h):
+        self._h = h
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().mp_fasta_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
 
 
 def _csr(items):

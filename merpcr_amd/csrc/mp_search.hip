@@ -1253,9 +1253,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ WaveLds s_wl[kWaves];
 
     // stage the seed prefilter in LDS (once per persistent workgroup)
+#if !(defined(MP_ABLATE) && MP_ABLATE == 31)  // timing only: no staging, no scan
     for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)
         reinterpret_cast<uint4*>(s_lf)[i] = reinterpret_cast<const uint4*>(a.lfilt)[i];
     __syncthreads();
+#endif
 
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -1303,6 +1305,9 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         locate(ss);
         words(ss, nw0, nw1, niv);
     }
+#if defined(MP_ABLATE) && (MP_ABLATE == 30 || MP_ABLATE == 31)  // timing only: no super-step loop
+    ss = n_supers;
+#endif
     while (ss < n_supers) {
         const SeqSpan sp = pf;
         const uint64_t sbase = pf_sbase;
@@ -1385,16 +1390,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                             const uint32_t i = po[q] & 31u;
                             const uint32_t key = funnel3(A, B, C, i) >> shw;
                             pk[q] = ((funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F)) << 4) | (key & 15u);
-#if defined(MP_ABLATE) && MP_ABLATE == 4  // timing only: level-2 loads coalesced
-                            rw[q] = a.kgrp[(uint32_t)lane + (key & 1u)];
-#elif defined(MP_ABLATE) && MP_ABLATE == 5  // timing only: non-temporal level-2 loads
-                            {
-                                const uint64_t t = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(a.kgrp) + (v ? (key >> 4) : 0u));
-                                rw[q] = make_uint2((uint32_t)t, (uint32_t)(t >> 32));
-                            }
-#else
                             rw[q] = a.kgrp[v ? (key >> 4) : 0u];
-#endif
                         } else {
                             pk[q] = v ? L.rq.r[e] : 0u;
                             po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
@@ -1410,7 +1406,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     }
                 }
                 wave_sync();  // every list entry is in registers before the seeds overwrite it
-#if defined(MP_ABLATE) && (MP_ABLATE == 3 || MP_ABLATE == 4)  // timing only: level 1, the list and the level-2 loads
+#if defined(MP_ABLATE) && MP_ABLATE == 3  // timing only: level 1, the list and the level-2 loads
                 for (int q = 0; q < kP; ++q) ncand += rw[q].x & 1u;
                 r0 += kSeedQR;
                 continue;

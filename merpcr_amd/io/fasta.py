@@ -47,15 +47,16 @@ class ReaderRecord(FASTARecord):
     path (MerPCR.search / find_hits) encodes ASCII bytes directly, so the CLI never pays
     the bytes -> str -> bytes round trip (about 1.4 s per Gbp)."""
 
-    def __init__(self, defline: str, raw: bytes):
-        self._raw = raw
+    def __init__(self, defline: str, raw, ascii=None):
+        self._raw = raw  # bytes, or a memoryview of the reader's own buffer
+        self._ascii = ascii
         self._str = None
         super().__init__(defline=defline, sequence=None)
 
     @property
     def sequence(self) -> str:
         if self._str is None:
-            self._str = self._raw.decode("utf-8")
+            self._str = str(self._raw, "utf-8")
         return self._str
 
     @sequence.setter
@@ -75,9 +76,12 @@ class ReaderRecord(FASTARecord):
         return f"FASTARecord(defline={self.defline!r}, sequence={self.sequence!r}, label={self.label!r})"
 
     def raw_ascii(self):
-        """The sequence as ASCII bytes without building the str, or None."""
-        if self._str is None and self._raw is not None and self._raw.isascii():
-            return self._raw
+        """The sequence as ASCII bytes (or a view of them) without building the str, or None."""
+        if self._str is None and self._raw is not None:
+            if self._ascii is None:  # the only non-ASCII bytes the filter keeps are U+017F's
+                self._ascii = bytes(self._raw).isascii()
+            if self._ascii:
+                return self._raw
         return None
 
 
@@ -95,8 +99,8 @@ class FASTALoader:
             return []
         logger.info(f"Reading FASTA file: {filename}")
         records = []
-        for defline, seq in _native.fasta_read(filename, _chunk_bytes):
-            records.append(ReaderRecord(defline, seq))
+        for defline, seq, ascii in _native.fasta_read(filename, _chunk_bytes, with_ascii=True):
+            records.append(ReaderRecord(defline, seq, ascii))
         logger.info(f"Loaded {len(records)} sequences in {time.time() - start:.2f} seconds")
         return records
 

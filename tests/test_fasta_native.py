@@ -127,3 +127,50 @@ def test_reader_records_keep_bytes(tmp_path):
     assert all(np.array_equal(x, y) for x, y in zip(enc, ref))
     got[0].sequence = "TTTT"
     assert got[0].raw_ascii() is None and np.array_equal(eng.encode_records(got[:1])[0], np.frombuffer(b"TTTT", np.uint8))
+
+
+def _parallel_read(path, threads):
+    try:
+        return [(d, s) for d, s in _native.fasta_read(path, 0, threads)]
+    except Exception as e:  # noqa: BLE001
+        return type(e)
+
+
+@pytest.mark.parametrize("threads", [2, 3, 7, 16])
+def test_parallel_reader_splits(tmp_path, threads):
+    """The parallel whole-file reader with more threads than a small file needs: its
+    validation, header and filter splits fall inside lines, UTF-8 sequences, CR/LF pairs
+    and headers; every split must give the streaming reader's records."""
+    rng = random.Random(99 + threads)
+    p = str(tmp_path / "x.fa")
+    for i in range(300):
+        text = _random_text(rng)
+        if not text:
+            continue
+        with open(p, "wb") as fh:
+            fh.write(text.encode("utf-8"))
+        exp = _native.fasta_read(p, 1 << 20) if _expected(p) is not UnicodeDecodeError else UnicodeDecodeError
+        got = _parallel_read(p, threads)
+        assert got == exp, (i, text)
+
+
+def test_parallel_reader_long_lines_and_records(tmp_path):
+    """Multi-megabyte single-line and 60-column records, soft-masked, with N runs: the
+    parallel reader (default threads, pieces of ~64 KiB and more) equals the streaming one."""
+    import numpy as np
+    rng = np.random.default_rng(3)
+    parts = []
+    for r in range(5):
+        n = int(rng.integers(1, 3_000_000))
+        s = np.frombuffer(b"ACGTNacgtn", np.uint8)[rng.integers(0, 10, n)].tobytes()
+        parts.append(f">rec{r} some words\t \n".encode())
+        if r % 2:
+            parts.append(s + b"\n")
+        else:
+            parts.append(b"\n".join(s[i:i + 60] for i in range(0, n, 60)) + b"\r\n")
+    p = str(tmp_path / "big.fa")
+    with open(p, "wb") as fh:
+        fh.write(b"".join(parts))
+    exp = _native.fasta_read(p, 1 << 20)
+    for threads in (0, 5):
+        assert _native.fasta_read(p, 0, threads) == exp
