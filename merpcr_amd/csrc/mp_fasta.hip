@@ -551,4 +551,18 @@ MP_EXPORT int mp_fasta_record_ascii(void* fasta, uint64_t i, int32_t* ascii) {
     return MP_OK;
 }
 
-MP_EXPORT void mp_fasta_destroy(void* fasta) { delete (Fasta*)fasta; }
+// Large handles are freed on a detached thread: returning gigabytes of touched pages to
+// the system took ~0.26 s of the CLI's wall time for c3's 3 GB genome.
+MP_EXPORT void mp_fasta_destroy(void* fasta) {
+    Fasta* f = (Fasta*)fasta;
+    if (!f) return;
+    if (f->total < ((uint64_t)64 << 20)) {
+        delete f;
+        return;
+    }
+    try {
+        std::thread([f] { delete f; }).detach();
+    } catch (...) {
+        delete f;
+    }
+}
