@@ -1197,6 +1197,9 @@ constexpr uint32_t kSChunk = MP_SCHUNK;
 // in chunks of 8, 0.323 in chunks of 4; full c3 is best with 8).  Only scans under
 // MP_SCHED_MIN super-steps per wave keep the static order.
 constexpr uint32_t kSChunkShort = 128;
+#ifndef MP_SCHUNK_SHORT
+#define MP_SCHUNK_SHORT 4
+#endif
 #ifndef MP_SCHED_MIN
 #define MP_SCHED_MIN 4u
 #endif
@@ -1215,7 +1218,7 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
             return (uint64_t)blockIdx.x * (uint64_t)kW + (uint64_t)w;
         }
         stride = 0;
-        chunk = n_supers < (uint64_t)waves * kSChunkShort ? 4u : kSChunk;
+        chunk = n_supers < (uint64_t)waves * kSChunkShort ? (uint32_t)MP_SCHUNK_SHORT : kSChunk;
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
         ctr = reinterpret_cast<unsigned int*>(counters + kSchedBase + x * kStatStride);
