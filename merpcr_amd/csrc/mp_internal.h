@@ -348,7 +348,31 @@ inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 // internal entry points shared across TUs
 int sort_hits(Search* s, uint64_t n, hipStream_t st);
 bool sort_hits_device_ok(const Search* s);
-int sort_hits_device(Search* s, hipStream_t st);  // hit count read on the device, writes s->out
+// The device sort's packing and bucketing of the 64-bit order key (k << low_bits | record
+// rank << try_bits | try rank; bucket = key >> shift), fixed per search before the scan.
+struct SortPlan {
+    unsigned try_bits = 0, low_bits = 0, shift = 0;
+    uint32_t nb = 0;
+};
+SortPlan sort_plan(const Search* s);
+// fused: pair_kernel already wrote the packed keys (tmp_lo) and the bucket counts
+int sort_hits_device(Search* s, hipStream_t st, bool fused);  // hit count read on the device, writes s->out
+uint32_t* sort_bucket_counts(Search* s);          // the bucket count array (zeroed by the scan kernels)
+
+// Raw hits arrive in runs of one bucket (a survivor's tries, a wave's batch of nearby
+// survivors; IUPAC primers over N runs pile thousands on a few positions).  Same-address
+// atomics serialise at the L2, so each wave collapses its runs of equal buckets: the run
+// head adds the run length once and hands the base to the run's other lanes.  Wave-uniform.
+__device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint32_t& head, uint32_t& len) {
+    const uint32_t prev = (uint32_t)__shfl_up((int)b, 1, 64);
+    const uint64_t heads = __ballot(on && (lane == 0 || prev != b));
+    const uint64_t upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+    head = upto ? 63u - (uint32_t)__clzll(upto) : 0u;  // this lane's run head
+    const uint64_t above = heads & ~((2ull << lane) - 1ull);
+    const uint64_t onm = __ballot(on);
+    const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1u : 64u - (uint32_t)__clzll(onm);
+    len = end - (uint32_t)lane;  // meaningful on heads only
+}
 int alloc_sort_buckets(Search* s);                // the device sort's bucket arrays (at create)
 constexpr int kSortOverflow = 6;                  // counters[6]: a device-sort bucket overflowed
 int sort_runs(Genome* g, hipStream_t st);

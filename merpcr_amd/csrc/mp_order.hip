@@ -28,21 +28,6 @@ static unsigned bits_for(uint64_t v) {
 constexpr uint32_t kSortCap = 2048;
 constexpr unsigned kMaxBucketBits = 16;
 
-// Raw hits arrive in runs of one bucket (a survivor's tries, a wave's batch of nearby
-// survivors; IUPAC primers over N runs pile thousands on a few positions).  Same-address
-// atomics serialise at the L2, so each wave collapses its runs of equal buckets: the run
-// head adds the run length once and hands the base to the run's other lanes.
-__device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint32_t& head, uint32_t& len) {
-    const uint32_t prev = (uint32_t)__shfl_up((int)b, 1, 64);
-    const uint64_t heads = __ballot(on && (lane == 0 || prev != b));
-    const uint64_t upto = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
-    head = upto ? 63u - (uint32_t)__clzll(upto) : 0u;  // this lane's run head
-    const uint64_t above = heads & ~((2ull << lane) - 1ull);
-    const uint64_t onm = __ballot(on);
-    const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1u : 64u - (uint32_t)__clzll(onm);
-    len = end - (uint32_t)lane;  // meaningful on heads only
-}
-
 __global__ void bucket_hist(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
                             const unsigned long long* __restrict__ counters, uint64_t cap, unsigned try_bits,
                             unsigned low_bits, unsigned shift, uint64_t* __restrict__ keys, uint32_t* __restrict__ cnt) {
@@ -197,36 +182,46 @@ int alloc_sort_buckets(Search* s) {
     return MP_OK;
 }
 
-int sort_hits_device(Search* s, hipStream_t st) {
+SortPlan sort_plan(const Search* s) {
+    SortPlan P;
     const unsigned hi_bits = bits_for(s->genome->total);
-    const unsigned try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
-    const unsigned low_bits = s->table->rank_bits + try_bits;
-    const unsigned key_bits = hi_bits + low_bits;
+    P.try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
+    P.low_bits = s->table->rank_bits + P.try_bits;
+    const unsigned key_bits = hi_bits + P.low_bits;
     // ~32 hits per bucket at the buffer's capacity (the count is not known on the host)
     unsigned bb = bits_for(s->cap / 32);
     bb = std::min(std::max(bb, 6u), kMaxBucketBits);
     if (s->opt.sort_bucket_bits > 0) bb = std::min((unsigned)s->opt.sort_bucket_bits, kMaxBucketBits);
     bb = std::min(bb, key_bits);
-    const unsigned shift = key_bits - bb;
-    const uint32_t nb = 1u << bb;
+    P.shift = key_bits - bb;
+    P.nb = 1u << bb;
+    return P;
+}
+
+uint32_t* sort_bucket_counts(Search* s) { return s->bucket; }
+
+int sort_hits_device(Search* s, hipStream_t st, bool fused) {
+    const SortPlan P = sort_plan(s);
     const int arc = alloc_sort_buckets(s);
     if (arc) return arc;
     uint32_t* cnt = s->bucket;
     uint32_t* off = cnt + (1u << kMaxBucketBits);
     uint32_t* cursor = off + (1u << kMaxBucketBits) + 1;
-    MP_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)nb * 4, st));
     const uint32_t grid = (uint32_t)std::min<uint64_t>((s->cap + 255) / 256, 2048);
-    hipLaunchKernelGGL(bucket_hist, dim3(grid), dim3(256), 0, st, s->keys, s->keys + s->cap, s->counters, s->cap,
-                       try_bits, low_bits, shift, s->tmp_lo, cnt);
+    if (!fused) {
+        MP_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)P.nb * 4, st));
+        hipLaunchKernelGGL(bucket_hist, dim3(grid), dim3(256), 0, st, s->keys, s->keys + s->cap, s->counters, s->cap,
+                           P.try_bits, P.low_bits, P.shift, s->tmp_lo, cnt);
+        MP_HIP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, cnt, P.nb, off, cursor);
     MP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, cnt, nb, off, cursor);
-    MP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, s->counters, s->cap, shift, cursor,
+    hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, s->counters, s->cap, P.shift, cursor,
                        s->tmp_hi);
     MP_HIP_CHECK(hipGetLastError());
     const Genome* g = s->genome;
-    hipLaunchKernelGGL(bucket_sort_decode, dim3(nb), dim3(256), 0, st, s->tmp_hi, off, try_bits, low_bits, g->d_base,
-                       g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->counters);
+    hipLaunchKernelGGL(bucket_sort_decode, dim3(P.nb), dim3(256), 0, st, s->tmp_hi, off, P.try_bits, P.low_bits,
+                       g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->counters);
     MP_HIP_CHECK(hipGetLastError());
     return MP_OK;
 }

@@ -87,7 +87,18 @@ struct ScanArgs {
     uint64_t surv_cap;
     uint4* tails;           // bucket-tail references (2 x uint4 each), see tail_kernel
     uint64_t tails_cap;
+    // device sort fused into the pair check (SortPlan): pair_kernel writes each hit's packed
+    // order key and counts its bucket; the scan kernels zero the counts (null: not fused)
+    uint64_t* sort_keys;
+    uint32_t* sort_cnt;
+    uint32_t sort_nb, sort_shift, sort_try_bits, sort_low_bits;
 };
+
+// Bucket counts of the fused device sort, zeroed by every block of a scan kernel.
+__device__ __forceinline__ void zero_sort_counts(const ScanArgs& a) {
+    if (!a.sort_cnt) return;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.sort_nb; i += gridDim.x * blockDim.x) a.sort_cnt[i] = 0;
+}
 
 // 64-bit min/max as plain compares (HIP's templated min/max on 64-bit integers went
 // through f64 conversions in the scan kernel's loop header).
@@ -287,19 +298,39 @@ struct HitStage {
     uint32_t n;
 };
 
+// The stage's hits at hit list slots off, off + 1, ...: the raw (hi, lo) pair and, for the
+// fused device sort, the packed order key and its bucket count (bucket_hist's work).
+// Wave-uniform (the bucket runs ballot).
+__device__ __forceinline__ void write_hits(const ScanArgs& a, const HitStage& S, uint64_t off, int lane) {
+    for (uint32_t b0 = 0; b0 < S.n; b0 += 64) {
+        const uint32_t i = b0 + (uint32_t)lane;
+        const bool on = i < S.n && off + i < a.cap;
+        uint32_t bk = 0xFFFFFFFFu;
+        if (on) {
+            const uint64_t hi = S.hi[i], lo = S.lo[i];
+            a.hit_hi[off + i] = hi;
+            a.hit_lo[off + i] = lo;
+            if (a.sort_cnt) {
+                const uint64_t key = (hi << a.sort_low_bits) | ((lo >> 32) << a.sort_try_bits) | (lo & 0xFFFFFFFFull);
+                a.sort_keys[off + i] = key;
+                bk = (uint32_t)(key >> a.sort_shift);
+            }
+        }
+        if (a.sort_cnt) {
+            uint32_t head, len;
+            bucket_runs(bk, on, lane, head, len);
+            if (on && head == (uint32_t)lane) atomicAdd(&a.sort_cnt[bk], len);
+        }
+    }
+}
+
 __device__ __forceinline__ void stage_flush(const ScanArgs& a, HitStage& S, int lane) {
     const uint32_t cnt = S.n;
     if (!cnt) return;
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(&a.counters[0], (unsigned long long)cnt);
     base = (unsigned long long)__shfl((long long)base, 0, 64);
-    for (uint32_t i = (uint32_t)lane; i < cnt; i += 64) {
-        const unsigned long long idx = base + i;
-        if (idx < a.cap) {
-            a.hit_hi[idx] = S.hi[i];
-            a.hit_lo[idx] = S.lo[i];
-        }
-    }
+    write_hits(a, S, base, lane);
     wave_sync_lds();
     if (lane == 0) S.n = 0;
     wave_sync_lds();
@@ -1255,6 +1286,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
 
+    zero_sort_counts(a);
     // stage the seed prefilter in LDS (once per persistent workgroup)
 #if !(defined(MP_ABLATE) && MP_ABLATE == 31)  // timing only: no staging, no scan
     for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)
@@ -1616,6 +1648,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     const uint32_t ngrp = max(1u, (1u << (2 * W)) / 32);
     uint32_t* s_esc = reinterpret_cast<uint32_t*>(s_grp + ngrp);
     uint32_t* s_sum = s_esc + ngrp;  // dsum_mode: 16-bit summary per key, two per word
+    zero_sort_counts(a);
     for (uint32_t i = threadIdx.x; i < ngrp; i += kDenseBlock) {
         s_grp[i] = a.dgrp[i];
         s_esc[i] = a.dgesc[i];
@@ -1977,12 +2010,7 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     const int w = threadIdx.x >> 6;
     uint64_t off = s_base;
     for (int q = 0; q < w; ++q) off += s_st[q].n;
-    for (uint32_t i = (uint32_t)lane; i < S.n; i += 64) {
-        if (off + i < a.cap) {
-            a.hit_hi[off + i] = S.hi[i];
-            a.hit_lo[off + i] = S.lo[i];
-        }
-    }
+    write_hits(a, S, off, lane);
 }
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
@@ -2236,6 +2264,10 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     // crowded hit positions (IUPAC primers over N runs, repeats) overflow the buckets and
     // pay both sorts; once seen, this search orders with rocPRIM directly
     const bool dev_sort = sort_hits_device_ok(s) && !s->sort_crowded;
+    // the histogram pass of the device sort runs inside pair_kernel's hit flush
+    a.sort_cnt = nullptr;
+    a.sort_keys = nullptr;
+    a.sort_nb = a.sort_shift = a.sort_try_bits = a.sort_low_bits = 0;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
                                                        (uint64_t)s->n_cu * kBlocksPerCU);
     // scan -> fingerprint survivors (+ bucket-tail references -> tail survivors) -> pair
@@ -2266,6 +2298,15 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         a.surv_cap = s->surv_cap;
         a.tails = s->tails;
         a.tails_cap = s->tails_cap;
+        if (dev_sort) {  // after a hit-list regrowth too: the plan follows the capacity
+            const SortPlan P = sort_plan(s);
+            a.sort_cnt = sort_bucket_counts(s);
+            a.sort_keys = s->tmp_lo;
+            a.sort_nb = P.nb;
+            a.sort_shift = P.shift;
+            a.sort_try_bits = P.try_bits;
+            a.sort_low_bits = P.low_bits;
+        }
         if (rescan) {
             MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
             MP_HIP_CHECK(hipEventRecord(s->ev0, st));
@@ -2306,6 +2347,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
                 MP_HIP_CHECK(hipGetLastError());
             }
         } else {  // hit list regrown: counters of the pair check and the sort only
+            if (a.sort_cnt) MP_HIP_CHECK(hipMemsetAsync(a.sort_cnt, 0, (size_t)a.sort_nb * 4, st));
             MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long), st));
             MP_HIP_CHECK(hipMemsetAsync(s->counters + kSortOverflow, 0, sizeof(unsigned long long), st));
             MP_HIP_CHECK(hipMemsetAsync(s->counters + kPairQBase, 0, 8 * kStatStride * sizeof(unsigned long long), st));
@@ -2319,7 +2361,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         MP_HIP_CHECK(hipGetLastError());
         MP_HIP_CHECK(hipEventRecord(s->ev2, st));
         if (dev_sort) {  // hit order on the device count: no host round trip before the sort
-            const int src = sort_hits_device(s, st);
+            const int src = sort_hits_device(s, st, true);
             if (src) return src;
             MP_HIP_CHECK(hipEventRecord(s->ev3, st));
         }
