@@ -254,6 +254,9 @@ def main():
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
                     help="strong: one genome split in N owned ranges; weak: each rank scans its own "
                          "config-sized contig set (N x the genome)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="diagnostic: every rank on device 0 (rehearses the N-rank path, RCCL included, on a "
+                         "one-GPU box); the JSON line is then not the metric")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time only rank 0's owned range of an N-way split on this one GPU "
                          "(no collective); the JSON line is then not the metric")
@@ -265,7 +268,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = None
@@ -413,6 +416,8 @@ def main():
     }
     if args.shard_of > 1:
         out["diagnostic"] = f"rank 0 of a {args.shard_of}-way owned-range split, alone on one GPU (not the metric)"
+    if args.rehearse_one_gpu:
+        out["diagnostic"] = f"{world} ranks sharing device 0 (rehearsal of the N-rank path, not the metric)"
     parity_ok = True
     if world == 1 and not args.no_e2e:
         out["e2e"] = end_to_end(eng, table, names, lens, buf, offs, local, stream)
