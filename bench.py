@@ -275,7 +275,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")          # control plane only
-        comm = native_comm(local)                 # data plane: RCCL inside libmerpcr_hip
+        # data plane: RCCL inside libmerpcr_hip (RCCL refuses two ranks on one device: the
+        # one-GPU rehearsal gathers through gloo on the host instead)
+        comm = None if args.rehearse_one_gpu else native_comm(local)
 
     cfg = dict(synth.CONFIGS[args.config])
     total = int(cfg["total"] * args.scale) // 64 * 64
@@ -319,6 +321,12 @@ def main():
     def step():
         nonlocal gathered
         n = search.run(rng, stream)
+        if world > 1 and comm is None:  # rehearsal: host gather over gloo
+            from merpcr_amd.dist import gather_hits as gloo_gather
+            mine = search.fetch(n, stream)
+            buf_h = torch.from_numpy(np.frombuffer(mine.tobytes() + b"\0" * HIT_BYTES, dtype=np.uint8).copy())
+            got = gloo_gather(buf_h, n, seq_base=len(lens) * rank if weak else 0)
+            return got.numel() // HIT_BYTES if rank == 0 else n
         if world > 1:
             cap = gathered.numel() // HIT_BYTES if rank == 0 else 0
             try:
@@ -363,7 +371,8 @@ def main():
         tot_bases = float(sum(lens))
     tot_hits = float(nhits)  # after the gather: every rank's hits (N > 1)
     if rank != 0:
-        comm.close()
+        if comm is not None:
+            comm.close()
         torch.distributed.destroy_process_group()
         return
     bases = float(sum(lens))          # one rank's genome (= the whole job's at N=1 or strong)
@@ -433,7 +442,8 @@ def main():
                                                                   args.cpu_budget)
     print(json.dumps(out), flush=True)
     if world > 1:
-        comm.close()
+        if comm is not None:
+            comm.close()
         torch.distributed.destroy_process_group()
     if not parity_ok:
         log("FAIL: the GPU hit list differs from the CPU oracle's on the baseline sample")
