@@ -140,6 +140,9 @@ typedef struct mp_search_options {
 } mp_search_options;
 /* Replace the handle's options (reallocating the lists to the given capacities). */
 int mp_search_set_options(void* search, const mp_search_options* opt);
+/* Per-stage timing (tail, pair and order events; default on).  Off, a run records only the
+ * scan kernel's two events: each event between two kernels idles the GPU ~6 us. */
+int mp_search_set_stage_timing(void* search, int32_t on);
 /* Scan, verify, pair-check and sort.  *n_hits receives the number of hits of
  * the owned range (range NULL = whole genome).  Synchronises `stream`. */
 int mp_search_run(void* search, const mp_range* range, void* stream, uint64_t* n_hits);

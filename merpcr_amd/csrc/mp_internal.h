@@ -203,6 +203,7 @@ struct Search {
     std::vector<SeqSpan> last_spans;        // spans on the device (a rerun of the same range uploads nothing)
     unsigned long long* h_cnt = nullptr;    // pinned host copy of counters[0..8) (the run's one readback)
     hipEvent_t evd = nullptr;               // the readback's completion (polled, not slept on)
+    bool stage_timing = true;               // events around tail/pair/order too (mp_search_set_stage_timing)
 };
 
 // ---------------------------------------------------------------- device helpers

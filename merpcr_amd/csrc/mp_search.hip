@@ -2041,6 +2041,14 @@ __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* _
     out[i] = h;
 }
 
+// Per-stage events (tail, pair, order timings) only with stage timing on: each event
+// recorded between two kernels cost ~6 us of idle GPU (c2 step trace: 6 us gaps between
+// kernels with them, none without).  The scan kernel's own pair of events always stays.
+#define MID_EVENT(x)                  \
+    do {                              \
+        if (s->stage_timing) MP_HIP_CHECK(x); \
+    } while (0)
+
 // Wait for an event by polling (hipEventQuery) instead of a blocking synchronisation.
 static hipError_t wait_event(hipEvent_t ev) {
     for (;;) {
@@ -2101,6 +2109,13 @@ constexpr uint64_t kDefaultHitCap = 1 << 16, kDefaultSurvCap = 1 << 20, kDefault
 }  // namespace mp
 
 using namespace mp;
+
+MP_EXPORT int mp_search_set_stage_timing(void* search, int32_t on) {
+    Search* s = (Search*)search;
+    if (!s) return fail(MP_E_ARG, "mp_search_set_stage_timing: null search");
+    s->stage_timing = on != 0;
+    return MP_OK;
+}
 
 MP_EXPORT int mp_search_set_options(void* search, const mp_search_options* opt) {
     Search* s = (Search*)search;
@@ -2354,16 +2369,16 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
             MP_HIP_CHECK(hipEventRecord(s->ev0, st));
             MP_HIP_CHECK(hipEventRecord(s->evt, st));
         }
-        MP_HIP_CHECK(hipEventRecord(s->ev1, st));
+        MID_EVENT(hipEventRecord(s->ev1, st));
         const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
                                                                : s->pair_per_cu;
         hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
-        MP_HIP_CHECK(hipEventRecord(s->ev2, st));
+        MID_EVENT(hipEventRecord(s->ev2, st));
         if (dev_sort) {  // hit order on the device count: no host round trip before the sort
             const int src = sort_hits_device(s, st, true);
             if (src) return src;
-            MP_HIP_CHECK(hipEventRecord(s->ev3, st));
+            MID_EVENT(hipEventRecord(s->ev3, st));
         }
         // one readback into pinned memory, its completion polled: a blocking stream
         // synchronisation added tens of microseconds per run (small searches, sharded steps)
@@ -2373,7 +2388,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         memcpy(cnt, s->h_cnt, sizeof(cnt));
         if (rescan) {
             MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
-            MP_HIP_CHECK(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
+            MID_EVENT(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
         }
         if (cnt[2] <= s->surv_cap && cnt[4] <= s->tails_cap && cnt[0] <= s->cap) break;
         ++s->n_regrowths;
@@ -2387,7 +2402,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
     }
     if (cnt[2] > s->surv_cap || cnt[4] > s->tails_cap || cnt[0] > s->cap)
         return fail(MP_E_STATE, "mp_search_run: list overflow after growth");
-    MP_HIP_CHECK(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
+    MID_EVENT(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
     s->n_candidates = cnt[1];
     s->n_survivors = cnt[3];
     const uint64_t nh = cnt[0];
@@ -2401,10 +2416,11 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
                                g->d_base, g->d_len, g->n_seq, t->inv_rank, t->recs, s->out);
             MP_HIP_CHECK(hipGetLastError());
         }
-        MP_HIP_CHECK(hipEventRecord(s->ev3, st));
+        MID_EVENT(hipEventRecord(s->ev3, st));
         MP_HIP_CHECK(hipStreamSynchronize(st));
     }
-    MP_HIP_CHECK(hipEventElapsedTime(&s->order_ms, s->ev2, s->ev3));
+    MID_EVENT(hipEventElapsedTime(&s->order_ms, s->ev2, s->ev3));
+    if (!s->stage_timing) s->tail_ms = s->pair_ms = s->order_ms = -1.f;  // not measured
     s->n_hits = nh;
     if (n_hits) *n_hits = nh;
     return MP_OK;
