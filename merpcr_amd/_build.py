@@ -42,16 +42,18 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_native(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB) -> str:
-    """Compile the sources and link `lib`; `defines` (timing-only variants) get their own objects."""
+def build_native(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB, src_dir: str = CSRC,
+                 tag: str = "") -> str:
+    """Compile the sources and link `lib`; `defines` and a `src_dir` copy (timing-only
+    variants, scripts/ablate.py) get their own objects, named by `tag`."""
     os.makedirs(LIBDIR, exist_ok=True)
     cc = hipcc()
-    tag = "".join("_" + d.replace("=", "") for d in defines)
-    hdrs = [os.path.normpath(os.path.join(CSRC, h)) for h in HEADERS]
+    tag = tag + "".join("_" + d.replace("=", "") for d in defines)
+    hdrs = [os.path.normpath(os.path.join(src_dir, h)) for h in HEADERS]
     objs = []
     jobs = []
     for src in SOURCES:
-        sp = os.path.join(CSRC, src)
+        sp = os.path.join(src_dir, src)
         op = os.path.join(LIBDIR, src.replace(".hip", tag + ".o"))
         objs.append(op)
         if force or _stale(op, [sp] + hdrs):

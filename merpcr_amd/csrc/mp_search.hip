@@ -1288,11 +1288,9 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 
     zero_sort_counts(a);
     // stage the seed prefilter in LDS (once per persistent workgroup)
-#if !(defined(MP_ABLATE) && MP_ABLATE == 31)  // timing only: no staging, no scan
     for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)
         reinterpret_cast<uint4*>(s_lf)[i] = reinterpret_cast<const uint4*>(a.lfilt)[i];
     __syncthreads();
-#endif
 
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -1340,9 +1338,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         locate(ss);
         words(ss, nw0, nw1, niv);
     }
-#if defined(MP_ABLATE) && (MP_ABLATE == 30 || MP_ABLATE == 31)  // timing only: no super-step loop
-    ss = n_supers;
-#endif
     while (ss < n_supers) {
         const SeqSpan sp = pf;
         const uint64_t sbase = pf_sbase;
@@ -1366,12 +1361,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // pass -- full lanes, all passes' rank-word loads in flight together -- and the
             // seeds are compacted back into the same arrays as {offset, rank}
             const uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
-#if defined(MP_ABLATE) && MP_ABLATE == 1  // timing only: level 1 alone
-            ncand += (uint32_t)__popc(rem);
-            if (nx < n_supers) { locate(nx); words(nx, nw0, nw1, niv); }
-            ss = nx;
-            continue;
-#endif
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
@@ -1396,13 +1385,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                 }
                 wave_sync();
                 const uint32_t nr = min(tot - r0, kSeedQR);
-#if defined(MP_ABLATE) && MP_ABLATE == 2  // timing only: level 1 and the list
-                if (first) { first = false; if (nx < n_supers) { locate(nx); words(nx, nw0, nw1, niv); } }
-                ncand += (uint32_t)L.rq.r[lane] & 1u;
-                wave_sync();
-                r0 += kSeedQR;
-                continue;
-#endif
                 constexpr int kP = (kSeedQR + 63) / 64;
                 uint32_t pk[kP], po[kP];
                 uint2 rw[kP];
@@ -1441,11 +1423,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     }
                 }
                 wave_sync();  // every list entry is in registers before the seeds overwrite it
-#if defined(MP_ABLATE) && MP_ABLATE == 3  // timing only: level 1, the list and the level-2 loads
-                for (int q = 0; q < kP; ++q) ncand += rw[q].x & 1u;
-                r0 += kSeedQR;
-                continue;
-#endif
                 if constexpr (kRkf) {
                     // the few seeds that pass the key groups (c3: 4% of seeds) leave as key
                     // references for tail_kernel, with their window, exception bits and bases

@@ -1,6 +1,8 @@
 """Time ablation variants of the scan kernel on the same resident c3 data (timing only).
 
-Builds libmerpcr_hip_ablateN.so with -DMP_ABLATE=N next to the product library,
+Builds libmerpcr_hip_ablateN.so next to the product library from a copy of the sources
+with timing-only variant N of scripts/ablate_variants.py applied (the product source has no
+ablation code),
 generates the workload once, and for each variant packs the genome, runs the
 search `--steps` times and prints the mean scan-kernel time.  Hit counts of the
 variants are meaningless except for variant 0 (the product kernel).
@@ -14,6 +16,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
@@ -41,14 +44,20 @@ def main():
             defs = ("MP_NT_STREAM=1",)
         elif "=" in v:
             defs = tuple(v.split("+"))
-        else:
-            defs = (f"MP_ABLATE={int(v)}",)
+        else:  # a timing-only variant of scripts/ablate_variants.py on a copy of the sources
+            defs = ()
         tag = "".join(ch if ch.isalnum() else "_" for ch in v)
-        path = _build.LIB if not defs else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{tag}.so")
+        src_dir, src_tag = _build.CSRC, ""
+        if v.isdigit() and v != "0":
+            import ablate_variants
+            src_dir = ablate_variants.make_source_dir(int(v), _build.CSRC,
+                                                      os.path.join(tempfile.gettempdir(), f"mp_ablate_{v}"))
+            src_tag = f"_ablate{v}"
+        path = _build.LIB if v == "0" or v.startswith("opt:") else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{tag}.so")
         saved = _build.SOURCE_FLAGS
         if flags is not None:
             _build.SOURCE_FLAGS = flags
-        libs[v] = _build.build_native(defines=defs, lib=path)
+        libs[v] = _build.build_native(defines=defs, lib=path, src_dir=src_dir, tag=src_tag)
         _build.SOURCE_FLAGS = saved
     if args.build_only:
         return
