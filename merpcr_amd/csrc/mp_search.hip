@@ -450,26 +450,50 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
     // per try offset instead of one per survivor.
     const bool lp = keep && fast && clean;
     if (__any(lp)) {
-        const uint64_t* sj = pst + lane;
+        // A batch of B <= 32 survivors leaves 64 - B lanes idle, so the tries are split:
+        // the wave is 64 / Bp groups of Bp lanes (Bp = B rounded up to a power of two),
+        // lane L takes survivor L % Bp and the L / Bp-th slice of its tries.  The survivor's
+        // values come from its own lane by shuffles; its staged words and planes are its LDS
+        // column.  c2 (8 survivors per wave): the try loop from 101 passes to 13.
+        uint32_t Bp = 1;
+        while (Bp < batch) Bp <<= 1;
+        const int s = (int)((uint32_t)lane & (Bp - 1u));
+        const uint32_t grp = (uint32_t)lane / Bp, ngrp = 64u / Bp;
+        const bool slp = __shfl((int)lp, s, 64) != 0;
+        const uint32_t sl1 = (uint32_t)__shfl((int)r.l1, s, 64), sl2 = (uint32_t)__shfl((int)r.l2, s, 64);
+        const int slo = __shfl(lo, s, 64), shi = __shfl(hi, s, 64);
+        const uint32_t se = (uint32_t)__shfl((int)e, s, 64);
+        const uint64_t sP0 = shfl64(P0l, s), sgk = shfl64(gk, s);
+        const uint32_t srk = (uint32_t)__shfl((int)rk, s, 64);
+        const uint64_t* sj = pst + s;
         const uint64_t Q0 = sj[(kPW + kPE) * MP_PBATCH], Q1 = sj[(kPW + kPE + 1) * MP_PBATCH];
         const uint64_t Q2 = sj[(kPW + kPE + 2) * MP_PBATCH], Q3 = sj[(kPW + kPE + 3) * MP_PBATCH];
-        const uint64_t in2 = sp_lt((int)r.l2);
+        const uint64_t in2 = sp_lt((int)sl2);
         const uint64_t two = (Q0 & Q1) | (Q0 & Q2) | (Q0 & Q3) | (Q1 & Q2) | (Q1 & Q3) | (Q2 & Q3);
         const bool plain2 = two == 0 && ((Q0 | Q1 | Q2 | Q3) & in2) == in2;
         const uint64_t code2 = ((Q1 | Q3) & kEven) | (((Q2 | Q3) & kEven) << 1);
-        const uint64_t prot2 = sp_lt(min(a.X, (int)r.l2));  // '-' strand: positions < X
+        const uint64_t prot2 = sp_lt(min(a.X, (int)sl2));  // '-' strand: positions < X
         // try t (d = t - lo) is in bounds for t in [ta, lo + hi] (engine.py:548-560: a
         // non-positive offset needs the product to end past primer 1, and the window inside
         // the sequence, which hi already guarantees)
-        const int64_t ta = smin64((int64_t)lo + 1, smax64(0, (int64_t)r.l1 + r.l2 + lo - (int64_t)e));
-        const int32_t tb = lp ? lo + hi : -1;
-        const uint32_t a5 = (uint32_t)(P0l & 31);
+        const int64_t ta = smin64((int64_t)slo + 1, smax64(0, (int64_t)sl1 + sl2 + slo - (int64_t)se));
+        const int32_t tb = slp ? slo + shi : -1;
+        // this lane's slice [t0, t0 + chunk) of tries; chunk from the batch's largest count
+        int32_t tmax = tb + 1;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o, 64));
+        const int32_t chunk = (tmax + (int32_t)ngrp - 1) / (int32_t)ngrp;
+        const int32_t t0 = (int32_t)grp * chunk;
+        const uint32_t u0 = (uint32_t)(sP0 & 31) + (uint32_t)t0;  // first base of try t0 in the staged words
+        const uint32_t a5 = u0 & 31u;
+        const int w0 = min((int)(u0 >> 5), kPW - 2);
         auto fun = [&](uint64_t x0, uint64_t x1) { return a5 ? (x0 << (2 * a5)) | (x1 >> (64 - 2 * a5)) : x0; };
-        uint64_t G = fun(sj[0], sj[MP_PBATCH]);
-        uint64_t F = fun(sj[MP_PBATCH], sj[2 * MP_PBATCH]);
-        int nw = 2;
-        const bool all_plain = __all(!lp || plain2);
-        for (int32_t t = 0; __any(t <= tb); ++t) {
+        uint64_t G = fun(sj[w0 * MP_PBATCH], sj[(w0 + 1) * MP_PBATCH]);
+        uint64_t F = fun(sj[(w0 + 1) * MP_PBATCH], sj[min(w0 + 2, kPW - 1) * MP_PBATCH]);
+        int nw = w0 + 2;
+        const bool all_plain = __all(!slp || plain2);
+        for (int32_t k = 0; k < chunk; ++k) {  // wave-uniform trip count
+            const int32_t t = t0 + k;
             uint64_t mm;
             if (all_plain) {
                 const uint64_t x = G ^ code2;
@@ -480,10 +504,10 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
                 mm = ~((nhi & nlo & Q0) | (nhi & glo & Q1) | (ghi & nlo & Q2) | (ghi & glo & Q3)) & in2;
             }
             const bool hit = t >= ta && t <= tb && !(mm & prot2) && __popcll(mm) <= a.N;
-            stage_try_hit(a, S, lane, hit, gk, rk, t - lo);
+            stage_try_hit(a, S, lane, hit, sgk, srk, t - slo);
             G = (G << 2) | (F >> 62);
             F <<= 2;
-            if ((t & 31) == 31) {  // the next 32 bases
+            if ((k & 31) == 31) {  // the next 32 bases
                 const int w = min(nw, kPW - 2);
                 F = fun(sj[w * MP_PBATCH], sj[(w + 1) * MP_PBATCH]);
                 ++nw;

@@ -9,6 +9,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
   3   level 1, the list and the level-2 loads (consumed, nothing more)
   30  no super-step loop (launch, LDS staging, statistics)
   31  no LDS staging and no loop
+  50  pair_kernel without the lane-parallel try loop
+  51  pair_kernel without any try (prologue, primer-1 compare and staging only)
 """
 import os
 import shutil
@@ -20,6 +22,9 @@ _LOOP = ("    while (ss < n_supers) {\n        const SeqSpan sp = pf;\n        c
          "        const uint32_t n = pf_n;\n        SuperRegs R;")
 _STAGE = ("    for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)\n"
           "        reinterpret_cast<uint4*>(s_lf)[i] = reinterpret_cast<const uint4*>(a.lfilt)[i];\n")
+
+_LP = "    if (__any(lp)) {\n"
+_TODO = "    uint64_t todo = __ballot(keep && !lp);\n"
 
 VARIANTS = {
     1: [(_L1, "            if constexpr (kMode == 1) {  // ablation 1\n"
@@ -33,6 +38,8 @@ VARIANTS = {
               "                r0 += kSeedQR;\n                continue;\n")],
     30: [(_LOOP, "    ss = n_supers;  // ablation 30\n")],
     31: [(_LOOP, "    ss = n_supers;  // ablation 31\n"), (_STAGE, "    if (false)  // ablation 31\n")],
+    50: [(_LP, "    if (false)  // ablation 50\n")],
+    51: [(_LP, "    if (false)  // ablation 51\n"), (_TODO, "    keep = false;  // ablation 51\n")],
 }
 
 
