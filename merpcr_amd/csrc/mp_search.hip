@@ -1981,8 +1981,11 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     // pull the rest from the XCD's own counter (8 counters 256 B apart, ~1.3k atomics each).
     {
         // at least MP_PAIR_MINB survivors per batch (c2, 30k survivors: minimum 4, 16, 32, 64
-        // -> 0.049, 0.047, 0.050, 0.057 ms)
-        const uint32_t db = (uint32_t)umax64(MP_PAIR_MINB, umin64(MP_PDYN_BATCH, (n_surv + waves - 1) / waves));
+        // -> 0.049, 0.047, 0.050, 0.057 ms); at most 32 while there are fewer than 128 per
+        // wave (batches of 32 halve their try loop over two lane groups: c3 pair 0.111 ->
+        // 0.099 ms; c4, 650 per wave, is faster with 64: 0.80 vs 0.83 ms)
+        const uint64_t per_wave = (n_surv + waves - 1) / waves;
+        const uint32_t db = (uint32_t)umax64(MP_PAIR_MINB, umin64(per_wave < 128 ? 32 : MP_PDYN_BATCH, per_wave));
         const uint64_t nbat = (n_surv + db - 1) / db;
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
