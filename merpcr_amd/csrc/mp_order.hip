@@ -50,38 +50,68 @@ __global__ void bucket_hist(const uint64_t* __restrict__ hi, const uint64_t* __r
     }
 }
 
-// exclusive scan of the bucket counts (one 1024-thread workgroup, <= 64 buckets per
-// thread held in registers: one load round trip); cursor = offset
+// exclusive scan of the bucket counts (one 1024-thread workgroup); cursor = offset.  The
+// counts pass through LDS in tiles of kOffTile: coalesced loads and stores, 8 consecutive
+// counts per thread inside a tile, a wave shuffle scan and one LDS word per wave.  (Holding 64
+// consecutive counts per thread in registers made every load and store a 64-line gather: c4's
+// 65,536 buckets took 80 us.)
+constexpr uint32_t kOffTile = 8192;
 __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restrict__ cnt, uint32_t nb,
                                                        uint32_t* __restrict__ off, uint32_t* __restrict__ cursor) {
-    __shared__ uint32_t s_part[1024];
-    const uint32_t per = (nb + 1023) / 1024;  // <= 64 (nb <= 2^16)
-    const uint32_t b0 = threadIdx.x * per;
-    uint32_t v[64];
-    uint32_t sum = 0;
+    __shared__ uint4 s_v4[kOffTile / 4];
+    __shared__ uint32_t s_w[16];
+    uint32_t* s_v = reinterpret_cast<uint32_t*>(s_v4);
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += kOffTile) {
 #pragma unroll
-    for (uint32_t j = 0; j < 64; ++j) {
-        v[j] = j < per && b0 + j < nb ? cnt[b0 + j] : 0u;
-        sum += v[j];
-    }
-    s_part[threadIdx.x] = sum;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t x = threadIdx.x >= o ? s_part[threadIdx.x - o] : 0u;
-        __syncthreads();
-        s_part[threadIdx.x] += x;
-        __syncthreads();
-    }
-    uint32_t run = s_part[threadIdx.x] - sum;
-#pragma unroll
-    for (uint32_t j = 0; j < 64; ++j) {
-        if (j < per && b0 + j < nb) {
-            off[b0 + j] = run;
-            cursor[b0 + j] = run;
+        for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
+            const uint32_t i = j * 1024 + t;
+            s_v[i] = base + i < nb ? cnt[base + i] : 0u;
         }
-        run += v[j];
+        __syncthreads();
+        uint4 q0 = s_v4[2 * t], q1 = s_v4[2 * t + 1];
+        const uint32_t sum = q0.x + q0.y + q0.z + q0.w + q1.x + q1.y + q1.z + q1.w;
+        uint32_t x = sum;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if ((int)lane >= o) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint32_t wpre = 0, tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t sw = s_w[k];
+            wpre += k < w ? sw : 0u;
+            tot += sw;
+        }
+        uint32_t run = carry + wpre + x - sum, v;
+        v = q0.x; q0.x = run; run += v;
+        v = q0.y; q0.y = run; run += v;
+        v = q0.z; q0.z = run; run += v;
+        v = q0.w; q0.w = run; run += v;
+        v = q1.x; q1.x = run; run += v;
+        v = q1.y; q1.y = run; run += v;
+        v = q1.z; q1.z = run; run += v;
+        q1.w = run;
+        s_v4[2 * t] = q0;
+        s_v4[2 * t + 1] = q1;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
+            const uint32_t i = j * 1024 + t;
+            if (base + i < nb) {
+                const uint32_t o = s_v[i];
+                off[base + i] = o;
+                cursor[base + i] = o;
+            }
+        }
+        carry += tot;
+        __syncthreads();  // s_v and s_w are rewritten by the next tile
     }
-    if (threadIdx.x == 1023) off[nb] = s_part[1023];
+    if (t == 0) off[nb] = carry;
 }
 
 __global__ void bucket_scatter(const uint64_t* __restrict__ keys, const unsigned long long* __restrict__ counters,
@@ -103,71 +133,104 @@ __global__ void bucket_scatter(const uint64_t* __restrict__ keys, const unsigned
     }
 }
 
-// One workgroup per bucket: the keys (unique: one hit per (k, record, try)) are ranked by
-// counting the smaller ones, and each is decoded as decode_kernel does.
+// The decoded record of one key, written at its sorted slot (as decode_kernel does).
+__device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits, unsigned low_bits,
+                                  const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
+                                  uint32_t n_seq, const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
+                                  mp_hit* __restrict__ out) {
+    const uint64_t gk = key >> low_bits;
+    const uint32_t rank = (uint32_t)((key & ((1ull << low_bits) - 1ull)) >> try_bits);
+    const uint32_t tr = (uint32_t)(key & ((1ull << try_bits) - 1ull));
+    uint32_t a = 0, b = n_seq;  // last sequence with base <= gk
+    while (b - a > 1) {
+        const uint32_t mid = (a + b) >> 1;
+        if (seq_base[mid] <= gk) a = mid;
+        else b = mid;
+    }
+    const uint64_t k = gk - seq_base[a];
+    const uint32_t rec = inv_rank[rank];
+    const uint64_t len = seq_len[a];
+    const uint64_t size = recs[rec].size;
+    const uint64_t e = size > len - k ? len - k : size;
+    mp_hit h;
+    h.pos1 = k;
+    h.pos2 = (uint64_t)((int64_t)(k + e) - 1 + try_offset(tr));
+    h.seq = a;
+    h.rec = rec;
+    out[slot] = h;
+}
+
+// kBucketsPerBlock buckets per 256-thread workgroup.  When none of them holds more than 64
+// keys (the common case: ~32 per bucket at capacity) every wave ranks its own bucket's keys
+// (unique: one hit per (k, record, try)) by counting the smaller ones over shuffles.  Otherwise
+// the workgroup takes the buckets one after another: rank by counting through LDS up to 256
+// keys, bitonic sort in LDS up to kSortCap.  (One workgroup per bucket left c4's 65,536
+// workgroups of ~24 keys dispatch-bound: 94 us.)
+constexpr uint32_t kBucketsPerBlock = 4;
 __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
-                                                          unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
+                                                          uint32_t nb, unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
                                                           const uint64_t* __restrict__ seq_len, uint32_t n_seq,
                                                           const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
                                                           mp_hit* __restrict__ out, unsigned long long* __restrict__ counters) {
     __shared__ uint64_t s_k[kSortCap];
-    const uint32_t start = off[blockIdx.x], m = off[blockIdx.x + 1] - start;
-    if (m == 0) return;
-    if (m > kSortCap) {
-        if (threadIdx.x == 0) atomicOr(&counters[kSortOverflow], 1ull);
-        return;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t b0 = blockIdx.x * kBucketsPerBlock;
+    {
+        const bool in = b0 + wave < nb;  // nb < kBucketsPerBlock under a forced sort_bucket_bits
+        const uint32_t start = in ? off[b0 + wave] : 0u, m = in ? off[b0 + wave + 1] - start : 0u;
+        if (!__syncthreads_or(m > 64)) {
+            if (m == 0) return;  // wave-uniform; no barrier follows on this path
+            const uint64_t key = lane < m ? keys[start + lane] : ~0ull;
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < m; ++j) {
+                const uint64_t kj = __shfl(key, (int)j, 64);
+                r += kj < key || (kj == key && j < lane);  // ties: stable
+            }
+            if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+            return;
+        }
     }
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
-    const bool small = m <= 256;  // rank by counting; larger buckets: bitonic sort in LDS
-    if (!small) {
-        uint32_t P = 512;
-        while (P < m) P <<= 1;
-        for (uint32_t i = m + threadIdx.x; i < P; i += blockDim.x) s_k[i] = ~0ull;
-        __syncthreads();
-        for (uint32_t k = 2; k <= P; k <<= 1) {
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-                    const uint32_t ij = i ^ j;
-                    if (ij > i) {
-                        const uint64_t x = s_k[i], y = s_k[ij];
-                        if ((x > y) == ((i & k) == 0)) {
-                            s_k[i] = y;
-                            s_k[ij] = x;
+    for (uint32_t q = 0; q < kBucketsPerBlock && b0 + q < nb; ++q) {  // block-uniform loop
+        const uint32_t start = off[b0 + q], m = off[b0 + q + 1] - start;
+        if (m == 0) continue;
+        if (m > kSortCap) {
+            if (threadIdx.x == 0) atomicOr(&counters[kSortOverflow], 1ull);
+            continue;
+        }
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
+        const bool small = m <= 256;  // rank by counting; larger buckets: bitonic sort in LDS
+        if (!small) {
+            uint32_t P = 512;
+            while (P < m) P <<= 1;
+            for (uint32_t i = m + threadIdx.x; i < P; i += blockDim.x) s_k[i] = ~0ull;
+            __syncthreads();
+            for (uint32_t k = 2; k <= P; k <<= 1) {
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
+                        const uint32_t ij = i ^ j;
+                        if (ij > i) {
+                            const uint64_t x = s_k[i], y = s_k[ij];
+                            if ((x > y) == ((i & k) == 0)) {
+                                s_k[i] = y;
+                                s_k[ij] = x;
+                            }
                         }
                     }
+                    __syncthreads();
                 }
-                __syncthreads();
             }
         }
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-        const uint64_t key = s_k[i];
-        uint32_t r = i;
-        if (small) {
-            r = 0;
-            for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+            const uint64_t key = s_k[i];
+            uint32_t r = i;
+            if (small) {
+                r = 0;
+                for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
+            }
+            decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
         }
-        const uint64_t gk = key >> low_bits;
-        const uint32_t rank = (uint32_t)((key & ((1ull << low_bits) - 1ull)) >> try_bits);
-        const uint32_t tr = (uint32_t)(key & ((1ull << try_bits) - 1ull));
-        uint32_t a = 0, b = n_seq;  // last sequence with base <= gk
-        while (b - a > 1) {
-            const uint32_t mid = (a + b) >> 1;
-            if (seq_base[mid] <= gk) a = mid;
-            else b = mid;
-        }
-        const uint64_t k = gk - seq_base[a];
-        const uint32_t rec = inv_rank[rank];
-        const uint64_t len = seq_len[a];
-        const uint64_t size = recs[rec].size;
-        const uint64_t e = size > len - k ? len - k : size;
-        mp_hit h;
-        h.pos1 = k;
-        h.pos2 = (uint64_t)((int64_t)(k + e) - 1 + try_offset(tr));
-        h.seq = a;
-        h.rec = rec;
-        out[start + r] = h;
+        __syncthreads();  // s_k is refilled by the next bucket
     }
 }
 
@@ -220,7 +283,8 @@ int sort_hits_device(Search* s, hipStream_t st, bool fused) {
                        s->tmp_hi);
     MP_HIP_CHECK(hipGetLastError());
     const Genome* g = s->genome;
-    hipLaunchKernelGGL(bucket_sort_decode, dim3(P.nb), dim3(256), 0, st, s->tmp_hi, off, P.try_bits, P.low_bits,
+    hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
+                       s->tmp_hi, off, P.nb, P.try_bits, P.low_bits,
                        g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->counters);
     MP_HIP_CHECK(hipGetLastError());
     return MP_OK;
