@@ -160,11 +160,11 @@ __device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits
     out[slot] = h;
 }
 
-// kBucketsPerBlock buckets per 256-thread workgroup.  When none of them holds more than 64
-// keys (the common case: ~32 per bucket at capacity) every wave ranks its own bucket's keys
-// (unique: one hit per (k, record, try)) by counting the smaller ones over shuffles.  Otherwise
-// the workgroup takes the buckets one after another: rank by counting through LDS up to 256
-// keys, bitonic sort in LDS up to kSortCap.  (One workgroup per bucket left c4's 65,536
+// kBucketsPerBlock buckets per 256-thread workgroup.  A bucket of at most 64 keys (the common
+// case: ~32 per bucket at capacity) is ranked by its own wave, counting the smaller keys
+// (unique: one hit per (k, record, try)) over shuffles.  The workgroup then takes the larger
+// ones one after another: rank by counting through LDS up to 256 keys, bitonic sort in LDS up
+// to kSortCap.  (One workgroup per bucket left c4's 65,536
 // workgroups of ~24 keys dispatch-bound: 94 us.)
 constexpr uint32_t kBucketsPerBlock = 4;
 __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
@@ -178,8 +178,7 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
     {
         const bool in = b0 + wave < nb;  // nb < kBucketsPerBlock under a forced sort_bucket_bits
         const uint32_t start = in ? off[b0 + wave] : 0u, m = in ? off[b0 + wave + 1] - start : 0u;
-        if (!__syncthreads_or(m > 64)) {
-            if (m == 0) return;  // wave-uniform; no barrier follows on this path
+        if (m > 0 && m <= 64) {  // wave-uniform; no barrier inside
             const uint64_t key = lane < m ? keys[start + lane] : ~0ull;
             uint32_t r = 0;
             for (uint32_t j = 0; j < m; ++j) {
@@ -187,12 +186,12 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
                 r += kj < key || (kj == key && j < lane);  // ties: stable
             }
             if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
-            return;
         }
+        if (!__syncthreads_or(m > 64)) return;  // every wave reaches this barrier
     }
     for (uint32_t q = 0; q < kBucketsPerBlock && b0 + q < nb; ++q) {  // block-uniform loop
         const uint32_t start = off[b0 + q], m = off[b0 + q + 1] - start;
-        if (m == 0) continue;
+        if (m <= 64) continue;  // done by its wave above
         if (m > kSortCap) {
             if (threadIdx.x == 0) atomicOr(&counters[kSortOverflow], 1ull);
             continue;
