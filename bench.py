@@ -167,6 +167,63 @@ def reference_model(table, prm, buf, offs, lens, cores: int, budget_s: float):
             "one_core_mbps": round(rate1 / 1e6, 3)}
 
 
+def in_range(hits, rng):
+    """Mask of the hits whose (seq, pos1) lies in the owned range (seq_begin, seq_end, k_begin, k_end)."""
+    sb, se, kb, ke = rng
+    q, k = hits["seq"].astype(np.int64), hits["pos1"].astype(np.int64)
+    after_lo = (q > sb) | ((q == sb) & (k >= kb))
+    before_hi = (q < se) | ((q == se) & (k < ke))
+    return after_lo & before_hi
+
+
+def parity_distributed(table, genome, search, rng, got, world, rank, weak, n_seq, stream):
+    """Correctness gate of a sharded or multi-rank run (the oracle gate covers N=1):
+    * every rank: its own sorted list (seq shifted as the gather shifts it) is hashed, and
+      rank 0 compares each rank's segment of the gathered list with that rank's hash;
+    * strong scaling / --shard-of: rank 0's single-device search of the WHOLE genome
+      (itself checked against the C oracle by the N=1 bench) must equal the gathered
+      list, or, for a shard, its owned slice."""
+    import hashlib
+    from merpcr_amd import _native
+    mine = search.fetch(search.last_hits(), stream).copy()
+    if weak:
+        mine["seq"] += n_seq * rank
+    digest = hashlib.sha256(mine.tobytes()).hexdigest()
+    ok, why = True, []
+    if world > 1:
+        import torch.distributed as dist
+        every = [None] * world
+        dist.all_gather_object(every, (len(mine), digest))
+        if rank == 0:
+            off = 0
+            for r, (n, d) in enumerate(every):
+                seg = got[off:off + n] if got is not None else None
+                if seg is None or len(seg) != n or hashlib.sha256(seg.tobytes()).hexdigest() != d:
+                    ok = False
+                    why.append(f"rank {r} segment differs")
+                off += n
+            if got is not None and off != len(got):
+                ok = False
+                why.append(f"gathered {len(got)} hits, ranks hold {off}")
+    if rank == 0 and not weak:
+        full_s = _native.Search(table, genome)
+        full = full_s.fetch(full_s.run(None, stream), stream)
+        full_s.close()
+        if world > 1:
+            if got is None or got.tobytes() != full.tobytes():
+                ok = False
+                why.append(f"gathered list ({None if got is None else len(got)}) != single-device "
+                           f"whole-genome list ({len(full)})")
+        if rng is not None and world == 1:
+            want = full[in_range(full, rng)]
+            if mine.tobytes() != want.tobytes():
+                ok = False
+                why.append(f"shard list ({len(mine)}) != the owned slice of the whole-genome list ({len(want)})")
+    return {"ok": ok, "checked": ("gathered list vs per-rank hashes" if world > 1 else "") +
+            ("" if weak else (" + " if world > 1 else "") + "vs rank 0's single-device whole-genome search"),
+            "problems": why}
+
+
 def end_to_end(eng, table, names, lens, buf, offs, device, stream):
     """One pass from host bytes to output text (SURVEY 8d t_e2e), not the metric:
     H2D + 2-bit pack + exception index (mp_genome_put/seal), search, hit fetch and the
@@ -257,6 +314,8 @@ def main():
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="diagnostic: every rank on device 0 (rehearses the N-rank path, RCCL included, on a "
                          "one-GPU box); the JSON line is then not the metric")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one search handle: every step waits for the previous one (no run queued ahead)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time only rank 0's owned range of an N-way split on this one GPU "
                          "(no collective); the JSON line is then not the metric")
@@ -315,55 +374,122 @@ def main():
         f"range={rng}")
 
     gathered = None
+    last_gloo = [None]  # rehearsal: the host-gathered bytes of the last step
     if world > 1:
         gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)  # rank 0's gather buffer
+    shift = len(lens) * rank if weak else 0
 
-    def step():
+    # Steps are pipelined two deep (mp_search_enqueue / mp_search_complete on two search
+    # handles over the same resident table and genome): step i+1's kernels are queued before
+    # the host waits for step i, so the host turnaround between runs is off the GPU's path.
+    # With N > 1 each completed step's RCCL gather runs on a stream of its own, and the
+    # handle's next run waits (on the device) for its gather to have sent the hits.
+    nbuf = 1 if args.no_pipeline else 2
+    handles = [search] + [_native.Search(table, genome) for _ in range(nbuf - 1)]
+    gstream = torch.cuda.Stream(device=dev) if comm is not None else None
+    gdone = [None] * nbuf
+    scan_ms = []
+
+    def gather(h):
+        """Every rank's hits of handle h's completed run to rank 0; the job's hit count."""
         nonlocal gathered
-        n = search.run(rng, stream)
-        if world > 1 and comm is None:  # rehearsal: host gather over gloo
+        n = h.last_hits()
+        if world == 1:
+            return n, None
+        if comm is None:  # rehearsal: host gather over gloo
             from merpcr_amd.dist import gather_hits as gloo_gather
-            mine = search.fetch(n, stream)
+            mine = h.fetch(n, stream)
             buf_h = torch.from_numpy(np.frombuffer(mine.tobytes() + b"\0" * HIT_BYTES, dtype=np.uint8).copy())
-            got = gloo_gather(buf_h, n, seq_base=len(lens) * rank if weak else 0)
-            return got.numel() // HIT_BYTES if rank == 0 else n
-        if world > 1:
+            got = gloo_gather(buf_h, n, seq_base=shift)
+            last_gloo[0] = got
+            return (got.numel() // HIT_BYTES if rank == 0 else n), None
+        cap = gathered.numel() // HIT_BYTES if rank == 0 else 0
+        try:
+            n = comm.gather_hits(h, gathered.data_ptr(), cap, shift, gstream.cuda_stream)
+        except _native.NativeError as e:
+            if e.code != _native.MP_E_CAP:
+                raise
+            # rank 0's buffer too small: every rank got MP_E_CAP; grow and gather again
+            gstream.synchronize()
+            gathered = torch.empty(comm.last_total * 2 * HIT_BYTES, dtype=torch.uint8, device=dev)
             cap = gathered.numel() // HIT_BYTES if rank == 0 else 0
-            try:
-                n = comm.gather_hits(search, gathered.data_ptr(), cap, len(lens) * rank if weak else 0, stream)
-            except _native.NativeError as e:
-                if e.code != _native.MP_E_CAP:
-                    raise
-                # rank 0's buffer too small: every rank got MP_E_CAP; grow and gather again
-                need = comm.last_total
-                gathered = torch.empty(need * 2 * HIT_BYTES, dtype=torch.uint8, device=dev)
-                cap = gathered.numel() // HIT_BYTES if rank == 0 else 0
-                n = comm.gather_hits(search, gathered.data_ptr(), cap, len(lens) * rank if weak else 0, stream)
+            n = comm.gather_hits(h, gathered.data_ptr(), cap, shift, gstream.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(gstream)
+        return n, ev
+
+    def finish(j):
+        h = handles[j]
+        h.complete()
+        sm = h.last_stats()["scan_ms"]
+        if sm >= 0:
+            scan_ms.append(sm)
+        n, gdone[j] = gather(h)
         return n
 
-    # the timed steps record only the scan kernel's events (HIP events on the launch stream,
-    # for the roofline); the stage times come from one more run with every stage timed
-    search.set_stage_timing(False)
-    for _ in range(args.warmup):
-        step()
+    def run_steps(k):
+        """k steps, pipelined; returns the last step's job-wide hit count."""
+        pend, total = None, 0
+        cur = torch.cuda.current_stream()
+        for i in range(k):
+            j = i % nbuf
+            if pend == j:
+                total = finish(pend)
+                pend = None
+            if gdone[j] is not None:  # its previous run's hits are still being sent
+                cur.wait_event(gdone[j])
+                gdone[j] = None
+            handles[j].enqueue(rng, stream)
+            if pend is not None:
+                total = finish(pend)
+            pend = j
+        if pend is not None:
+            total = finish(pend)
+        return total
+
+    # Timed steps: no per-stage events (each idles the GPU ~6 us).  At N = 1 the scan kernel's
+    # own two events stay (roofline.achieved, HIP events on the launch stream, every timed
+    # step); sharded and multi-rank runs time the scan in the untimed step after them.
+    scan_in_timed = world == 1 and args.shard_of <= 1
+    for h in handles:
+        h.set_stage_timing(False)
+        h.set_scan_timing(scan_in_timed)
+    run_steps(args.warmup)
+    scan_ms.clear()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    scan_ms, nhits = [], 0
-    for _ in range(args.steps):
-        nhits = step()
-        scan_ms.append(search.last_stats()["scan_ms"])
+    nhits = run_steps(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    search.set_stage_timing(True)  # untimed: the stage breakdown of one more step
-    step()
+    timed_scan_ms = list(scan_ms)
+    # untimed: one more step with every stage timed (the stage breakdown; the scan time too
+    # when the timed steps carried no events)
+    search.set_stage_timing(True)
+    search.set_scan_timing(True)
+    scan_ms.clear()
+    for j in range(1, nbuf):
+        if gdone[j] is not None:
+            torch.cuda.current_stream().wait_event(gdone[j])
+            gdone[j] = None
+    gdone_keep = gdone[0]
+    if gdone_keep is not None:
+        torch.cuda.current_stream().wait_event(gdone_keep)
+        gdone[0] = None
+    search.enqueue(rng, stream)
+    finish(0)
     torch.cuda.synchronize()
+    if not timed_scan_ms:
+        timed_scan_ms = list(scan_ms)
+    scan_ms = timed_scan_ms
     stages = search.last_stats()
     tail_ms, pair_ms, order_ms = [stages["tail_ms"]], [stages["pair_ms"]], [stages["order_ms"]]
     st = search.last_stats()
+    for h in handles[1:]:
+        h.close()
     if world > 1:
         mx = torch.tensor([elapsed], dtype=torch.float64)
         torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
@@ -374,6 +500,13 @@ def main():
     else:
         tot_bases = float(sum(lens))
     tot_hits = float(nhits)  # after the gather: every rank's hits (N > 1)
+    dist_check = None
+    if world > 1 or args.shard_of > 1:
+        got = None
+        if world > 1 and rank == 0:
+            raw = (gathered[:nhits * HIT_BYTES] if comm is not None else last_gloo[0]).cpu().numpy()
+            got = np.frombuffer(raw.tobytes(), dtype=_native.HIT_DTYPE)
+        dist_check = parity_distributed(table, genome, search, rng, got, world, rank, weak, len(lens), stream)
     if rank != 0:
         if comm is not None:
             comm.close()
@@ -426,12 +559,19 @@ def main():
                      "alg_bytes_per_launch": int(alg_bytes),
                      "issue": (dict(issue_bound(pmc), source=f"profiles/{pmc_tag}_pmc.json") if pmc else None)},
         "setup_s": round(setup_s, 2),
+        "pipeline": (f"{nbuf} search handles: step i+1 enqueued before the host waits for step i "
+                     "(mp_search_enqueue/complete)" if nbuf > 1 else "none: each step waits for the previous"),
+        "scan_timing": ("HIP events around the scan kernel in every timed step" if scan_in_timed else
+                        "HIP events around the scan kernel in one untimed step after the timed ones"),
     }
     if args.shard_of > 1:
         out["diagnostic"] = f"rank 0 of a {args.shard_of}-way owned-range split, alone on one GPU (not the metric)"
     if args.rehearse_one_gpu:
         out["diagnostic"] = f"{world} ranks sharing device 0 (rehearsal of the N-rank path, not the metric)"
     parity_ok = True
+    if world > 1 or args.shard_of > 1:
+        out["parity_distributed"] = dist_check
+        parity_ok = dist_check["ok"]
     if world == 1 and not args.no_e2e:
         out["e2e"] = end_to_end(eng, table, names, lens, buf, offs, local, stream)
     if world == 1 and args.e2e_file:

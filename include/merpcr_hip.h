@@ -124,6 +124,7 @@ int mp_search_create(void* table, void* genome, void** search_out);
 #define MP_SORT_AUTO 0     /* device bucket sort when the order key fits 64 bits */
 #define MP_SORT_RADIX64 1  /* rocPRIM radix sort of the packed 64-bit key */
 #define MP_SORT_RADIX128 2 /* two stable rocPRIM passes over the 128-bit key */
+#define MP_SORT_SCATTER 3  /* device bucket sort starting from the scatter form (order mode 1) */
 typedef struct mp_search_options {
     int32_t tails;              /* MP_TAILS_* */
     int32_t no_defer;           /* 1: the ranked drain tests full-head buckets itself */
@@ -143,9 +144,19 @@ int mp_search_set_options(void* search, const mp_search_options* opt);
 /* Per-stage timing (tail, pair and order events; default on).  Off, a run records only the
  * scan kernel's two events: each event between two kernels idles the GPU ~6 us. */
 int mp_search_set_stage_timing(void* search, int32_t on);
+/* Scan kernel timing (its two HIP events, default on).  Off, mp_search_last_stats reports
+ * scan_ms = -1 and the run carries no event before the scan and none after it. */
+int mp_search_set_scan_timing(void* search, int32_t on);
 /* Scan, verify, pair-check and sort.  *n_hits receives the number of hits of
- * the owned range (range NULL = whole genome).  Synchronises `stream`. */
+ * the owned range (range NULL = whole genome).  Waits for the run (= enqueue + complete). */
 int mp_search_run(void* search, const mp_range* range, void* stream, uint64_t* n_hits);
+/* The asynchronous form: enqueue every kernel of a run on `stream` and return without
+ * waiting (the first run of a range uploads its spans).  Other work -- another search
+ * handle's run, a collective -- may be enqueued before mp_search_complete, which waits for
+ * it, regrows and reruns a list that overflowed, and reports the hit count.  One run per
+ * handle may be pending; the handle's hit buffers belong to it until completed. */
+int mp_search_enqueue(void* search, const mp_range* range, void* stream);
+int mp_search_complete(void* search, uint64_t* n_hits);
 /* Copy the sorted hits of the last run to host memory (cap entries). */
 int mp_search_fetch(void* search, mp_hit* out, uint64_t cap, void* stream);
 /* Copy the sorted hits of the last run into DEVICE memory on the search's GPU

@@ -31,7 +31,8 @@ EXPORTS = (
     "mp_table_create", "mp_table_stats", "mp_table_destroy",
     "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
     "mp_genome_stats", "mp_genome_reset", "mp_genome_destroy",
-    "mp_search_create", "mp_search_set_options", "mp_search_set_stage_timing", "mp_search_run", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
+    "mp_search_create", "mp_search_set_options", "mp_search_set_stage_timing", "mp_search_set_scan_timing", "mp_search_run",
+    "mp_search_enqueue", "mp_search_complete", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
     "mp_search_last_stats", "mp_search_regrowths", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
     "mp_multi_create", "mp_multi_genome", "mp_multi_put", "mp_multi_seal", "mp_multi_run", "mp_multi_fetch",
     "mp_multi_device_search", "mp_multi_destroy",
@@ -53,7 +54,7 @@ class MPRange(ctypes.Structure):
 
 
 MP_TAILS = {"auto": 0, "inline": 1, "kernel": 2}
-MP_SORT = {"auto": 0, "radix64": 1, "radix128": 2}
+MP_SORT = {"auto": 0, "radix64": 1, "radix128": 2, "scatter": 3}
 
 
 class MPSearchOptions(ctypes.Structure):
@@ -98,6 +99,9 @@ def _sig(lib):
     lib.mp_search_set_options.argtypes = [P, POINTER(MPSearchOptions)]
     lib.mp_search_set_stage_timing.argtypes = [P, c_int32]
     lib.mp_search_run.argtypes = [P, POINTER(MPRange), P, u64p]
+    lib.mp_search_set_scan_timing.argtypes = [P, c_int32]
+    lib.mp_search_enqueue.argtypes = [P, POINTER(MPRange), P]
+    lib.mp_search_complete.argtypes = [P, u64p]
     lib.mp_search_regrowths.argtypes = [P, u64p]
     lib.mp_search_fetch.argtypes = [P, P, c_uint64, P]
     lib.mp_search_fetch_device.argtypes = [P, P, c_uint64, P]
@@ -294,6 +298,22 @@ class Search:
         """Events around the tail, pair and order stages too (default on; off saves ~6 us
         per stage and run, and last_stats then reports those stages as -1)."""
         check(lib().mp_search_set_stage_timing(self._h, 1 if on else 0))
+
+    def set_scan_timing(self, on: bool):
+        """The scan kernel's own two events (default on; off, last_stats reports scan_ms -1)."""
+        check(lib().mp_search_set_scan_timing(self._h, 1 if on else 0))
+
+    def enqueue(self, rng=None, stream=None):
+        """Enqueue a whole run on `stream` without waiting (mp_search_enqueue); complete()
+        waits for it.  Lets the caller queue the next run (another handle) first."""
+        r = MPRange(*rng) if rng is not None else None
+        check(lib().mp_search_enqueue(self._h, ctypes.byref(r) if r is not None else None, c_void_p(stream or 0)))
+
+    def complete(self) -> int:
+        n = c_uint64(0)
+        check(lib().mp_search_complete(self._h, ctypes.byref(n)))
+        self._last_n = n.value
+        return n.value
 
     def regrowths(self) -> int:
         n = c_uint64()

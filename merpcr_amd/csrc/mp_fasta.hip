@@ -315,22 +315,14 @@ static size_t count_kept(const uint8_t* s, const uint8_t* e) {  // ASCII text
     return c;
 }
 
-// 1 = use the streaming reader (mmap failed); MP_OK / errors otherwise.
-static int load_parallel(const char* path, Fasta* f, int threads) {
-    const int fd = ::open(path, O_RDONLY);
-    if (fd < 0) return fail(MP_E_IO, std::string("cannot open FASTA file: ") + path);
+// 1 = use the streaming reader on the same descriptor (not a regular file, size 0 -- pipes,
+// /dev/stdin and /proc files report that -- or mmap failed); MP_OK / errors otherwise.
+// The caller owns fd.
+static int load_parallel(int fd, Fasta* f, int threads) {
     struct stat sb;
-    if (fstat(fd, &sb) != 0) {
-        ::close(fd);
-        return 1;
-    }
+    if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_size == 0) return 1;
     const size_t n = (size_t)sb.st_size;
-    if (n == 0) {
-        ::close(fd);
-        return MP_OK;
-    }
     void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
-    ::close(fd);
     if (m == MAP_FAILED) return 1;
     (void)madvise(m, n, MADV_SEQUENTIAL);
     const uint8_t* d = (const uint8_t*)m;
@@ -471,6 +463,8 @@ static int load_parallel(const char* path, Fasta* f, int threads) {
     return MP_OK;
 }
 
+static int load_stream(FILE* fp, const char* path, uint64_t chunk_bytes, void** out);
+
 MP_EXPORT int mp_fasta_load(const char* path, void** out) { return mp_fasta_load_parallel(path, 0, out); }
 
 MP_EXPORT int mp_fasta_load_parallel(const char* path, int32_t threads, void** out) {
@@ -478,16 +472,28 @@ MP_EXPORT int mp_fasta_load_parallel(const char* path, int32_t threads, void** o
     *out = nullptr;
     Fasta* f = new (std::nothrow) Fasta();
     if (!f) return fail(MP_E_NOMEM, "mp_fasta_load: out of host memory");
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) {
+        delete f;
+        return fail(MP_E_IO, std::string("cannot open FASTA file: ") + path);
+    }
     int rc;
     try {
-        rc = load_parallel(path, f, threads);
+        rc = load_parallel(fd, f, threads);
     } catch (const std::bad_alloc&) {
         rc = fail(MP_E_NOMEM, "mp_fasta_load: out of host memory");
     }
-    if (rc == 1) {  // not mappable: the streaming reader
+    if (rc == 1) {  // not mappable: the streaming reader, on the descriptor already open (a pipe
+                    // cannot be opened twice)
         delete f;
-        return mp_fasta_load_chunked(path, 0, out);
+        FILE* fp = fdopen(fd, "rb");
+        if (!fp) {
+            ::close(fd);
+            return fail(MP_E_IO, std::string("cannot open FASTA file: ") + path);
+        }
+        return load_stream(fp, path, 0, out);
     }
+    ::close(fd);
     if (rc) {
         delete f;
         return rc;
@@ -501,9 +507,14 @@ MP_EXPORT int mp_fasta_load_chunked(const char* path, uint64_t chunk_bytes, void
     if (!path || !out) return fail(MP_E_ARG, "mp_fasta_load: null pointer");
     if (chunk_bytes && chunk_bytes < 4) return fail(MP_E_ARG, "mp_fasta_load: chunk_bytes must be >= 4");
     *out = nullptr;
-    const size_t chunk = chunk_bytes ? (size_t)chunk_bytes : (size_t)64 << 20;
     FILE* fp = std::fopen(path, "rb");
     if (!fp) return fail(MP_E_IO, std::string("cannot open FASTA file: ") + path);
+    return load_stream(fp, path, chunk_bytes, out);
+}
+
+// The streaming reader over an open stream, which it closes.
+static int load_stream(FILE* fp, const char* path, uint64_t chunk_bytes, void** out) {
+    const size_t chunk = chunk_bytes ? (size_t)chunk_bytes : (size_t)64 << 20;
     Fasta* f = new (std::nothrow) Fasta();
     int rc = f ? MP_OK : fail(MP_E_NOMEM, "mp_fasta_load: out of host memory");
     if (!rc) {

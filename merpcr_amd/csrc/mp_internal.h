@@ -51,6 +51,13 @@ int fail(int code, const std::string& msg);
                                             hipGetErrorString(_e));            \
     } while (0)
 
+// Wait for an event by polling (hipEventQuery) instead of a blocking synchronisation: a
+// tight spin for the first ~20 us (a search's counter readback is on every step's critical
+// path), then the CPU is yielded between polls.  timeout_s > 0 bounds the wait: it returns
+// hipErrorNotReady when the event has not completed by then (a peer rank that never joins
+// a collective would otherwise hold this thread forever).
+hipError_t poll_event(hipEvent_t ev, double timeout_s = 0.0);
+
 // ---------------------------------------------------------------- constants
 constexpr uint64_t kEven = 0x5555555555555555ull;  // the low bit of every 2-bit slot
 constexpr int kHashedFilterLog2 = 27;               // 16 MiB hashed filter for W >= 14
@@ -194,16 +201,34 @@ struct Search {
     float scan_ms = 0.f, tail_ms = 0.f, pair_ms = 0.f, order_ms = 0.f;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, evt = nullptr;
     uint32_t* bucket = nullptr;  // device sort: bucket counts, offsets, cursors
-    bool sort_crowded = false;   // a device-sort bucket overflowed: later runs go to rocPRIM
+    uint64_t* slots = nullptr;   // order mode 0: every bucket's keys at bucket * slot_cap
+    size_t slots_bytes = 0;
+    // Hit order, sticky per handle and only ever raised (a crowded bucket seen once is
+    // likely seen again): 0 = bucket slots written by pair_kernel + one sort/decode kernel;
+    // 1 = scatter by the fused offsets + per-bucket LDS sort (up to kSortCap keys);
+    // 2 = rocPRIM on the host-known count.  Keys over 64 bits always take 2.
+    int order_mode = 0;
     mp_search_options opt{};     // kernel-path selection (all zero = automatic)
     uint32_t pair_per_cu = 0;    // resident pair_kernel blocks per CU (occupancy query at create)
     uint32_t dense_per_cu = 0;   // resident dense_kernel blocks per CU
     size_t dense_lds = 0;        // dense_kernel dynamic LDS bytes
     uint64_t n_regrowths = 0;    // list regrowths over the handle's life (tests)
     std::vector<SeqSpan> last_spans;        // spans on the device (a rerun of the same range uploads nothing)
-    unsigned long long* h_cnt = nullptr;    // pinned host copy of counters[0..8) (the run's one readback)
-    hipEvent_t evd = nullptr;               // the readback's completion (polled, not slept on)
+    // pinned, device-mapped host words: [0, 8) counters[0..8) written by finish_kernel at
+    // the end of every run (the run's one readback, no copy); [8] staging for a host upload
+    unsigned long long* h_cnt = nullptr;
+    unsigned long long* d_hcnt = nullptr;   // h_cnt as the device sees it
+    hipEvent_t evd = nullptr;               // the run's completion (polled, not slept on)
     bool stage_timing = true;               // events around tail/pair/order too (mp_search_set_stage_timing)
+    bool scan_timing = true;                // the scan kernel's own two events (mp_search_set_scan_timing)
+    bool dirty = false;                     // counters not known to be zero (an abandoned run): memset first
+    // an enqueued run waiting for mp_search_complete
+    bool pending = false;
+    bool pend_empty = false;                // nothing to scan: completes with no hits
+    hipStream_t pend_st = nullptr;
+    uint64_t pend_tiles = 0;                // super-steps of the enqueued run
+    int pend_mode = 0;                      // its order mode
+    alignas(16) unsigned char pend_args[640];  // its ScanArgs (mp_search.hip)
 };
 
 // ---------------------------------------------------------------- device helpers
@@ -354,11 +379,18 @@ bool sort_hits_device_ok(const Search* s);
 struct SortPlan {
     unsigned try_bits = 0, low_bits = 0, shift = 0;
     uint32_t nb = 0;
+    uint32_t slot_cap = 0;  // order mode 0: keys per bucket slot
 };
+constexpr uint32_t kSlotCap = 256;  // order mode 0: bucket slot capacity (~8x the planned mean)
 SortPlan sort_plan(const Search* s);
-// fused: pair_kernel already wrote the packed keys (tmp_lo) and the bucket counts
-int sort_hits_device(Search* s, hipStream_t st, bool fused);  // hit count read on the device, writes s->out
+// pair_kernel already wrote the packed keys (tmp_lo), the bucket counts and (its last block)
+// the bucket offsets/cursors; mode 0: the keys also in their bucket slots.  Hit count read
+// on the device; writes s->out.
+int sort_hits_device(Search* s, hipStream_t st, int mode);
 uint32_t* sort_bucket_counts(Search* s);          // the bucket count array (zeroed by the scan kernels)
+uint32_t* sort_bucket_offsets(Search* s);         // nb + 1 offsets
+uint32_t* sort_bucket_cursors(Search* s);
+int alloc_sort_slots(Search* s, const SortPlan& P);  // mode 0's slot array for plan P
 
 // Raw hits arrive in runs of one bucket (a survivor's tries, a wave's batch of nearby
 // survivors; IUPAC primers over N runs pile thousands on a few positions).  Same-address
@@ -374,6 +406,70 @@ __device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint3
     const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1u : 64u - (uint32_t)__clzll(onm);
     len = end - (uint32_t)lane;  // meaningful on heads only
 }
+// Exclusive scan of nb bucket counts by one 1024-thread workgroup: off[0..nb] (off[nb] =
+// total) and cursor[0..nb) = off.  The counts pass through LDS (s_v4: kOffTile counts) in
+// tiles: coalesced loads and stores, 8 consecutive counts per thread inside a tile, a wave
+// shuffle scan and one LDS word per wave (s_w: 16).  (64 consecutive counts per thread in
+// registers made every access a 64-line gather: c4's 65,536 buckets took 80 us.)  The
+// counts are read at device scope: pair_kernel's last block calls this right after the
+// other blocks' atomics.
+constexpr uint32_t kOffTile = 8192;
+__device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32_t nb, uint32_t* off,
+                                                     uint32_t* cursor, uint4* s_v4, uint32_t* s_w) {
+    uint32_t* s_v = reinterpret_cast<uint32_t*>(s_v4);
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += kOffTile) {
+#pragma unroll
+        for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
+            const uint32_t i = j * 1024 + t;
+            s_v[i] = base + i < nb ? __hip_atomic_load(cnt + base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        }
+        __syncthreads();
+        uint4 q0 = s_v4[2 * t], q1 = s_v4[2 * t + 1];
+        const uint32_t sum = q0.x + q0.y + q0.z + q0.w + q1.x + q1.y + q1.z + q1.w;
+        uint32_t x = sum;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if ((int)lane >= o) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        uint32_t wpre = 0, tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t sw = s_w[k];
+            wpre += k < w ? sw : 0u;
+            tot += sw;
+        }
+        uint32_t run = carry + wpre + x - sum, v;
+        v = q0.x; q0.x = run; run += v;
+        v = q0.y; q0.y = run; run += v;
+        v = q0.z; q0.z = run; run += v;
+        v = q0.w; q0.w = run; run += v;
+        v = q1.x; q1.x = run; run += v;
+        v = q1.y; q1.y = run; run += v;
+        v = q1.z; q1.z = run; run += v;
+        q1.w = run;
+        s_v4[2 * t] = q0;
+        s_v4[2 * t + 1] = q1;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
+            const uint32_t i = j * 1024 + t;
+            if (base + i < nb) {
+                const uint32_t o = s_v[i];
+                off[base + i] = o;
+                cursor[base + i] = o;
+            }
+        }
+        carry += tot;
+        __syncthreads();  // s_v and s_w are rewritten by the next tile
+    }
+    if (t == 0) off[nb] = carry;
+}
+
 int alloc_sort_buckets(Search* s);                // the device sort's bucket arrays (at create)
 constexpr int kSortOverflow = 6;                  // counters[6]: a device-sort bucket overflowed
 int sort_runs(Genome* g, hipStream_t st);

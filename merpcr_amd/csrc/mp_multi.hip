@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -54,6 +55,7 @@ struct Multi {
     std::vector<uint64_t> len;
     mp_hit* all = nullptr;          // gathered hits on dev[0]
     uint64_t all_cap = 0, n_all = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;  // gather timing on dev[0], made once
     float gather_ms = 0.f;
 };
 
@@ -66,9 +68,11 @@ static void free_multi(Multi* m) {
         if (m->gen[i]) mp_genome_destroy(m->gen[i]);
         if (m->st[i]) hipStreamDestroy(m->st[i]);
     }
-    if (m->all) {
+    if (!m->dev.empty()) {
         hipSetDevice(m->dev[0]);
-        hipFree(m->all);
+        if (m->all) hipFree(m->all);
+        if (m->e0) hipEventDestroy(m->e0);
+        if (m->e1) hipEventDestroy(m->e1);
     }
     delete m;
 }
@@ -175,6 +179,9 @@ MP_EXPORT int mp_multi_create(uint32_t n_dev, const int32_t* devices, void* cons
         else if (hipSetDevice(m->dev[d]) != hipSuccess || hipStreamCreateWithFlags(&m->st[d], hipStreamNonBlocking) != hipSuccess)
             rc = fail(MP_E_HIP, "mp_multi_create: stream creation failed");
     }
+    if (!rc && (hipSetDevice(m->dev[0]) != hipSuccess || hipEventCreate(&m->e0) != hipSuccess ||
+                hipEventCreate(&m->e1) != hipSuccess))
+        rc = fail(MP_E_HIP, "mp_multi_create: event creation failed");
     if (!rc) {
         std::vector<int> sorted(m->dev);
         std::sort(sorted.begin(), sorted.end());
@@ -238,10 +245,7 @@ MP_EXPORT int mp_multi_run(void* multi, uint64_t* n_hits) {
         MP_HIP_CHECK(hipMalloc(&m->all, cap * sizeof(mp_hit)));
         m->all_cap = cap;
     }
-    hipEvent_t e0, e1;
-    MP_HIP_CHECK(hipEventCreate(&e0));
-    MP_HIP_CHECK(hipEventCreate(&e1));
-    MP_HIP_CHECK(hipEventRecord(e0, m->st[0]));
+    MP_HIP_CHECK(hipEventRecord(m->e0, m->st[0]));
     uint64_t off = 0;
     if (!m->comm.empty()) {
         // gatherv over RCCL: devices[0] receives every device's sorted list at its offset
@@ -268,11 +272,9 @@ MP_EXPORT int mp_multi_run(void* multi, uint64_t* n_hits) {
             off += m->counts[d];
         }
     }
-    MP_HIP_CHECK(hipEventRecord(e1, m->st[0]));
+    MP_HIP_CHECK(hipEventRecord(m->e1, m->st[0]));
     MP_HIP_CHECK(hipStreamSynchronize(m->st[0]));
-    MP_HIP_CHECK(hipEventElapsedTime(&m->gather_ms, e0, e1));
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
+    MP_HIP_CHECK(hipEventElapsedTime(&m->gather_ms, m->e0, m->e1));
     m->n_all = total;
     if (n_hits) *n_hits = total;
     return MP_OK;
@@ -308,6 +310,7 @@ struct Comm {
     uint64_t* d_meta = nullptr;  // nranks x {count, seq shift, capacity}
     uint64_t* h_meta = nullptr;  // pinned: this rank's 3 words, then the gathered nranks x 3
     hipEvent_t ev = nullptr;     // the gathered counts' arrival (polled)
+    double timeout_s = 600.0;    // MP_COMM_TIMEOUT_S: bound on waiting for the other ranks
 };
 }  // namespace mp
 
@@ -326,6 +329,7 @@ MP_EXPORT int mp_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, in
     *out = nullptr;
     MP_HIP_CHECK(hipSetDevice(device));
     Comm* c = new Comm();
+    if (const char* t = std::getenv("MP_COMM_TIMEOUT_S")) c->timeout_s = std::atof(t);
     c->rank = rank;
     c->nranks = nranks;
     c->device = device;
@@ -371,10 +375,12 @@ MP_EXPORT int mp_comm_gather_hits(void* comm, void* search, uint32_t seq_shift, 
     MP_NCCL_CHECK(ncclAllGather(c->d_meta + (size_t)c->rank * 3, c->d_meta, 3, ncclUint64, c->c, st));
     MP_HIP_CHECK(hipMemcpyAsync(c->h_meta + 3, c->d_meta, (size_t)c->nranks * 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     MP_HIP_CHECK(hipEventRecord(c->ev, st));
-    for (;;) {
-        const hipError_t e = hipEventQuery(c->ev);
-        if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) MP_HIP_CHECK(e);
+    {
+        const hipError_t e = poll_event(c->ev, c->timeout_s);
+        if (e == hipErrorNotReady)
+            return fail(MP_E_HIP, "mp_comm_gather_hits: the counts exchange did not complete within the "
+                                  "timeout (a rank missing from the collective?)");
+        MP_HIP_CHECK(e);
     }
     uint64_t total = 0;
     for (int r = 0; r < c->nranks; ++r) total += meta[(size_t)r * 3];

@@ -50,68 +50,13 @@ __global__ void bucket_hist(const uint64_t* __restrict__ hi, const uint64_t* __r
     }
 }
 
-// exclusive scan of the bucket counts (one 1024-thread workgroup); cursor = offset.  The
-// counts pass through LDS in tiles of kOffTile: coalesced loads and stores, 8 consecutive
-// counts per thread inside a tile, a wave shuffle scan and one LDS word per wave.  (Holding 64
-// consecutive counts per thread in registers made every load and store a 64-line gather: c4's
-// 65,536 buckets took 80 us.)
-constexpr uint32_t kOffTile = 8192;
+// exclusive scan of the bucket counts by one 1024-thread workgroup (bucket_offsets_block,
+// mp_internal.h): pair_kernel's last block runs it, so this kernel is only the unfused form.
 __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restrict__ cnt, uint32_t nb,
                                                        uint32_t* __restrict__ off, uint32_t* __restrict__ cursor) {
     __shared__ uint4 s_v4[kOffTile / 4];
     __shared__ uint32_t s_w[16];
-    uint32_t* s_v = reinterpret_cast<uint32_t*>(s_v4);
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += kOffTile) {
-#pragma unroll
-        for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
-            const uint32_t i = j * 1024 + t;
-            s_v[i] = base + i < nb ? cnt[base + i] : 0u;
-        }
-        __syncthreads();
-        uint4 q0 = s_v4[2 * t], q1 = s_v4[2 * t + 1];
-        const uint32_t sum = q0.x + q0.y + q0.z + q0.w + q1.x + q1.y + q1.z + q1.w;
-        uint32_t x = sum;  // inclusive scan over the wave
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-            if ((int)lane >= o) x += y;
-        }
-        if (lane == 63) s_w[w] = x;
-        __syncthreads();
-        uint32_t wpre = 0, tot = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k) {
-            const uint32_t sw = s_w[k];
-            wpre += k < w ? sw : 0u;
-            tot += sw;
-        }
-        uint32_t run = carry + wpre + x - sum, v;
-        v = q0.x; q0.x = run; run += v;
-        v = q0.y; q0.y = run; run += v;
-        v = q0.z; q0.z = run; run += v;
-        v = q0.w; q0.w = run; run += v;
-        v = q1.x; q1.x = run; run += v;
-        v = q1.y; q1.y = run; run += v;
-        v = q1.z; q1.z = run; run += v;
-        q1.w = run;
-        s_v4[2 * t] = q0;
-        s_v4[2 * t + 1] = q1;
-        __syncthreads();
-#pragma unroll
-        for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
-            const uint32_t i = j * 1024 + t;
-            if (base + i < nb) {
-                const uint32_t o = s_v[i];
-                off[base + i] = o;
-                cursor[base + i] = o;
-            }
-        }
-        carry += tot;
-        __syncthreads();  // s_v and s_w are rewritten by the next tile
-    }
-    if (t == 0) off[nb] = carry;
+    bucket_offsets_block(cnt, nb, off, cursor, s_v4, s_w);
 }
 
 __global__ void bucket_scatter(const uint64_t* __restrict__ keys, const unsigned long long* __restrict__ counters,
@@ -233,10 +178,56 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
     }
 }
 
+// Order mode 0: pair_kernel left every bucket's keys in its slot (bucket b at b * slot_cap,
+// in arrival order) and, from its last block, the bucket offsets.  One wave per bucket ranks
+// the bucket's keys -- up to 64 by shuffles, up to slot_cap by counting through the wave's
+// LDS -- and writes the decoded records at off[b] + rank.  No scatter pass, no block barrier.
+// A bucket over slot_cap (its keys did not all fit) sets counters[kSortOverflow]; the host
+// then orders the run in mode 1 from the linear keys.
+constexpr uint32_t kSlotWaves = 4;
+__global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
+    const uint64_t* __restrict__ slots, uint32_t slot_cap, const uint32_t* __restrict__ off, uint32_t nb,
+    unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
+    uint32_t n_seq, const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs, mp_hit* __restrict__ out,
+    unsigned long long* __restrict__ counters) {
+    __shared__ uint64_t s_k[kSlotWaves][kSlotCap];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t b = blockIdx.x * kSlotWaves + wave;
+    if (b >= nb) return;  // wave-uniform, and no block barrier follows
+    const uint32_t start = off[b], m = off[b + 1] - start;
+    if (m == 0) return;
+    if (m > slot_cap) {
+        if (lane == 0) atomicOr(&counters[kSortOverflow], 1ull);
+        return;
+    }
+    const uint64_t* src = slots + (uint64_t)b * slot_cap;
+    if (m <= 64) {
+        const uint64_t key = lane < m ? src[lane] : ~0ull;
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint64_t kj = __shfl(key, (int)j, 64);
+            r += kj < key || (kj == key && j < lane);  // ties: stable (keys are unique anyway)
+        }
+        if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+        return;
+    }
+    uint64_t* k = s_k[wave];
+    for (uint32_t i = lane; i < m; i += 64) k[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t i = lane; i < m; i += 64) {
+        const uint64_t key = k[i];
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < m; ++j) r += k[j] < key || (k[j] == key && j < i);
+        decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+    }
+}
+
 bool sort_hits_device_ok(const Search* s) {
     const unsigned hi_bits = bits_for(s->genome->total);
     const unsigned try_bits = bits_for(2ull * (uint64_t)std::max(s->table->prm.margin, 0));
-    return hi_bits + s->table->rank_bits + try_bits <= 64 && s->opt.sort == MP_SORT_AUTO;
+    return hi_bits + s->table->rank_bits + try_bits <= 64 && (s->opt.sort == MP_SORT_AUTO || s->opt.sort == MP_SORT_SCATTER);
 }
 
 int alloc_sort_buckets(Search* s) {
@@ -257,31 +248,43 @@ SortPlan sort_plan(const Search* s) {
     bb = std::min(bb, key_bits);
     P.shift = key_bits - bb;
     P.nb = 1u << bb;
+    P.slot_cap = kSlotCap;
     return P;
 }
 
 uint32_t* sort_bucket_counts(Search* s) { return s->bucket; }
+uint32_t* sort_bucket_offsets(Search* s) { return s->bucket + (1u << kMaxBucketBits); }
+uint32_t* sort_bucket_cursors(Search* s) { return s->bucket + 2 * (1u << kMaxBucketBits) + 1; }
 
-int sort_hits_device(Search* s, hipStream_t st, bool fused) {
+int alloc_sort_slots(Search* s, const SortPlan& P) {
+    const size_t need = (size_t)P.nb * P.slot_cap * sizeof(uint64_t);
+    if (need <= s->slots_bytes) return MP_OK;
+    hipFree(s->slots);
+    s->slots = nullptr;
+    s->slots_bytes = 0;
+    MP_HIP_CHECK(hipMalloc(&s->slots, need));
+    s->slots_bytes = need;
+    return MP_OK;
+}
+
+int sort_hits_device(Search* s, hipStream_t st, int mode) {
     const SortPlan P = sort_plan(s);
     const int arc = alloc_sort_buckets(s);
     if (arc) return arc;
-    uint32_t* cnt = s->bucket;
-    uint32_t* off = cnt + (1u << kMaxBucketBits);
-    uint32_t* cursor = off + (1u << kMaxBucketBits) + 1;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((s->cap + 255) / 256, 2048);
-    if (!fused) {
-        MP_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)P.nb * 4, st));
-        hipLaunchKernelGGL(bucket_hist, dim3(grid), dim3(256), 0, st, s->keys, s->keys + s->cap, s->counters, s->cap,
-                           P.try_bits, P.low_bits, P.shift, s->tmp_lo, cnt);
+    const uint32_t* off = sort_bucket_offsets(s);
+    uint32_t* cursor = sort_bucket_cursors(s);
+    const Genome* g = s->genome;
+    if (mode == 0) {
+        hipLaunchKernelGGL(sort_decode_slots, dim3((P.nb + kSlotWaves - 1) / kSlotWaves), dim3(64 * kSlotWaves), 0, st,
+                           s->slots, P.slot_cap, off, P.nb, P.try_bits, P.low_bits, g->d_base, g->d_len, g->n_seq,
+                           s->table->inv_rank, s->table->recs, s->out, s->counters);
         MP_HIP_CHECK(hipGetLastError());
+        return MP_OK;
     }
-    hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, cnt, P.nb, off, cursor);
-    MP_HIP_CHECK(hipGetLastError());
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((s->cap + 255) / 256, 2048);
     hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, s->counters, s->cap, P.shift, cursor,
                        s->tmp_hi);
     MP_HIP_CHECK(hipGetLastError());
-    const Genome* g = s->genome;
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
                        s->tmp_hi, off, P.nb, P.try_bits, P.low_bits,
                        g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->counters);

@@ -92,6 +92,10 @@ struct ScanArgs {
     uint64_t* sort_keys;
     uint32_t* sort_cnt;
     uint32_t sort_nb, sort_shift, sort_try_bits, sort_low_bits;
+    uint32_t* sort_off;     // pair_kernel's last block writes the bucket offsets / cursors here
+    uint32_t* sort_cursor;
+    uint64_t* sort_slots;   // order mode 0: keys straight into their bucket slot (null: mode 1)
+    uint32_t slot_cap;
 };
 
 // Bucket counts of the fused device sort, zeroed by every block of a scan kernel.
@@ -114,7 +118,8 @@ __device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x > 
 constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
 constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;  // pair_kernel batch counters, 8 x 256 B
 constexpr int kSchedBase = kPairQBase + 8 * kStatStride;  // scan super-step chunk counters, 8 x 256 B
-constexpr size_t kCounterBytes = (size_t)(kSchedBase + 8 * kStatStride) * 8;
+constexpr int kDoneBase = kSchedBase + 8 * kStatStride;   // pair_kernel blocks finished (fused offsets)
+constexpr size_t kCounterBytes = (size_t)(kDoneBase + kStatStride) * 8;
 #ifndef MP_PDYN_BATCH
 #define MP_PDYN_BATCH 64
 #endif
@@ -306,12 +311,13 @@ __device__ __forceinline__ void write_hits(const ScanArgs& a, const HitStage& S,
         const uint32_t i = b0 + (uint32_t)lane;
         const bool on = i < S.n && off + i < a.cap;
         uint32_t bk = 0xFFFFFFFFu;
+        uint64_t key = 0;
         if (on) {
             const uint64_t hi = S.hi[i], lo = S.lo[i];
             a.hit_hi[off + i] = hi;
             a.hit_lo[off + i] = lo;
             if (a.sort_cnt) {
-                const uint64_t key = (hi << a.sort_low_bits) | ((lo >> 32) << a.sort_try_bits) | (lo & 0xFFFFFFFFull);
+                key = (hi << a.sort_low_bits) | ((lo >> 32) << a.sort_try_bits) | (lo & 0xFFFFFFFFull);
                 a.sort_keys[off + i] = key;
                 bk = (uint32_t)(key >> a.sort_shift);
             }
@@ -319,7 +325,14 @@ __device__ __forceinline__ void write_hits(const ScanArgs& a, const HitStage& S,
         if (a.sort_cnt) {
             uint32_t head, len;
             bucket_runs(bk, on, lane, head, len);
-            if (on && head == (uint32_t)lane) atomicAdd(&a.sort_cnt[bk], len);
+            if (a.sort_slots) {  // order mode 0: the run's place in its bucket slot, one returning atomic
+                uint32_t at = 0;
+                if (on && head == (uint32_t)lane) at = atomicAdd(&a.sort_cnt[bk], len);
+                at = (uint32_t)__shfl((int)at, (int)(head & 63u), 64) + ((uint32_t)lane - head);
+                if (on && at < a.slot_cap) a.sort_slots[(uint64_t)bk * a.slot_cap + at] = key;
+            } else if (on && head == (uint32_t)lane) {
+                atomicAdd(&a.sort_cnt[bk], len);
+            }
         }
     }
 }
@@ -2015,6 +2028,35 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     uint64_t off = s_base;
     for (int q = 0; q < w; ++q) off += s_st[q].n;
     write_hits(a, S, off, lane);
+    if (a.sort_off) {
+        // bucket_offsets fused: the last block to finish scans the bucket counts (every other
+        // block's count atomics precede its fence and its arrival), in the batch stages' LDS
+        __threadfence();
+        __syncthreads();
+        __shared__ uint32_t s_last;
+        if (threadIdx.x == 0)
+            s_last = atomicAdd(reinterpret_cast<unsigned int*>(&a.counters[kDoneBase]), 1u) == gridDim.x - 1u;
+        __syncthreads();
+        if (s_last) {
+            __threadfence();
+            static_assert(sizeof(s_pst) >= (kOffTile / 4) * sizeof(uint4) + 16 * sizeof(uint32_t), "offset tile fits");
+            uint4* tile = reinterpret_cast<uint4*>(&s_pst[0][0]);
+            bucket_offsets_block(a.sort_cnt, a.sort_nb, a.sort_off, a.sort_cursor, tile,
+                                 reinterpret_cast<uint32_t*>(tile + kOffTile / 4));
+        }
+    }
+}
+
+// The run's last kernel: counters[0..8) into the device-mapped pinned words the host polls
+// (no copy), then every counter zeroed for the next run (no fill before it).
+__global__ __launch_bounds__(1024) void finish_kernel(unsigned long long* __restrict__ counters, uint32_t n_words,
+                                                      unsigned long long* __restrict__ h_out) {
+    unsigned long long v = 0;
+    if (threadIdx.x < 8) v = counters[threadIdx.x];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n_words; i += blockDim.x) counters[i] = 0ull;
+    if (threadIdx.x < 8) h_out[threadIdx.x] = v;
+    __threadfence_system();
 }
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
@@ -2053,20 +2095,13 @@ __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* _
         if (s->stage_timing) MP_HIP_CHECK(x); \
     } while (0)
 
-// Wait for an event by polling (hipEventQuery) instead of a blocking synchronisation.
-static hipError_t wait_event(hipEvent_t ev) {
-    for (;;) {
-        const hipError_t e = hipEventQuery(ev);
-        if (e != hipErrorNotReady) return e;
-    }
-}
-
 static void free_search(Search* s) {
     if (!s) return;
     hipFree(s->keys); hipFree(s->tmp_hi); hipFree(s->tmp_lo); hipFree(s->out); hipFree(s->sort_tmp);
     hipFree(s->counters); hipFree(s->spans); hipFree(s->bucket);
     hipFree(s->surv);
     hipFree(s->tails);
+    hipFree(s->slots);
     if (s->ev0) hipEventDestroy(s->ev0);
     if (s->ev1) hipEventDestroy(s->ev1);
     if (s->ev2) hipEventDestroy(s->ev2);
@@ -2124,13 +2159,14 @@ MP_EXPORT int mp_search_set_stage_timing(void* search, int32_t on) {
 MP_EXPORT int mp_search_set_options(void* search, const mp_search_options* opt) {
     Search* s = (Search*)search;
     if (!s || !opt) return fail(MP_E_ARG, "mp_search_set_options: null pointer");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_set_options: a run is enqueued");
     if (opt->tails < MP_TAILS_AUTO || opt->tails > MP_TAILS_KERNEL || opt->sort < MP_SORT_AUTO ||
-        opt->sort > MP_SORT_RADIX128 || opt->sort_bucket_bits < 0 || opt->sort_bucket_bits > 16 ||
+        opt->sort > MP_SORT_SCATTER || opt->sort_bucket_bits < 0 || opt->sort_bucket_bits > 16 ||
         opt->pair_blocks_per_cu < 0)
         return fail(MP_E_ARG, "mp_search_set_options: option out of range");
     MP_HIP_CHECK(hipSetDevice(s->genome->device));
     s->opt = *opt;
-    s->sort_crowded = false;
+    s->order_mode = opt->sort == MP_SORT_SCATTER ? 1 : 0;
     int rc = alloc_hits(s, opt->hit_cap ? opt->hit_cap : kDefaultHitCap);
     if (!rc) rc = alloc_surv(s, opt->surv_cap ? opt->surv_cap : kDefaultSurvCap);
     if (!rc) rc = alloc_tails(s, opt->tail_cap ? opt->tail_cap : kDefaultTailCap);
@@ -2173,10 +2209,14 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
             rc = fail(MP_E_HIP, "event creation failed");
             break;
         }
-        if (hipHostMalloc((void**)&s->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+        // device-mapped pinned words: finish_kernel writes the run's counters straight into them
+        if (hipHostMalloc((void**)&s->h_cnt, 16 * sizeof(unsigned long long), hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&s->d_hcnt, (void*)s->h_cnt, 0) != hipSuccess) {
             rc = fail(MP_E_NOMEM, "pinned counter allocation failed");
             break;
         }
+        std::memset((void*)s->h_cnt, 0, 16 * sizeof(unsigned long long));
+        if (hipMemset(s->counters, 0, kCounterBytes) != hipSuccess) { rc = fail(MP_E_HIP, "counter reset failed"); break; }
         rc = alloc_hits(s, kDefaultHitCap);
         if (!rc) rc = alloc_surv(s, kDefaultSurvCap);
         if (!rc) rc = alloc_tails(s, kDefaultTailCap);
@@ -2190,9 +2230,219 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
     return MP_OK;
 }
 
-MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, uint64_t* n_hits) {
+namespace mp {
+
+static_assert(sizeof(ScanArgs) <= sizeof(Search::pend_args), "ScanArgs fits the pending-run slot");
+
+// The list pointers, capacities and hit-order fields of a run in order mode `mode`.
+static int set_lists(Search* s, ScanArgs& a, int mode) {
+    a.hit_hi = s->keys;
+    a.hit_lo = s->keys + s->cap;
+    a.counters = s->counters;
+    a.cap = s->cap;
+    a.surv = s->surv;
+    a.surv_cap = s->surv_cap;
+    a.tails = s->tails;
+    a.tails_cap = s->tails_cap;
+    a.sort_cnt = nullptr;
+    a.sort_keys = nullptr;
+    a.sort_off = a.sort_cursor = nullptr;
+    a.sort_slots = nullptr;
+    a.sort_nb = a.sort_shift = a.sort_try_bits = a.sort_low_bits = a.slot_cap = 0;
+    if (mode < 2) {  // after a hit-list regrowth too: the plan follows the capacity
+        const SortPlan P = sort_plan(s);
+        a.sort_cnt = sort_bucket_counts(s);
+        a.sort_keys = s->tmp_lo;
+        a.sort_off = sort_bucket_offsets(s);
+        a.sort_cursor = sort_bucket_cursors(s);
+        a.sort_nb = P.nb;
+        a.sort_shift = P.shift;
+        a.sort_try_bits = P.try_bits;
+        a.sort_low_bits = P.low_bits;
+        if (mode == 0) {
+            const int rc = alloc_sort_slots(s, P);
+            if (rc) return rc;
+            a.sort_slots = s->slots;
+            a.slot_cap = P.slot_cap;
+        }
+    }
+    return MP_OK;
+}
+
+// Every kernel of one run, back to back on the stream with no host wait: scan -> fingerprint
+// survivors (+ bucket-tail references -> tail survivors) -> pair check -> hit keys and bucket
+// counts (+ offsets, from pair_kernel's last block) -> hit order (modes 0 and 1) ->
+// finish_kernel (counters into the mapped host words, then zeroed) -> the completion event.
+static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStream_t st, int mode) {
+    Table* t = s->table;
+    if (s->dirty) {  // an abandoned run may have left counts behind
+        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
+        s->dirty = false;
+    }
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU);
+    bool inl = t->n_rec > t->n_keys + t->n_keys / 4;  // bucket tails inline vs tail_kernel
+    if (s->opt.tails == MP_TAILS_INLINE) inl = true;
+    if (s->opt.tails == MP_TAILS_KERNEL) inl = false;
+    // W <= kDenseMaxW: dense_kernel (bucket index in LDS, filter-word octs)
+    const bool dense = (uint32_t)t->prm.wordsize <= kDenseMaxW && !s->opt.no_dense;
+    // level-2 filter of the filtered rank groups: I = 0 (the 2-bit mismatch count is then a
+    // lower bound), compact 8-B heads (not h16)
+    const bool rkf = t->kgrp_F >= 2 && !t->h16 && a.I == 0 && !s->opt.no_rank_filter && t->filt_direct &&
+                     !t->lds_exact && a.W >= 11 && a.W <= 13;
+    const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
+    if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
+    if (dense) {
+        const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
+                                                            (uint64_t)s->n_cu * (uint64_t)s->dense_per_cu);
+        const size_t lds = s->dense_lds;
+        if (a.N == 0) hipLaunchKernelGGL(dense_kernel<0>, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        else if (a.N == 1) hipLaunchKernelGGL(dense_kernel<1>, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        else if (a.N == 2) hipLaunchKernelGGL(dense_kernel<2>, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        else hipLaunchKernelGGL(dense_kernel<-1>, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+    } else if (inl) {
+        if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    } else {
+        if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h16)
+            hipLaunchKernelGGL((scan_kernel<1, false, 2, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 2 && a.defer_full && rkf)
+            hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
+            hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && a.defer_full && rkf)
+            hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && a.defer_full && t->h16)
+            hipLaunchKernelGGL((scan_kernel<1, false, 1, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && a.defer_full)
+            hipLaunchKernelGGL((scan_kernel<1, false, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, false, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
+    }
+    MP_HIP_CHECK(hipGetLastError());
+    if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
+    if (!dense && !inl && (t->max_bucket > 1 || a.defer_full)) {  // defer_full: single-record full heads too
+        hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, a);
+        MP_HIP_CHECK(hipGetLastError());
+    }
+    MID_EVENT(hipEventRecord(s->ev1, st));
+    const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
+                                                           : s->pair_per_cu;
+    hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, a);
+    MP_HIP_CHECK(hipGetLastError());
+    MID_EVENT(hipEventRecord(s->ev2, st));
+    if (mode < 2) {  // hit order on the device count: no host round trip before it
+        const int rc = sort_hits_device(s, st, mode);
+        if (rc) return rc;
+    }
+    MID_EVENT(hipEventRecord(s->ev3, st));
+    hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(1024), 0, st, s->counters, (uint32_t)(kCounterBytes / 8), s->d_hcnt);
+    MP_HIP_CHECK(hipGetLastError());
+    MP_HIP_CHECK(hipEventRecord(s->evd, st));
+    return MP_OK;
+}
+
+// Wait for the enqueued run and read its counters (written by finish_kernel).
+static int wait_counts(Search* s, unsigned long long* cnt) {
+    MP_HIP_CHECK(poll_event(s->evd));
+    std::memcpy(cnt, (const void*)s->h_cnt, 8 * sizeof(unsigned long long));
+    return MP_OK;
+}
+
+// The run's order again, synchronously, one mode up (a bucket overflowed in `from`); raises
+// the handle's sticky mode.  The linear keys (tmp_lo; hi/lo for rocPRIM) are intact.
+static int redo_order(Search* s, hipStream_t st, int from, uint64_t nh) {
+    Genome* g = s->genome;
+    Table* t = s->table;
+    for (int mode = from + 1; mode <= 2; ++mode) {
+        s->order_mode = std::max(s->order_mode, mode);
+        if (mode == 1) {
+            // bucket_scatter reads the hit count on the device; finish_kernel zeroed it
+            s->h_cnt[8] = nh;
+            MP_HIP_CHECK(hipMemcpyAsync(s->counters, (const void*)&s->h_cnt[8], sizeof(unsigned long long),
+                                        hipMemcpyHostToDevice, st));
+            const int rc = sort_hits_device(s, st, 1);
+            if (rc) return rc;
+            unsigned long long ovf = 0;
+            MP_HIP_CHECK(hipMemcpyAsync(&s->h_cnt[9], s->counters + kSortOverflow, sizeof(ovf), hipMemcpyDeviceToHost, st));
+            MP_HIP_CHECK(hipStreamSynchronize(st));
+            ovf = s->h_cnt[9];
+            MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
+            if (!ovf) break;
+            continue;
+        }
+        const int rc = sort_hits(s, nh, st);
+        if (rc) return rc;
+        if (nh) {
+            const uint32_t blocks = (uint32_t)((nh + 255) / 256);
+            hipLaunchKernelGGL(decode_kernel, dim3(blocks), dim3(256), 0, st, s->keys, s->keys + s->cap, nh,
+                               g->d_base, g->d_len, g->n_seq, t->inv_rank, t->recs, s->out);
+            MP_HIP_CHECK(hipGetLastError());
+        }
+        MP_HIP_CHECK(hipStreamSynchronize(st));
+    }
+    return MP_OK;
+}
+
+static int search_complete(Search* s, uint64_t* n_hits) {
+    hipStream_t st = s->pend_st;
+    ScanArgs& a = *reinterpret_cast<ScanArgs*>(s->pend_args);
+    const int mode0 = s->pend_mode;
+    int mode = mode0;
+    unsigned long long cnt[8];
+    int rc = wait_counts(s, cnt);
+    if (rc) return rc;
+    if (s->scan_timing || s->stage_timing) MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
+    else s->scan_ms = -1.f;
+    MID_EVENT(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
+    // A list that overflowed is grown and the whole run enqueued again (rare: the first runs of
+    // a handle); kernels never write past a capacity.
+    for (int attempt = 0; cnt[2] > s->surv_cap || cnt[4] > s->tails_cap || cnt[0] > s->cap; ++attempt) {
+        if (attempt == 3) return fail(MP_E_STATE, "mp_search_run: list overflow after growth");
+        ++s->n_regrowths;
+        if (cnt[4] > s->tails_cap) rc = alloc_tails(s, cnt[4] + cnt[4] / 4 + 1024);
+        if (!rc && cnt[2] > s->surv_cap) rc = alloc_surv(s, cnt[2] + cnt[2] / 2 + 1024);
+        if (!rc && cnt[0] > s->cap) rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
+        mode = sort_hits_device_ok(s) ? s->order_mode : 2;
+        if (!rc) rc = set_lists(s, a, mode);
+        if (!rc) rc = enqueue_kernels(s, a, s->pend_tiles, st, mode);
+        if (!rc) rc = wait_counts(s, cnt);
+        if (rc) return rc;
+        if (s->scan_timing || s->stage_timing) MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
+        MID_EVENT(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
+    }
+    (void)mode0;
+    MID_EVENT(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
+    MID_EVENT(hipEventElapsedTime(&s->order_ms, s->ev2, s->ev3));
+    s->n_candidates = cnt[1];
+    s->n_survivors = cnt[3];
+    const uint64_t nh = cnt[0];
+    if (mode == 2 || cnt[kSortOverflow]) {  // the device order did not hold this run's keys
+        rc = redo_order(s, st, mode == 2 ? 1 : mode, nh);
+        if (rc) return rc;
+    }
+    if (!s->stage_timing) s->tail_ms = s->pair_ms = s->order_ms = -1.f;  // not measured
+    s->n_hits = nh;
+    if (n_hits) *n_hits = nh;
+    return MP_OK;
+}
+
+}  // namespace mp
+
+MP_EXPORT int mp_search_set_scan_timing(void* search, int32_t on) {
     Search* s = (Search*)search;
-    if (!s) return fail(MP_E_ARG, "mp_search_run: null search");
+    if (!s) return fail(MP_E_ARG, "mp_search_set_scan_timing: null search");
+    s->scan_timing = on != 0;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* stream) {
+    Search* s = (Search*)search;
+    if (!s) return fail(MP_E_ARG, "mp_search_enqueue: null search");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_enqueue: the previous run was not completed (mp_search_complete)");
     Table* t = s->table;
     Genome* g = s->genome;
     if (!g->sealed) return fail(MP_E_STATE, "mp_search_run: genome not sealed (call mp_genome_seal)");
@@ -2233,11 +2483,15 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         tiles += (phi - sp.p_al + kSuper - 1) / kSuper;
         windows += phi - plo;
     }
+    // windows: counted here, on the host, from the spans the kernel walks
     s->n_windows = windows;
     s->n_candidates = 0;
     s->n_hits = 0;
     s->scan_ms = s->tail_ms = 0.f;
-    if (n_hits) *n_hits = 0;
+    s->pend_st = st;
+    s->pend_tiles = tiles;
+    s->pend_empty = tiles == 0;
+    s->pending = true;
     if (!tiles) return MP_OK;
     const uint32_t n_real_spans = (uint32_t)spans.size();
     {
@@ -2245,189 +2499,79 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
         sentinel.super0 = tiles;
         spans.push_back(sentinel);
     }
-    if (spans.size() > s->spans_cap) {
-        hipFree(s->spans);
-        s->spans = nullptr;
-        s->spans_cap = 0;
-        s->last_spans.clear();
-        MP_HIP_CHECK(hipMalloc(&s->spans, spans.size() * sizeof(SeqSpan)));
-        s->spans_cap = spans.size();
-    }
-    // the same range again (a repeated search, a benchmark step): the device copy is current
-    if (spans.size() != s->last_spans.size() ||
-        memcmp(spans.data(), s->last_spans.data(), spans.size() * sizeof(SeqSpan)) != 0) {
-        s->last_spans.clear();
-        MP_HIP_CHECK(hipMemcpyAsync(s->spans, spans.data(), spans.size() * sizeof(SeqSpan), hipMemcpyHostToDevice, st));
-        s->last_spans = spans;
-    }
-
-    ScanArgs a;
-    a.g2 = g->g2; a.gexc = g->gexc; a.ginv = g->ginv;
-    a.xr_start = g->xr_start; a.xr_char = g->xr_char; a.xr_dir = g->xr_dir; a.n_xr = g->n_xr;
-    a.has_u = g->has_u ? 1 : 0;
-    a.seq_base = g->d_base; a.seq_len = g->d_len;
-    a.spans = s->spans; a.n_spans = n_real_spans;
-    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
-    a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
-    a.defer_full = t->defer_full && !s->opt.no_defer;
-    a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F;
-    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.lfilt = t->lfilt;
-    a.slots = t->slots; a.slot_log2 = t->slot_log2;
-    a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
-    a.planes = t->planes; a.pchars = t->pchars;
-    a.W = t->prm.wordsize; a.M = t->prm.margin; a.N = t->prm.mismatches;
-    a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
-    a.g_lo = g_lo; a.g_hi = g_hi;
-
-    unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // crowded hit positions (IUPAC primers over N runs, repeats) overflow the buckets and
-    // pay both sorts; once seen, this search orders with rocPRIM directly
-    const bool dev_sort = sort_hits_device_ok(s) && !s->sort_crowded;
-    // the histogram pass of the device sort runs inside pair_kernel's hit flush
-    a.sort_cnt = nullptr;
-    a.sort_keys = nullptr;
-    a.sort_nb = a.sort_shift = a.sort_try_bits = a.sort_low_bits = 0;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves,
-                                                       (uint64_t)s->n_cu * kBlocksPerCU);
-    // scan -> fingerprint survivors (+ bucket-tail references -> tail survivors) -> pair
-    // check -> hit keys, back to back on the stream with one host synchronisation; the
-    // pair kernel reads the survivor count on the device.  A list that overflowed is
-    // grown and the whole pass rerun.
-    bool inl = t->n_rec > t->n_keys + t->n_keys / 4;  // bucket tails inline vs tail_kernel
-    if (s->opt.tails == MP_TAILS_INLINE) inl = true;
-    if (s->opt.tails == MP_TAILS_KERNEL) inl = false;
-    // W <= kDenseMaxW: dense_kernel (bucket index in LDS, filter-word octs)
-    const bool dense = (uint32_t)t->prm.wordsize <= kDenseMaxW && !s->opt.no_dense;
-    // level-2 filter of the filtered rank groups: I = 0 (the 2-bit mismatch count is then a
-    // lower bound), compact 8-B heads (not h16)
-    const bool rkf = t->kgrp_F >= 2 && !t->h16 && a.I == 0 && !s->opt.no_rank_filter && t->filt_direct &&
-                     !t->lds_exact && a.W >= 11 && a.W <= 13;
-    const size_t dense_lds = s->dense_lds;
-    const uint32_t dense_per_cu = s->dense_per_cu;
-    // A list that overflowed is grown and its producers rerun: the scan (and tail_kernel)
-    // when survivors or bucket-tail references were lost, only the pair check and the sort
-    // when just the hit list was too small.
-    bool rescan = true;
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        a.hit_hi = s->keys;
-        a.hit_lo = s->keys + s->cap;
-        a.counters = s->counters;
-        a.cap = s->cap;
-        a.surv = s->surv;
-        a.surv_cap = s->surv_cap;
-        a.tails = s->tails;
-        a.tails_cap = s->tails_cap;
-        if (dev_sort) {  // after a hit-list regrowth too: the plan follows the capacity
-            const SortPlan P = sort_plan(s);
-            a.sort_cnt = sort_bucket_counts(s);
-            a.sort_keys = s->tmp_lo;
-            a.sort_nb = P.nb;
-            a.sort_shift = P.shift;
-            a.sort_try_bits = P.try_bits;
-            a.sort_low_bits = P.low_bits;
-        }
-        if (rescan) {
-            MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
-            MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-            if (dense) {
-                const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
-                                                                    (uint64_t)s->n_cu * (uint64_t)dense_per_cu);
-                if (a.N == 0) hipLaunchKernelGGL(dense_kernel<0>, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
-                else if (a.N == 1) hipLaunchKernelGGL(dense_kernel<1>, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
-                else if (a.N == 2) hipLaunchKernelGGL(dense_kernel<2>, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
-                else hipLaunchKernelGGL(dense_kernel<-1>, dim3(dgrid), dim3(kDenseBlock), dense_lds, st, a);
-            } else if (inl) {
-                if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
-                else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
-            } else {
-                if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h16)
-                    hipLaunchKernelGGL((scan_kernel<1, false, 2, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct && t->lds_k == 2 && a.defer_full && rkf)
-                    hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
-                    hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct && a.defer_full && rkf)
-                    hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct && a.defer_full && t->h16)
-                    hipLaunchKernelGGL((scan_kernel<1, false, 1, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct && a.defer_full)
-                    hipLaunchKernelGGL((scan_kernel<1, false, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);
-                else if (t->filt_direct) hipLaunchKernelGGL((scan_kernel<1, false, 1>), dim3(grid), dim3(kBlock), 0, st, a);
-                else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
+    int rc = MP_OK;
+    do {
+        if (spans.size() > s->spans_cap) {
+            hipFree(s->spans);
+            s->spans = nullptr;
+            s->spans_cap = 0;
+            s->last_spans.clear();
+            if (hipMalloc(&s->spans, spans.size() * sizeof(SeqSpan)) != hipSuccess) {
+                rc = fail(MP_E_NOMEM, "mp_search_run: span allocation failed");
+                break;
             }
-            MP_HIP_CHECK(hipGetLastError());
-            MP_HIP_CHECK(hipEventRecord(s->evt, st));
-            if (!dense && !inl && (t->max_bucket > 1 || a.defer_full)) {  // defer_full: single-record full heads too
-                hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, a);
-                MP_HIP_CHECK(hipGetLastError());
+            s->spans_cap = spans.size();
+        }
+        // the same range again (a repeated search, a benchmark step): the device copy is current
+        if (spans.size() != s->last_spans.size() ||
+            memcmp(spans.data(), s->last_spans.data(), spans.size() * sizeof(SeqSpan)) != 0) {
+            s->last_spans.clear();
+            if (hipMemcpyAsync(s->spans, spans.data(), spans.size() * sizeof(SeqSpan), hipMemcpyHostToDevice, st) !=
+                    hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {  // the pageable source must outlive the copy
+                rc = fail(MP_E_HIP, "mp_search_run: span upload failed");
+                break;
             }
-        } else {  // hit list regrown: counters of the pair check and the sort only
-            if (a.sort_cnt) MP_HIP_CHECK(hipMemsetAsync(a.sort_cnt, 0, (size_t)a.sort_nb * 4, st));
-            MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, sizeof(unsigned long long), st));
-            MP_HIP_CHECK(hipMemsetAsync(s->counters + kSortOverflow, 0, sizeof(unsigned long long), st));
-            MP_HIP_CHECK(hipMemsetAsync(s->counters + kPairQBase, 0, 8 * kStatStride * sizeof(unsigned long long), st));
-            MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-            MP_HIP_CHECK(hipEventRecord(s->evt, st));
+            s->last_spans = spans;
         }
-        MID_EVENT(hipEventRecord(s->ev1, st));
-        const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
-                                                               : s->pair_per_cu;
-        hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, a);
-        MP_HIP_CHECK(hipGetLastError());
-        MID_EVENT(hipEventRecord(s->ev2, st));
-        if (dev_sort) {  // hit order on the device count: no host round trip before the sort
-            const int src = sort_hits_device(s, st, true);
-            if (src) return src;
-            MID_EVENT(hipEventRecord(s->ev3, st));
-        }
-        // one readback into pinned memory, its completion polled: a blocking stream
-        // synchronisation added tens of microseconds per run (small searches, sharded steps)
-        MP_HIP_CHECK(hipMemcpyAsync(s->h_cnt, s->counters, sizeof(cnt), hipMemcpyDeviceToHost, st));
-        MP_HIP_CHECK(hipEventRecord(s->evd, st));
-        MP_HIP_CHECK(wait_event(s->evd));
-        memcpy(cnt, s->h_cnt, sizeof(cnt));
-        if (rescan) {
-            MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
-            MID_EVENT(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
-        }
-        if (cnt[2] <= s->surv_cap && cnt[4] <= s->tails_cap && cnt[0] <= s->cap) break;
-        ++s->n_regrowths;
-        int rc = MP_OK;
-        rescan = cnt[4] > s->tails_cap || cnt[2] > s->surv_cap;
-        if (cnt[4] > s->tails_cap) rc = alloc_tails(s, cnt[4] + cnt[4] / 4 + 1024);
-        if (!rc && cnt[2] > s->surv_cap) rc = alloc_surv(s, cnt[2] + cnt[2] / 2 + 1024);
-        // hits are produced from the survivors only when those all fit
-        if (!rc && !rescan && cnt[0] > s->cap) rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
-        if (rc) return rc;
+        ScanArgs& a = *reinterpret_cast<ScanArgs*>(s->pend_args);
+        a = ScanArgs{};
+        a.g2 = g->g2; a.gexc = g->gexc; a.ginv = g->ginv;
+        a.xr_start = g->xr_start; a.xr_char = g->xr_char; a.xr_dir = g->xr_dir; a.n_xr = g->n_xr;
+        a.has_u = g->has_u ? 1 : 0;
+        a.seq_base = g->d_base; a.seq_len = g->d_len;
+        a.spans = s->spans; a.n_spans = n_real_spans;
+        a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
+        a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
+        a.defer_full = t->defer_full && !s->opt.no_defer;
+        a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F;
+        a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.lfilt = t->lfilt;
+        a.slots = t->slots; a.slot_log2 = t->slot_log2;
+        a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
+        a.planes = t->planes; a.pchars = t->pchars;
+        a.W = t->prm.wordsize; a.M = t->prm.margin; a.N = t->prm.mismatches;
+        a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
+        a.g_lo = g_lo; a.g_hi = g_hi;
+        // keys over 64 bits, or a forced rocPRIM sort: mode 2
+        const int mode = sort_hits_device_ok(s) ? s->order_mode : 2;
+        s->pend_mode = mode;
+        rc = set_lists(s, a, mode);
+        if (!rc) rc = enqueue_kernels(s, a, tiles, st, mode);
+    } while (0);
+    if (rc) {
+        s->pending = false;
+        s->dirty = true;
     }
-    if (cnt[2] > s->surv_cap || cnt[4] > s->tails_cap || cnt[0] > s->cap)
-        return fail(MP_E_STATE, "mp_search_run: list overflow after growth");
-    MID_EVENT(hipEventElapsedTime(&s->pair_ms, s->ev1, s->ev2));
-    s->n_candidates = cnt[1];
-    s->n_survivors = cnt[3];
-    const uint64_t nh = cnt[0];
-    if (dev_sort && cnt[kSortOverflow]) s->sort_crowded = true;
-    if (!dev_sort || cnt[kSortOverflow]) {  // 128-bit order key, or a crowded bucket: rocPRIM
-        int rc = sort_hits(s, nh, st);
-        if (rc) return rc;
-        if (nh) {
-            const uint32_t blocks = (uint32_t)((nh + 255) / 256);
-            hipLaunchKernelGGL(decode_kernel, dim3(blocks), dim3(256), 0, st, s->keys, s->keys + s->cap, nh,
-                               g->d_base, g->d_len, g->n_seq, t->inv_rank, t->recs, s->out);
-            MP_HIP_CHECK(hipGetLastError());
-        }
-        MID_EVENT(hipEventRecord(s->ev3, st));
-        MP_HIP_CHECK(hipStreamSynchronize(st));
-    }
-    MID_EVENT(hipEventElapsedTime(&s->order_ms, s->ev2, s->ev3));
-    if (!s->stage_timing) s->tail_ms = s->pair_ms = s->order_ms = -1.f;  // not measured
-    s->n_hits = nh;
-    if (n_hits) *n_hits = nh;
-    return MP_OK;
+    return rc;
+}
+
+MP_EXPORT int mp_search_complete(void* search, uint64_t* n_hits) {
+    Search* s = (Search*)search;
+    if (!s) return fail(MP_E_ARG, "mp_search_complete: null search");
+    if (!s->pending) return fail(MP_E_STATE, "mp_search_complete: no run enqueued (mp_search_enqueue)");
+    MP_HIP_CHECK(hipSetDevice(s->genome->device));
+    if (n_hits) *n_hits = 0;
+    s->pending = false;
+    if (s->pend_empty) return MP_OK;
+    const int rc = search_complete(s, n_hits);
+    if (rc) s->dirty = true;
+    return rc;
+}
+
+MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, uint64_t* n_hits) {
+    const int rc = mp_search_enqueue(search, range, stream);
+    if (rc) return rc;
+    return mp_search_complete(search, n_hits);
 }
 
 MP_EXPORT int mp_search_fetch(void* search, mp_hit* out, uint64_t cap, void* stream) {

@@ -4,7 +4,10 @@
 // the Python host hands over the oriented records in sts_records order with the
 // (hash_offset, key) pair _hash_value computed for primer1 (engine.py:331-355);
 // this file turns them into the device structures the scan kernel probes.
+#include <sched.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <unordered_map>
 
@@ -19,6 +22,20 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int code, const std::string& msg) {
     set_error(msg);
     return code;
+}
+
+hipError_t poll_event(hipEvent_t ev, double timeout_s) {
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = clk::now();
+    for (uint32_t i = 0;; ++i) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        if (i < 4096) continue;  // ~20 us of tight spin
+        if (timeout_s > 0 && (i & 255) == 0 &&
+            std::chrono::duration<double>(clk::now() - t0).count() > timeout_s)
+            return hipErrorNotReady;
+        sched_yield();
+    }
 }
 
 template <class T>

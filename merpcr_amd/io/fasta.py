@@ -72,6 +72,11 @@ class ReaderRecord(FASTARecord):
 
     __hash__ = None
 
+    def __reduce__(self):
+        # pickle / copy / deepcopy as the reference's plain dataclass: _raw may be a view of
+        # the native reader's buffer, which neither pickles nor outlives the reader
+        return (FASTARecord, (self.defline, self.sequence, self.label))
+
     def __repr__(self):
         return f"FASTARecord(defline={self.defline!r}, sequence={self.sequence!r}, label={self.label!r})"
 

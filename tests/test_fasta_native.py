@@ -174,3 +174,36 @@ def test_parallel_reader_long_lines_and_records(tmp_path):
     exp = _native.fasta_read(p, 1 << 20)
     for threads in (0, 5):
         assert _native.fasta_read(p, 0, threads) == exp
+
+
+def test_reader_records_pickle_and_copy(tmp_path):
+    """Records from the native reader serialise as the reference's plain FASTARecord."""
+    import copy
+    import pickle
+
+    from merpcr_amd.core.models import FASTARecord
+    p = tmp_path / "a.fa"
+    p.write_text(">s1 first\nACGTNacgt\n>s2\nGGGG\n")
+    recs = FASTALoader.load_file(str(p))
+    for r in recs:
+        for back in (pickle.loads(pickle.dumps(r)), copy.copy(r), copy.deepcopy(r)):
+            assert type(back) is FASTARecord
+            assert (back.defline, back.sequence, back.label) == (r.defline, r.sequence, r.label)
+
+
+def test_non_regular_file_streams(tmp_path):
+    """A pipe (st_size 0, not mappable) goes through the streaming reader, not an empty mmap."""
+    import threading
+    fifo = tmp_path / "f.fifo"
+    os.mkfifo(fifo)
+    text = ">p\nACGT\nTTAA\n>q\nGG\n"
+
+    def writer():
+        with open(fifo, "w") as fh:
+            fh.write(text)
+
+    th = threading.Thread(target=writer)
+    th.start()
+    got = [(d, bytes(s)) for d, s in _native.fasta_read(str(fifo), 0)]
+    th.join()
+    assert got == [(">p", b"ACGTTTAA"), (">q", b"GG")]

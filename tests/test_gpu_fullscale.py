@@ -26,7 +26,13 @@ _THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
 
 
 @pytest.mark.parametrize("name,total,records", [("c3", 40_000_000, 3), ("c4", 40_000_000, 3),
-                                                ("c5", 12_000_000, 2)])
+                                                ("c5", 12_000_000, 2),
+                                                # c2's whole workload: 10k STS x one 250 Mbp record
+                                                ("c2", 250_000_000, 1),
+                                                # one 300 Mbp record: hits past 2^27 / 2^28 and in the
+                                                # record's last kbp (u32 span offsets, exception-run
+                                                # directory indices deep in a record)
+                                                ("c3", 300_000_000, 1)])
 def test_full_table_prefix_vs_c_oracle(name, total, records):
     import torch
     cfg = synth.CONFIGS[name]
@@ -62,3 +68,7 @@ def test_full_table_prefix_vs_c_oracle(name, total, records):
     assert stats["windows"] >= 0.9 * total
     assert len(got) == len(ref), (len(got), len(ref), stats)
     assert got.tobytes() == ref.tobytes()
+    if records == 1 and total >= 1 << 28:
+        pos = got["pos1"].astype(np.int64)
+        assert (pos > 1 << 28).sum() > 1000, "no hits deep in the record"
+        assert pos.max() > total - 5_000, (int(pos.max()), total)
