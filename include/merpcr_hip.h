@@ -104,6 +104,12 @@ int mp_genome_put_device(void* genome, uint32_t seq, uint64_t offset, const uint
 /* Build the exception-run index; required once after the last put. */
 int mp_genome_seal(void* genome, void* stream);
 int mp_genome_stats(void* genome, uint64_t* total_bases, uint64_t* n_exc_runs, uint64_t* dev_bytes);
+/* Diagnostic (tests): copy the packed planes of a sealed genome to host memory -- g2
+ * (total/32 words), gexc and ginv (total/64 words each; total = padded bases, the sum of
+ * each length rounded up to 64) and the sorted exception-run index (n_exc_runs starts and
+ * characters).  Any pointer may be NULL to skip that array. */
+int mp_genome_download(void* genome, uint64_t* g2, uint64_t* gexc, uint64_t* ginv, uint64_t* xr_start,
+                       uint8_t* xr_char);
 /* Re-lay the handle out for a new set of sequences (the next search() call of the
  * engine): device planes are reused when the new layout fits them, else regrown.  The
  * handle is unsealed and empty afterwards; searches created on it stay valid. */
@@ -255,6 +261,10 @@ int mp_sts_info(void* sts, int32_t* status, uint64_t* counts);
  * 2i, alias = 2i+1), primer1 u8[], p1_off u64[n+1], primer2 u8[], p2_off u64[n+1],
  * text u8[] (UTF-8), text_off u64[n_text+1]. */
 int mp_sts_arrays(void* sts, const void** ptrs);
+/* The formatter's record column (mp_format_hits rec_text / rec_off) of the parsed
+ * records: UTF-8 "{id}\t{alias}\t({direct})" per record, concatenated (*n_bytes), with
+ * n+1 offsets.  Borrowed, valid until destroy. */
+int mp_sts_record_texts(void* sts, const uint8_t** text, const uint64_t** off, uint64_t* n_bytes);
 void mp_sts_destroy(void* sts);
 
 /* ---- output (replaces the per-hit print of MerPCR.search, engine.py:436-444) --

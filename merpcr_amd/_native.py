@@ -30,7 +30,7 @@ EXPORTS = (
     "mp_abi_version", "mp_last_error", "mp_device_count",
     "mp_table_create", "mp_table_stats", "mp_table_destroy",
     "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
-    "mp_genome_stats", "mp_genome_reset", "mp_genome_destroy",
+    "mp_genome_stats", "mp_genome_download", "mp_genome_reset", "mp_genome_destroy",
     "mp_search_create", "mp_search_set_options", "mp_search_set_stage_timing", "mp_search_set_scan_timing", "mp_search_run",
     "mp_search_enqueue", "mp_search_complete", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
     "mp_search_last_stats", "mp_search_regrowths", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
@@ -39,7 +39,7 @@ EXPORTS = (
     "mp_comm_unique_id", "mp_comm_create", "mp_comm_gather_hits", "mp_comm_destroy",
     "mp_fasta_load", "mp_fasta_load_parallel", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record_ascii", "mp_fasta_record", "mp_fasta_destroy",
     "mp_format_hits",
-    "mp_sts_parse", "mp_sts_info", "mp_sts_arrays", "mp_sts_destroy",
+    "mp_sts_parse", "mp_sts_info", "mp_sts_arrays", "mp_sts_record_texts", "mp_sts_destroy",
 )
 
 
@@ -92,6 +92,7 @@ def _sig(lib):
     lib.mp_genome_put_device.argtypes = [P, c_uint32, c_uint64, P, c_uint64, P]
     lib.mp_genome_seal.argtypes = [P, P]
     lib.mp_genome_stats.argtypes = [P, u64p, u64p, u64p]
+    lib.mp_genome_download.argtypes = [P, P, P, P, P, P]
     lib.mp_genome_reset.argtypes = [P, c_uint32, P]
     lib.mp_genome_destroy.argtypes = [P]
     lib.mp_genome_destroy.restype = None
@@ -136,6 +137,7 @@ def _sig(lib):
     lib.mp_sts_parse.argtypes = [c_char_p, c_int32, ctypes.c_int64, POINTER(c_void_p)]
     lib.mp_sts_info.argtypes = [P, POINTER(c_int32), u64p]
     lib.mp_sts_arrays.argtypes = [P, POINTER(c_void_p)]
+    lib.mp_sts_record_texts.argtypes = [P, POINTER(c_void_p), POINTER(c_void_p), u64p]
     lib.mp_sts_destroy.argtypes = [P]
     lib.mp_sts_destroy.restype = None
     lib.mp_format_hits.argtypes = [P, c_uint64, P, P, c_uint32, P, P, c_uint32, P, c_uint64, u64p]
@@ -265,6 +267,18 @@ class Genome:
         a, b, c = c_uint64(), c_uint64(), c_uint64()
         check(lib().mp_genome_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return {"bases": a.value, "exc_runs": b.value, "dev_bytes": c.value}
+
+    def download(self):
+        """(g2, gexc, ginv, xr_start, xr_char) of the sealed genome (diagnostic, tests)."""
+        total = int(sum((int(n) + 63) // 64 * 64 for n in self.lengths))
+        n_xr = self.stats()["exc_runs"]
+        g2 = np.empty(total // 32, dtype=np.uint64)
+        ge = np.empty(total // 64, dtype=np.uint64)
+        gi = np.empty(total // 64, dtype=np.uint64)
+        xs = np.empty(max(n_xr, 1), dtype=np.uint64)
+        xc = np.empty(max(n_xr, 1), dtype=np.uint8)
+        check(lib().mp_genome_download(self._h, ptr(g2), ptr(ge), ptr(gi), ptr(xs), ptr(xc)))
+        return g2, ge, gi, xs[:n_xr], xc[:n_xr]
 
     def close(self):
         if self._h:
@@ -497,7 +511,13 @@ def sts_parse(path: str, wordsize: int, default_pcr_size: int):
             return np.ctypeslib.as_array(ctypes.cast(ptrs[i], POINTER(np.ctypeslib.as_ctypes_type(dtype))),
                                          shape=(count,)).copy()
 
+        tp, op, nb = c_void_p(), c_void_p(), c_uint64()
+        check(lib().mp_sts_record_texts(h, ctypes.byref(tp), ctypes.byref(op), ctypes.byref(nb)))
+        rec_text = (np.ctypeslib.as_array(ctypes.cast(tp, POINTER(ctypes.c_uint8)), shape=(nb.value,)).copy()
+                    if nb.value else np.zeros(0, dtype=np.uint8))
+        rec_off = np.ctypeslib.as_array(ctypes.cast(op, POINTER(ctypes.c_uint64)), shape=(n + 1,)).copy()
         return {"status": st.value, "n": n, "bad_line": cnt[1], "short": cnt[2], "ambig": cnt[3],
+                "rec_text": rec_text, "rec_text_off": rec_off,
                 "badsize": cnt[4], "max_pcr_size": cnt[5],
                 "key": arr(0, np.uint32, n), "hash_off": arr(1, np.uint32, n), "pcr_size": arr(2, np.uint64, n),
                 "line": arr(3, np.uint64, n), "direct": arr(4, np.uint8, n), "text_idx": arr(5, np.uint32, n),
@@ -574,10 +594,16 @@ def _csr(items):
 class Formatter:
     """Output-line formatter over fixed label and record texts (mp_format_hits)."""
 
-    def __init__(self, labels, rec_texts):
+    def __init__(self, labels, rec_texts, rec_off=None):
+        """rec_texts: one str per record, or (rec_off given) their UTF-8 bytes concatenated
+        as a uint8 array with len + 1 offsets."""
         self.labels, self.label_off = _csr(labels)
-        self.rec, self.rec_off = _csr(rec_texts)
-        self.n_seq, self.n_rec = len(labels), len(rec_texts)
+        if rec_off is None:
+            self.rec, self.rec_off = _csr(rec_texts)
+        else:
+            self.rec = np.ascontiguousarray(rec_texts, dtype=np.uint8)
+            self.rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+        self.n_seq, self.n_rec = len(labels), len(self.rec_off) - 1
 
     def __call__(self, hits: np.ndarray) -> bytes:
         hits = np.ascontiguousarray(hits, dtype=HIT_DTYPE)

@@ -60,6 +60,131 @@ _IUPAC_SETS = {"A": "A", "C": "C", "G": "G", "T": "TU", "U": "TU", "R": "AGR", "
                "D": "AGTURKWD", "H": "ACTUYMWH", "V": "ACGRMSV", "N": "ACGTURYMKSWBDHVN"}
 
 
+class _LazyRecords(list):
+    """``sts_records`` of a natively parsed STS file: a real list (the reference's
+    ``List[STSRecord]``, engine.py:62) whose STSRecord objects are built from the parser's
+    arrays on first use -- any read or write of the list.  The device search, the table
+    build and the formatter read the arrays and never touch it, so a CLI run builds no
+    record object (200k of them took 0.6 s for 100k STS)."""
+
+    __slots__ = ("_src", "_n", "_mutated")
+
+    def __init__(self, src, n: int):
+        super().__init__()
+        self._src = src  # _NativeRecords, shared with the table view; None once built
+        self._n = n
+        self._mutated = False
+
+    def _ready(self):
+        if self._src is not None:
+            src, self._src = self._src, None
+            src.materialize()
+
+    def native_len(self):
+        """Record count without building the records (None after a mutation)."""
+        if self._src is not None:
+            return self._n
+        return None if self._mutated else list.__len__(self)
+
+    def __reduce__(self):  # pickles as the plain list
+        self._ready()
+        return (list, (list(list.__iter__(self)),))
+
+
+class _LazyTable(dict):
+    """``sts_table`` of a natively parsed STS file: a real dict (engine.py:63) of key ->
+    bucket list, holding the same record objects as ``sts_records``, filled on first use."""
+
+    __slots__ = ("_src",)
+
+    def __init__(self, src):
+        super().__init__()
+        self._src = src
+
+    def _ready(self):
+        if self._src is not None:
+            src, self._src = self._src, None
+            src.materialize()
+
+    def __reduce__(self):
+        self._ready()
+        return (dict, (dict(dict.items(self)),))
+
+
+def _wrap(cls, base, names, mutating):
+    for name in names:
+        fn = getattr(base, name)
+
+        def method(self, *a, __fn=fn, **k):
+            self._ready()
+            if mutating and hasattr(self, "_mutated"):
+                self._mutated = True
+            return __fn(self, *a, **k)
+
+        method.__name__ = name
+        setattr(cls, name, method)
+
+
+_wrap(_LazyRecords, list, ("__len__", "__getitem__", "__iter__", "__reversed__", "__contains__", "__eq__",
+                           "__ne__", "__lt__", "__le__", "__gt__", "__ge__", "__add__", "__mul__", "__rmul__",
+                           "__repr__", "index", "count", "copy"), False)
+_wrap(_LazyRecords, list, ("__setitem__", "__delitem__", "__iadd__", "__imul__", "append", "extend", "insert",
+                           "pop", "remove", "sort", "reverse", "clear"), True)
+_wrap(_LazyTable, dict, ("__len__", "__getitem__", "__iter__", "__reversed__", "__contains__", "__eq__", "__ne__",
+                         "__repr__", "__or__", "__ror__", "get", "keys", "values", "items", "copy",
+                         "__setitem__", "__delitem__", "__ior__", "setdefault", "pop", "popitem", "update",
+                         "clear"), False)
+
+
+class _NativeRecords:
+    """The parser's arrays behind a lazy ``sts_records`` / ``sts_table`` pair; builds the
+    STSRecord objects (and the buckets, in file order) once, into both containers."""
+
+    def __init__(self, r):
+        self.r = r
+        self.recs = None
+        self.table = None
+        self._blob = None
+
+    def materialize(self):
+        r, recs, table = self.r, self.recs, self.table
+        if r is None:
+            return
+        self.r = None
+        p1s = r["p1"].tobytes().decode("ascii")
+        p2s = r["p2"].tobytes().decode("ascii")
+        p1o, p2o = r["p1_off"].tolist(), r["p2_off"].tolist()
+        text, to = r["text"].tobytes(), r["text_off"].tolist()
+        if text.isascii():
+            ts = text.decode("ascii")
+            items = [ts[to[i]:to[i + 1]] for i in range(len(to) - 1)]
+        else:
+            items = [text[to[i]:to[i + 1]].decode("utf-8") for i in range(len(to) - 1)]
+        out = []
+        tab = {}
+        for i, (ti, size, line, hoff, d, key) in enumerate(zip(
+                r["text_idx"].tolist(), r["pcr_size"].tolist(), r["line"].tolist(), r["hash_off"].tolist(),
+                r["direct"].tolist(), r["key"].tolist())):
+            rec = STSRecord(items[2 * ti], p1s[p1o[i]:p1o[i + 1]], p2s[p2o[i]:p2o[i + 1]], size,
+                            items[2 * ti + 1], line, hoff, "+" if d == 43 else "-")
+            out.append(rec)
+            b = tab.get(key)
+            if b is None:
+                tab[key] = [rec]
+            else:
+                b.append(rec)
+        list.extend(recs, out)
+        dict.update(table, tab)
+        recs._src = None
+        table._src = None
+
+    def record_texts(self):
+        """UTF-8 "id\\talias\\t(direct)" of every record, concatenated, and offsets: the
+        formatter's record column (engine.py:437-443), built by the parser
+        (mp_sts_record_texts)."""
+        return self._blob
+
+
 class MerPCR:
     """Electronic-PCR STS search (reference: core/engine.py:44)."""
 
@@ -168,33 +293,16 @@ class MerPCR:
         if r["status"] == _native.MP_STS_PYTHON:
             return None
         n = r["n"]
-        p1s = r["p1"].tobytes().decode("ascii")
-        p2s = r["p2"].tobytes().decode("ascii")
-        p1o, p2o = r["p1_off"].tolist(), r["p2_off"].tolist()
-        text, to = r["text"].tobytes(), r["text_off"].tolist()
-        if text.isascii():
-            ts = text.decode("ascii")
-            items = [ts[to[i]:to[i + 1]] for i in range(len(to) - 1)]
-        else:
-            items = [text[to[i]:to[i + 1]].decode("utf-8") for i in range(len(to) - 1)]
-        keys = r["key"].tolist()
-        table = self.sts_table
-        recs = self.sts_records
-        for i, (ti, size, line, hoff, d, key) in enumerate(zip(
-                r["text_idx"].tolist(), r["pcr_size"].tolist(), r["line"].tolist(), r["hash_off"].tolist(),
-                r["direct"].tolist(), keys)):
-            rec = STSRecord(items[2 * ti], p1s[p1o[i]:p1o[i + 1]], p2s[p2o[i]:p2o[i + 1]], size,
-                            items[2 * ti + 1], line, hoff, "+" if d == 43 else "-")
-            recs.append(rec)
-            b = table.get(key)
-            if b is None:
-                table[key] = [rec]
-            else:
-                b.append(rec)
-        self._sts_keys = keys
+        # the record objects are built lazily (_LazyRecords): the search path reads the arrays
+        src = _NativeRecords(r)
+        src._blob = (r["rec_text"], r["rec_text_off"])
+        src.recs = self.sts_records = _LazyRecords(src, n)
+        src.table = self.sts_table = _LazyTable(src)
+        self._sts_src = src
+        self._sts_keys = r["key"].tolist()
         self.max_pcr_size = r["max_pcr_size"]
-        self._native_arrays = (recs, n, (r["key"], r["hash_off"], r["pcr_size"], r["p1"], r["p1_off"],
-                                         r["p2"], r["p2_off"]))
+        self._native_arrays = (self.sts_records, n, (r["key"], r["hash_off"], r["pcr_size"], r["p1"], r["p1_off"],
+                                                     r["p2"], r["p2_off"]))
         if r["status"] == _native.MP_STS_BAD_LINE:
             logger.error(f"Bad STS file format at line {r['bad_line']}. Expected at least 4 fields.")
             return False
@@ -257,7 +365,7 @@ class MerPCR:
         if badsize:
             logger.warning(f"{badsize} STSs have a primer length sum greater than the pcr size: "
                            "expected pcr size adjusted")
-        logger.info(f"Loaded {len(self.sts_records)} STS records in {time.time() - start:.2f} seconds")
+        logger.info(f"Loaded {self._n_records()} STS records in {time.time() - start:.2f} seconds")
         return True
 
     def _parse_pcr_size(self, pcr_size_str: str) -> int:
@@ -353,11 +461,24 @@ class MerPCR:
         return MPParams(self.wordsize, self.margin, self.mismatches, self.three_prime_match,
                         self.iupac_mode)
 
+    def _n_records(self) -> int:
+        """len(sts_records), without building a lazy list's records."""
+        recs = self.sts_records
+        n = recs.native_len() if isinstance(recs, _LazyRecords) else None
+        return len(recs) if n is None else n
+
+    def _native_current(self) -> bool:
+        """sts_records is still exactly what the native parser produced."""
+        na = getattr(self, "_native_arrays", None)
+        recs = self.sts_records
+        return (na is not None and na[0] is recs and isinstance(recs, _LazyRecords) and not recs._mutated
+                and recs.native_len() == na[1])
+
     def _table_arrays(self):
         """Record arrays for mp_table_create in sts_records order."""
         recs = self.sts_records
         na = getattr(self, "_native_arrays", None)
-        if na is not None and na[0] is recs and na[1] == len(recs):
+        if self._native_current():
             return na[2]
         if len(self._sts_keys) != len(recs):
             self._sts_keys = [self._hash_value(r.primer1)[1] for r in recs]
@@ -377,7 +498,7 @@ class MerPCR:
     def device_table(self):
         """The seed table resident on this engine's GPU (rebuilt when stale)."""
         from .. import _native
-        sig = (id(self.sts_records), len(self.sts_records), self.wordsize, self.margin,
+        sig = (id(self.sts_records), self._n_records(), self._native_current(), self.wordsize, self.margin,
                self.mismatches, self.three_prime_match, self.iupac_mode, self.device)
         if self._dev_table is None or self._dev_table_sig != sig:
             self._dev_table = _native.Table(self._params(), self.device, *self._table_arrays())
@@ -559,9 +680,22 @@ class MerPCR:
     def format_bytes(self, fasta_records: Sequence[FASTARecord], hits: np.ndarray) -> bytes:
         """The output text of engine.py:437-443 for `hits`, UTF-8, by mp_format_hits."""
         from .. import _native
-        fmt = _native.Formatter([r.label for r in fasta_records],
-                                [f"{r.id}\t{r.alias}\t({r.direct})" for r in self.sts_records])
-        return fmt(hits)
+        return _native.Formatter([r.label for r in fasta_records], *self._record_texts())(hits)
+
+    def _record_texts(self):
+        """The formatter's record column (UTF-8 "id\talias\t(direct)" per record, and
+        offsets), cached until sts_records changes: from the parser's bytes while the records
+        are the native parser's, else from the record objects."""
+        if self._native_current():
+            return self._sts_src.record_texts()
+        recs = self.sts_records
+        key = (id(recs), len(recs))
+        cache = getattr(self, "_rec_text_cache", None)
+        if cache is None or cache[0] != key or cache[1] is not recs:
+            from .._native import _csr
+            cache = (key, recs, _csr([f"{r.id}\t{r.alias}\t({r.direct})" for r in recs]))
+            self._rec_text_cache = cache
+        return cache[2]
 
     def format_hits(self, fasta_records: Sequence[FASTARecord], hits: np.ndarray) -> List[str]:
         """Output lines exactly as engine.py:437-443 prints them."""

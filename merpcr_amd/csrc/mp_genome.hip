@@ -2,32 +2,71 @@
 //
 // Stands in for the sequence strings that MerPCR.search walks per record
 // (src/merpcr/core/engine.py:373-411, upper-cased at engine.py:455) after
-// FASTALoader's character filter (src/merpcr/io/fasta.py:60).  One thread packs
-// one 64-base group: two 2-bit words, one ginv word and one gexc word, and lists
-// the heads of exception runs (maximal same-character stretches of non-ACGT
-// bases inside its put) for the sparse character index.
+// FASTALoader's character filter (src/merpcr/io/fasta.py:60).  pack_kernel turns each
+// 64-base group into two 2-bit words, one ginv word and one gexc word, and lists the
+// heads of exception runs (maximal same-character stretches of non-ACGT bases inside
+// its put) for the sparse character index.
 #include <algorithm>
 
 #include "mp_internal.h"
 
 namespace mp {
 
-__device__ __forceinline__ uint8_t dev_upcase(uint8_t c) {
-    return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c;
+// ---------------------------------------------------------------- byte classification
+// Four bytes at a time (SWAR).  Per byte b, u = upper-case(b) (a-z only, as str.upper() on
+// the ASCII letters; engine.py:455):
+//   2-bit code  A=0 C=1 G=2 T=U=3 (bits 2-3 xor bits 1-2 of the byte, case-blind), 0 for
+//               every other byte (an exception base reads as 'A' in the 2-bit plane)
+//   inv         u is not one of A/C/G/T/U: every W-mer through it is unseeded (engine.py:464-503)
+//   exc         u is not exactly A/C/G/T: the primer compare looks the character up
+// Bit 7 of each byte of the masks below carries the per-byte result.
+
+// 0x80 in each byte of v that is zero (exact: no carry crosses a byte)
+__device__ __forceinline__ uint32_t zbytes(uint32_t v) {
+    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+}
+// per-byte flags (bit 7 of each byte, byte 0 = first base) -> 4 bits, first base on top
+__device__ __forceinline__ uint32_t nib4(uint32_t m) {
+    const uint32_t t = m >> 7;
+    return ((t & 1u) << 3) | ((t >> 6) & 4u) | ((t >> 15) & 2u) | ((t >> 24) & 1u);
+}
+struct Cls4 {
+    uint32_t code8;  // the 4 bases' 2-bit codes, first base on top
+    uint32_t exc, inv;  // per-byte flags (bit 7)
+    uint32_t up;     // upper-cased bytes
+};
+__device__ __forceinline__ Cls4 classify4(uint32_t w) {
+    const uint32_t l = w | 0x20202020u;  // case-blind compare against the lower-case letters
+    const uint32_t acgt = zbytes(l ^ 0x61616161u) | zbytes(l ^ 0x63636363u) | zbytes(l ^ 0x67676767u) |
+                          zbytes(l ^ 0x74747474u);
+    const uint32_t acgtu = acgt | zbytes(l ^ 0x75757575u);
+    uint32_t c = ((w >> 2) ^ (w >> 1)) & 0x03030303u;
+    c &= (acgtu >> 7) * 3u;
+    Cls4 r;
+    r.code8 = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) | (c >> 24);
+    r.exc = ~acgt & 0x80808080u;
+    r.inv = ~acgtu & 0x80808080u;
+    const uint32_t t = w & 0x7F7F7F7Fu;  // a-z: t >= 0x61, t <= 0x7A and the byte is ASCII
+    const uint32_t lower = (t + 0x1F1F1F1Fu) & (0xFAFAFAFAu - t) & ~w & 0x80808080u;
+    r.up = w - (lower >> 2);
+    return r;
+}
+__device__ __forceinline__ uint32_t byte_of(uint4 v, uint32_t i) {  // byte i of 16, no register indexing
+    const uint32_t w = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);
+    return (w >> (8u * (i & 3u))) & 0xFFu;
 }
 
-// code in bits 0-1, exc in bit 2, inv in bit 3
-__device__ __forceinline__ uint32_t classify(uint8_t u) {
-    switch (u) {
-        case 'A': return 0u;
-        case 'C': return 1u;
-        case 'G': return 2u;
-        case 'T': return 3u;
-        case 'U': return 3u | 4u;
-        default: return 4u | 8u;
-    }
-}
-
+// Filtered sequence bytes -> the planes.  A wave packs a 4 KiB tile per iteration: four
+// 1 KiB pieces, each one coalesced 16-B load per lane, all four issued before any is used.
+// A lane classifies its 16 bytes (classify4); four neighbouring lanes make one 64-base group:
+// its two g2 words and its gexc / ginv words come together by shuffles and are stored by the
+// group's first lanes (contiguous in memory across the wave).  Heads of exception runs
+// (maximal stretches of one non-ACGT character inside this put) are listed for the sparse
+// character index with one wave-aggregated reservation per piece.  Bytes past nbytes are
+// padding (ambiguous, never a run head).  (The previous form, one thread per 64 bytes
+// through a 64-byte private array, ran at ~160 GB/s.)
+constexpr uint32_t kPackTile = 4096;
+constexpr uint32_t kPackPiece = 1024;
 __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ src, uint64_t nbytes,
                                                    uint64_t gstart, uint64_t* __restrict__ g2,
                                                    uint64_t* __restrict__ gexc,
@@ -37,87 +76,109 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ s
                                                    unsigned long long* __restrict__ xr_count,
                                                    uint64_t xr_cap, uint64_t xr_base,
                                                    unsigned long long* __restrict__ u_count) {
-    const uint64_t grp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t i0 = grp * 64;
-    const bool active = i0 < nbytes;
-    uint64_t w0 = 0, w1 = 0, exc = ~0ull, inv = ~0ull;
-    uint32_t heads = 0;
-    uint64_t headmask = 0;  // bit 63-i set at run heads
-    if (active) {
-        const uint32_t cnt = (uint32_t)min<uint64_t>(64, nbytes - i0);
-        uint8_t prev = 0;
-        bool prev_exc = false;
-        if (i0 > 0) {
-            prev = dev_upcase(src[i0 - 1]);
-            prev_exc = (classify(prev) & 4u) != 0;
-        }
-        uint8_t buf[64];
-        if (cnt == 64) {
-            const uint4* s4 = reinterpret_cast<const uint4*>(src + i0);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t q = lane & 3u;
+    const uint64_t n_tiles = (nbytes + kPackTile - 1) / kPackTile;
+    const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const bool vec_ok = (reinterpret_cast<uintptr_t>(src) & 15u) == 0;
+    uint32_t n_u = 0;
+    for (uint64_t tile = wave0; tile < n_tiles; tile += n_waves) {  // wave-uniform
+        const uint64_t t0 = tile * kPackTile;
+        uint4 v[4];
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const uint4 x = s4[v];
-                *reinterpret_cast<uint4*>(buf + 16 * v) = x;
-            }
-        } else {
-            for (uint32_t i = 0; i < 64; ++i) buf[i] = i < cnt ? src[i0 + i] : 0;
-        }
-        exc = 0;
-        inv = 0;
-#pragma unroll 8
-        for (uint32_t i = 0; i < 64; ++i) {
-            const uint8_t u = dev_upcase(buf[i]);
-            const uint32_t c = classify(u);
-            const bool pad = i >= cnt;
-            const uint64_t code = pad ? 0ull : (uint64_t)(c & 3u);
-            if (i < 32) w0 |= code << (62 - 2 * i);
-            else w1 |= code << (62 - 2 * (i - 32));
-            const bool e = pad || (c & 4u);
-            const bool v = pad || (c & 8u);
-            exc |= (uint64_t)e << (63 - i);
-            inv |= (uint64_t)v << (63 - i);
-            const bool head = !pad && (c & 4u) && (!prev_exc || prev != u);
-            headmask |= (uint64_t)head << (63 - i);
-            prev = u;
-            prev_exc = !pad && (c & 4u);
-        }
-        heads = __popcll(headmask);
-        const uint32_t nu = (uint32_t)__popcll(exc & ~inv & (cnt == 64 ? ~0ull : ~(~0ull >> cnt)));
-        if (nu) atomicAdd(u_count, (unsigned long long)nu);
-        const uint64_t gw = (gstart + i0) >> 5;
-        g2[gw] = w0;
-        g2[gw + 1] = w1;
-        gexc[(gstart + i0) >> 6] = exc;
-        ginv[(gstart + i0) >> 6] = inv;
-    }
-    // wave-aggregated reservation of run-index entries
-    const uint64_t ball = __ballot(heads > 0);
-    uint32_t incl = heads;
-    const int lane = threadIdx.x & 63;
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t o = t0 + (uint64_t)k * kPackPiece + (uint64_t)lane * 16u;
+            if (vec_ok && o + 16 <= nbytes) {
+                v[k] = *reinterpret_cast<const uint4*>(src + o);
+            } else {  // the put's ragged end (or an unaligned source): bytes, 0 past the end
+                uint32_t b[16];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    const uint32_t total = __shfl(incl, 63, 64);
-    unsigned long long wbase = 0;
-    if (ball) {
-        if (lane == 0) wbase = atomicAdd(xr_count, (unsigned long long)total);
-        wbase = __shfl(wbase, 0, 64);
-    }
-    if (heads) {
-        uint64_t out = xr_base + wbase + (incl - heads);
-        uint64_t m = headmask;
-        while (m) {
-            const int i = __clzll(m);  // position of the top set bit = base index
-            m &= ~(1ull << (63 - i));
-            if (out < xr_cap) {
-                xr_start[out] = gstart + i0 + (uint64_t)i;
-                xr_char[out] = dev_upcase(src[i0 + i]);
+                for (int j = 0; j < 16; ++j) b[j] = o + (uint64_t)j < nbytes ? src[o + j] : 0u;
+                v[k] = make_uint4(b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24, b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24,
+                                  b[8] | b[9] << 8 | b[10] << 16 | b[11] << 24,
+                                  b[12] | b[13] << 8 | b[14] << 16 | b[15] << 24);
             }
-            ++out;
+        }
+        // the byte before the tile (run heads continue across tiles, not across puts)
+        uint32_t prev_up = 0, prev_exc = 0;
+        if (t0 > 0) {
+            const Cls4 c = classify4((uint32_t)src[t0 - 1]);
+            prev_up = c.up & 0xFFu;
+            prev_exc = c.exc & 0x80u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t o = t0 + (uint64_t)k * kPackPiece + (uint64_t)lane * 16u;  // this lane's first byte
+            const Cls4 c0 = classify4(v[k].x), c1 = classify4(v[k].y), c2 = classify4(v[k].z), c3 = classify4(v[k].w);
+            const uint64_t left = o < nbytes ? nbytes - o : 0;
+            const uint32_t valid16 = left >= 16 ? 0xFFFFu : (0xFFFFu << (16u - (uint32_t)left)) & 0xFFFFu;
+            const uint32_t code32 = (c0.code8 << 24) | (c1.code8 << 16) | (c2.code8 << 8) | c3.code8;
+            uint32_t exc16 = (nib4(c0.exc) << 12) | (nib4(c1.exc) << 8) | (nib4(c2.exc) << 4) | nib4(c3.exc);
+            uint32_t inv16 = (nib4(c0.inv) << 12) | (nib4(c1.inv) << 8) | (nib4(c2.inv) << 4) | nib4(c3.inv);
+            exc16 |= ~valid16 & 0xFFFFu;  // padding: ambiguous
+            inv16 |= ~valid16 & 0xFFFFu;
+            n_u += (uint32_t)__popc(exc16 & ~inv16 & valid16);
+            // run heads: an exception byte whose predecessor (in this put) is not the same
+            // exception character
+            const uint32_t pu_l = (uint32_t)__shfl_up((int)(c3.up >> 24), 1, 64);
+            const uint32_t pe_l = (uint32_t)__shfl_up((int)(c3.exc >> 24), 1, 64);
+            const uint32_t pu0 = lane ? pu_l : prev_up, pe0 = lane ? pe_l : prev_exc;
+            const uint32_t h0 = c0.exc & ~(((c0.exc << 8) | pe0) & zbytes(c0.up ^ ((c0.up << 8) | pu0)));
+            const uint32_t h1 = c1.exc & ~(((c1.exc << 8) | (c0.exc >> 24)) & zbytes(c1.up ^ ((c1.up << 8) | (c0.up >> 24))));
+            const uint32_t h2 = c2.exc & ~(((c2.exc << 8) | (c1.exc >> 24)) & zbytes(c2.up ^ ((c2.up << 8) | (c1.up >> 24))));
+            const uint32_t h3 = c3.exc & ~(((c3.exc << 8) | (c2.exc >> 24)) & zbytes(c3.up ^ ((c3.up << 8) | (c2.up >> 24))));
+            const uint32_t head16 = ((nib4(h0) << 12) | (nib4(h1) << 8) | (nib4(h2) << 4) | nib4(h3)) & valid16;
+            // the next piece's lane 0 continues from this piece's last byte (lane 63)
+            prev_up = (uint32_t)__shfl((int)(c3.up >> 24), 63, 64);
+            prev_exc = (uint32_t)__shfl((int)(c3.exc >> 24), 63, 64);
+            // one 64-base group per 4 lanes: g2 words from lanes q = 0, 2; flag words from q = 0
+            const uint32_t code_n = (uint32_t)__shfl_down((int)code32, 1, 64);
+            const uint32_t e1 = (uint32_t)__shfl_down((int)exc16, 1, 64), e2 = (uint32_t)__shfl_down((int)exc16, 2, 64),
+                           e3 = (uint32_t)__shfl_down((int)exc16, 3, 64);
+            const uint32_t i1 = (uint32_t)__shfl_down((int)inv16, 1, 64), i2 = (uint32_t)__shfl_down((int)inv16, 2, 64),
+                           i3 = (uint32_t)__shfl_down((int)inv16, 3, 64);
+            const uint64_t grp0 = o - (uint64_t)q * 16u;  // the group's first byte in the put
+            if (grp0 < nbytes) {
+                const uint64_t gb = gstart + grp0;
+                if ((q & 1u) == 0) g2[(gb >> 5) + (q >> 1)] = ((uint64_t)code32 << 32) | code_n;
+                if (q == 0) {
+                    gexc[gb >> 6] = ((uint64_t)exc16 << 48) | ((uint64_t)e1 << 32) | ((uint64_t)e2 << 16) | e3;
+                    ginv[gb >> 6] = ((uint64_t)inv16 << 48) | ((uint64_t)i1 << 32) | ((uint64_t)i2 << 16) | i3;
+                }
+            }
+            // wave-aggregated reservation of run-index entries (rare: N runs, IUPAC bases)
+            if (__any(head16 != 0u)) {
+                const uint32_t nh = (uint32_t)__popc(head16);
+                uint32_t incl = nh;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+                    if ((int)lane >= d) incl += y;
+                }
+                const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+                unsigned long long wbase = 0;
+                if (lane == 0) wbase = atomicAdd(xr_count, (unsigned long long)total);
+                wbase = (unsigned long long)__shfl((long long)wbase, 0, 64);
+                uint64_t out = xr_base + wbase + (incl - nh);
+                uint32_t m = head16;
+                const uint4 up = make_uint4(c0.up, c1.up, c2.up, c3.up);
+                while (m) {
+                    const uint32_t i = (uint32_t)__clz(m) - 16u;  // byte index, first base = bit 15
+                    m &= ~(0x8000u >> i);
+                    if (out < xr_cap) {
+                        xr_start[out] = gstart + o + i;
+                        xr_char[out] = (uint8_t)byte_of(up, i);
+                    }
+                    ++out;
+                }
+            }
         }
     }
+    // U bases seen (RNA input): one atomic per wave
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) n_u += (uint32_t)__shfl_xor((int)n_u, d, 64);
+    if (lane == 0 && n_u) atomicAdd(u_count, (unsigned long long)n_u);
 }
 
 // dir[b] = index of the last exception run starting at or before b << kDirShift.
@@ -172,8 +233,8 @@ static int put_device_bytes(Genome* g, uint32_t seq, uint64_t offset, const uint
         return fail(MP_E_ARG, "mp_genome_put: non-final chunk must be a multiple of 64 bytes");
     if (!nbytes) return MP_OK;
     g->sealed = false;
-    const uint64_t groups = (nbytes + 63) / 64;
-    const uint32_t blocks = (uint32_t)((groups + 255) / 256);
+    const uint64_t tiles = (nbytes + kPackTile - 1) / kPackTile;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((tiles + 3) / 4, 8192);  // 4 waves per block
     // first pass: pack + count runs; grow the run index and redo on overflow
     for (int attempt = 0; attempt < 2; ++attempt) {
         MP_HIP_CHECK(hipMemsetAsync(g->d_counter, 0, sizeof(unsigned long long), st));
@@ -339,6 +400,20 @@ MP_EXPORT int mp_genome_stats(void* genome, uint64_t* total_bases, uint64_t* n_e
     }
     if (n_exc_runs) *n_exc_runs = g->n_xr;
     if (dev_bytes) *dev_bytes = g->dev_bytes;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_genome_download(void* genome, uint64_t* g2, uint64_t* gexc, uint64_t* ginv, uint64_t* xr_start,
+                                 uint8_t* xr_char) {
+    Genome* g = (Genome*)genome;
+    if (!g) return fail(MP_E_ARG, "mp_genome_download: null genome");
+    if (!g->sealed) return fail(MP_E_STATE, "mp_genome_download: genome not sealed");
+    MP_HIP_CHECK(hipSetDevice(g->device));
+    if (g2) MP_HIP_CHECK(hipMemcpy(g2, g->g2, g->total / 32 * 8, hipMemcpyDeviceToHost));
+    if (gexc) MP_HIP_CHECK(hipMemcpy(gexc, g->gexc, g->total / 64 * 8, hipMemcpyDeviceToHost));
+    if (ginv) MP_HIP_CHECK(hipMemcpy(ginv, g->ginv, g->total / 64 * 8, hipMemcpyDeviceToHost));
+    if (xr_start && g->n_xr) MP_HIP_CHECK(hipMemcpy(xr_start, g->xr_start, g->n_xr * 8, hipMemcpyDeviceToHost));
+    if (xr_char && g->n_xr) MP_HIP_CHECK(hipMemcpy(xr_char, g->xr_char, g->n_xr, hipMemcpyDeviceToHost));
     return MP_OK;
 }
 

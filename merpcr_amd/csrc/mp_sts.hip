@@ -35,6 +35,8 @@ struct Sts {
     std::vector<uint8_t> direct;  // '+' or '-'
     std::vector<uint8_t> p1, p2, text;
     std::vector<uint64_t> p1_off{0}, p2_off{0}, text_off{0};  // text: id0, alias0, id1, ...
+    std::vector<uint8_t> rtext;       // mp_sts_record_texts, built on first request
+    std::vector<uint64_t> rtext_off;
 };
 
 // Python int() of an ASCII field: surrounding whitespace, optional sign, decimal digits
@@ -287,6 +289,45 @@ MP_EXPORT int mp_sts_arrays(void* sts, const void** ptrs) {
                        s->text_idx.data(), s->p1.data(), s->p1_off.data(), s->p2.data(), s->p2_off.data(),
                        s->text.data(), s->text_off.data()};
     std::memcpy(ptrs, v, sizeof(v));
+    return MP_OK;
+}
+
+MP_EXPORT int mp_sts_record_texts(void* sts, const uint8_t** text, const uint64_t** off, uint64_t* n_bytes) {
+    Sts* s = (Sts*)sts;
+    if (!s || !text || !off || !n_bytes) return fail(MP_E_ARG, "mp_sts_record_texts: null pointer");
+    const size_t n = s->key.size();
+    if (s->rtext_off.size() != n + 1) {
+        try {
+            s->rtext_off.assign(n + 1, 0);
+            uint64_t tot = 0;
+            for (size_t i = 0; i < n; ++i) {
+                const uint32_t t = s->text_idx[i];
+                tot += (s->text_off[2 * t + 2] - s->text_off[2 * t]) + 5;  // id \t alias \t ( d )
+                s->rtext_off[i + 1] = tot;
+            }
+            s->rtext.resize(tot);
+            uint8_t* o = s->rtext.data();
+            for (size_t i = 0; i < n; ++i) {
+                const uint32_t t = s->text_idx[i];
+                const uint64_t a0 = s->text_off[2 * t], a1 = s->text_off[2 * t + 1], a2 = s->text_off[2 * t + 2];
+                std::memcpy(o, s->text.data() + a0, a1 - a0);
+                o += a1 - a0;
+                *o++ = '\t';
+                std::memcpy(o, s->text.data() + a1, a2 - a1);
+                o += a2 - a1;
+                *o++ = '\t';
+                *o++ = '(';
+                *o++ = s->direct[i];
+                *o++ = ')';
+            }
+        } catch (const std::bad_alloc&) {
+            s->rtext_off.clear();
+            return fail(MP_E_NOMEM, "mp_sts_record_texts: out of host memory");
+        }
+    }
+    *text = s->rtext.data();
+    *off = s->rtext_off.data();
+    *n_bytes = s->rtext.size();
     return MP_OK;
 }
 

@@ -14,6 +14,7 @@ import os
 import random
 import time
 
+import numpy as np
 import pytest
 
 from merpcr_amd import MerPCR, _native
@@ -118,3 +119,40 @@ def test_invalid_utf8_raises(tmp_path):
     p.write_bytes(b"A\tACGTACGTACGT\tACGTACGTACGT\t200\t\xff\n")
     with pytest.raises(UnicodeDecodeError):
         MerPCR(wordsize=8).load_sts_file(str(p))
+
+
+def test_lazy_records_and_record_texts(tmp_path):
+    """A native load builds no STSRecord until sts_records / sts_table are used; the
+    formatter's record column then comes from the parser's bytes and equals the
+    f"{id}\\t{alias}\\t({direct})" text of the built records; any mutation of the list makes
+    the engine rebuild its arrays from the objects."""
+    import copy
+    import pickle
+
+    from merpcr_amd._native import _csr
+    rng = random.Random(7)
+    p = tmp_path / "a.sts"
+    p.write_text("".join(f"S{i}\t{_primer(rng, 11)}\t{_primer(rng, 11)}\t{rng.choice([s for s in SIZES if s.strip()])}\t"
+                         f"{rng.choice(['al', 'ſ x', ''])}\n" for i in range(300)))
+    eng = MerPCR(wordsize=11)
+    assert eng.load_sts_file(str(p))
+    assert eng.sts_records._src is not None and eng.sts_table._src is not None
+    n = eng._n_records()
+    arrays = eng._table_arrays()
+    blob, off = eng._record_texts()
+    assert eng.sts_records._src is not None, "the search path built the records"
+    assert len(eng.sts_records) == n
+    assert eng.sts_table._src is None  # one build fills both
+    want = _csr([f"{r.id}\t{r.alias}\t({r.direct})" for r in eng.sts_records])
+    assert np.array_equal(blob, want[0]) and np.array_equal(off, want[1])
+    assert sum(len(v) for v in eng.sts_table.values()) == n
+    ids = {id(r) for v in eng.sts_table.values() for r in v}
+    assert ids == {id(r) for r in eng.sts_records}
+    assert type(pickle.loads(pickle.dumps(eng.sts_records))) is list
+    assert copy.deepcopy(eng.sts_records) == list(eng.sts_records)
+    assert eng._native_current() and eng._table_arrays() is arrays
+    eng.sts_records.append(eng.sts_records[0])
+    assert not eng._native_current()
+    assert eng._n_records() == n + 1
+    blob2, off2 = eng._record_texts()
+    assert len(off2) == n + 2
