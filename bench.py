@@ -316,6 +316,8 @@ def main():
                          "one-GPU box); the JSON line is then not the metric")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one search handle: every step waits for the previous one (no run queued ahead)")
+    ap.add_argument("--one-stream", action="store_true",
+                    help="pipelined handles share one stream (no kernel of step i+1 overlaps step i)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time only rank 0's owned range of an N-way split on this one GPU "
                          "(no collective); the JSON line is then not the metric")
@@ -386,6 +388,10 @@ def main():
     # handle's next run waits (on the device) for its gather to have sent the hits.
     nbuf = 1 if args.no_pipeline else 2
     handles = [search] + [_native.Search(table, genome) for _ in range(nbuf - 1)]
+    # one stream per handle (--one-stream: all on the default stream): step i+1's scan may then
+    # start on the CUs that step i's latency-bound tail / pair / order kernels leave idle
+    streams = [torch.cuda.current_stream()] + [
+        torch.cuda.current_stream() if args.one_stream else torch.cuda.Stream(device=dev) for _ in range(nbuf - 1)]
     gstream = torch.cuda.Stream(device=dev) if comm is not None else None
     gdone = [None] * nbuf
     scan_ms = []
@@ -430,16 +436,15 @@ def main():
     def run_steps(k):
         """k steps, pipelined; returns the last step's job-wide hit count."""
         pend, total = None, 0
-        cur = torch.cuda.current_stream()
         for i in range(k):
             j = i % nbuf
             if pend == j:
                 total = finish(pend)
                 pend = None
             if gdone[j] is not None:  # its previous run's hits are still being sent
-                cur.wait_event(gdone[j])
+                streams[j].wait_event(gdone[j])
                 gdone[j] = None
-            handles[j].enqueue(rng, stream)
+            handles[j].enqueue(rng, streams[j].cuda_stream)
             if pend is not None:
                 total = finish(pend)
             pend = j
@@ -447,10 +452,13 @@ def main():
             total = finish(pend)
         return total
 
-    # Timed steps: no per-stage events (each idles the GPU ~6 us).  At N = 1 the scan kernel's
-    # own two events stay (roofline.achieved, HIP events on the launch stream, every timed
-    # step); sharded and multi-rank runs time the scan in the untimed step after them.
-    scan_in_timed = world == 1 and args.shard_of <= 1
+    # Timed steps: no per-stage events (each idles the GPU ~6 us).  The scan kernel's own two
+    # events (roofline.achieved: HIP events on its launch stream) stay in the timed steps only
+    # when no kernel of another step can run beside it (one stream, N = 1): with two streams
+    # step i+1's scan overlaps step i's tail / pair / order, and the events would time both.
+    # Otherwise the scan is timed in three untimed steps after the timed ones, one at a time
+    # on one stream, on the same resident data.
+    scan_in_timed = (nbuf == 1 or args.one_stream) and world == 1 and args.shard_of <= 1
     for h in handles:
         h.set_stage_timing(False)
         h.set_scan_timing(scan_in_timed)
@@ -466,22 +474,19 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     timed_scan_ms = list(scan_ms)
-    # untimed: one more step with every stage timed (the stage breakdown; the scan time too
-    # when the timed steps carried no events)
-    search.set_stage_timing(True)
+    # untimed: three more steps of handle 0 alone (the scan time when the timed steps carried
+    # no events), the last with every stage timed (the stage breakdown)
+    torch.cuda.synchronize()
+    for j in range(nbuf):
+        gdone[j] = None
     search.set_scan_timing(True)
     scan_ms.clear()
-    for j in range(1, nbuf):
-        if gdone[j] is not None:
-            torch.cuda.current_stream().wait_event(gdone[j])
-            gdone[j] = None
-    gdone_keep = gdone[0]
-    if gdone_keep is not None:
-        torch.cuda.current_stream().wait_event(gdone_keep)
+    for u in range(3):
+        search.set_stage_timing(u == 2)
+        search.enqueue(rng, stream)
+        finish(0)
+        torch.cuda.synchronize()
         gdone[0] = None
-    search.enqueue(rng, stream)
-    finish(0)
-    torch.cuda.synchronize()
     if not timed_scan_ms:
         timed_scan_ms = list(scan_ms)
     scan_ms = timed_scan_ms
@@ -559,10 +564,13 @@ def main():
                      "alg_bytes_per_launch": int(alg_bytes),
                      "issue": (dict(issue_bound(pmc), source=f"profiles/{pmc_tag}_pmc.json") if pmc else None)},
         "setup_s": round(setup_s, 2),
-        "pipeline": (f"{nbuf} search handles: step i+1 enqueued before the host waits for step i "
-                     "(mp_search_enqueue/complete)" if nbuf > 1 else "none: each step waits for the previous"),
-        "scan_timing": ("HIP events around the scan kernel in every timed step" if scan_in_timed else
-                        "HIP events around the scan kernel in one untimed step after the timed ones"),
+        "pipeline": (f"{nbuf} search handles on {'one stream' if args.one_stream else f'{nbuf} streams'}: step i+1 "
+                     "enqueued before the host waits for step i (mp_search_enqueue/complete)"
+                     if nbuf > 1 else "none: each step waits for the previous"),
+        "scan_timing": ("HIP events around the scan kernel on its launch stream in every timed step"
+                        if scan_in_timed else
+                        "HIP events around the scan kernel on its launch stream in 3 untimed steps after the "
+                        "timed ones, run one at a time (in the timed steps kernels of consecutive steps overlap)"),
     }
     if args.shard_of > 1:
         out["diagnostic"] = f"rank 0 of a {args.shard_of}-way owned-range split, alone on one GPU (not the metric)"

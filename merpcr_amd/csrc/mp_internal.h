@@ -132,6 +132,7 @@ struct Table {
     int h16 = 0;                  // many heads need plain/never masks (IUPAC primers): 16-B heads
     uint64_t* kgrp = nullptr;     // W 11..13: key groups, one u64 per 16 keys (see kKgrpKeys)
     uint32_t kgrp_F = 0;          // primer-1 bases W..W+F-1 a key-group field holds (0: no key groups)
+    int kgrp_wild = 0;            // I = 1 field form: two 24-bit fields with the non-plain bases marked
     uint2* binfo = nullptr;       // W <= kDenseMaxW: per key rank {first padded entry, records}
     uint16_t* dfilt = nullptr;    // W <= kDenseMaxW: 2-B filter word per padded entry (kDenseAlways...)
     uint2* dgrp = nullptr;        // W <= kDenseMaxW: per 32 keys {inline-bucket bits, first oct | any escape << 31}
@@ -211,6 +212,7 @@ struct Search {
     mp_search_options opt{};     // kernel-path selection (all zero = automatic)
     uint32_t pair_per_cu = 0;    // resident pair_kernel blocks per CU (occupancy query at create)
     uint32_t dense_per_cu = 0;   // resident dense_kernel blocks per CU
+    uint32_t sched_short = 4;    // super-steps per claim in short scans (MP_SCHUNK_SHORT, tuning)
     size_t dense_lds = 0;        // dense_kernel dynamic LDS bytes
     uint64_t n_regrowths = 0;    // list regrowths over the handle's life (tests)
     std::vector<SeqSpan> last_spans;        // spans on the device (a rerun of the same range uploads nothing)
@@ -360,6 +362,7 @@ __host__ __device__ __forceinline__ uint32_t lds_block_mask(uint32_t x, uint32_t
 constexpr uint32_t kKgrpKeys = 16;
 constexpr uint32_t kKgrpFields = 3;
 constexpr uint32_t kKgrpFlag = 0x8000u;
+constexpr uint32_t kKgrpWildFields = 2;  // I = 1 key groups: two 24-bit fields {codes, wild bases}
 
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {
     return d == 0 ? 0u : (d < 0 ? (uint32_t)(-2 * d - 1) : (uint32_t)(2 * d));
@@ -383,9 +386,9 @@ struct SortPlan {
 };
 constexpr uint32_t kSlotCap = 256;  // order mode 0: bucket slot capacity (~8x the planned mean)
 SortPlan sort_plan(const Search* s);
-// pair_kernel already wrote the packed keys (tmp_lo), the bucket counts and (its last block)
-// the bucket offsets/cursors; mode 0: the keys also in their bucket slots.  Hit count read
-// on the device; writes s->out.
+// pair_kernel already wrote the packed keys (tmp_lo) and the bucket counts; mode 0: the keys
+// also in their bucket slots.  Bucket offsets, then the sort.  Hit count read on the device;
+// writes s->out.
 int sort_hits_device(Search* s, hipStream_t st, int mode);
 uint32_t* sort_bucket_counts(Search* s);          // the bucket count array (zeroed by the scan kernels)
 uint32_t* sort_bucket_offsets(Search* s);         // nb + 1 offsets
@@ -410,9 +413,7 @@ __device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint3
 // total) and cursor[0..nb) = off.  The counts pass through LDS (s_v4: kOffTile counts) in
 // tiles: coalesced loads and stores, 8 consecutive counts per thread inside a tile, a wave
 // shuffle scan and one LDS word per wave (s_w: 16).  (64 consecutive counts per thread in
-// registers made every access a 64-line gather: c4's 65,536 buckets took 80 us.)  The
-// counts are read at device scope: pair_kernel's last block calls this right after the
-// other blocks' atomics.
+// registers made every access a 64-line gather: c4's 65,536 buckets took 80 us.)
 constexpr uint32_t kOffTile = 8192;
 __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32_t nb, uint32_t* off,
                                                      uint32_t* cursor, uint4* s_v4, uint32_t* s_w) {
@@ -423,7 +424,7 @@ __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32
 #pragma unroll
         for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
             const uint32_t i = j * 1024 + t;
-            s_v[i] = base + i < nb ? __hip_atomic_load(cnt + base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            s_v[i] = base + i < nb ? cnt[base + i] : 0u;
         }
         __syncthreads();
         uint4 q0 = s_v4[2 * t], q1 = s_v4[2 * t + 1];

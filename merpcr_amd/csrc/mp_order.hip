@@ -51,7 +51,7 @@ __global__ void bucket_hist(const uint64_t* __restrict__ hi, const uint64_t* __r
 }
 
 // exclusive scan of the bucket counts by one 1024-thread workgroup (bucket_offsets_block,
-// mp_internal.h): pair_kernel's last block runs it, so this kernel is only the unfused form.
+// mp_internal.h).
 __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restrict__ cnt, uint32_t nb,
                                                        uint32_t* __restrict__ off, uint32_t* __restrict__ cursor) {
     __shared__ uint4 s_v4[kOffTile / 4];
@@ -271,9 +271,14 @@ int sort_hits_device(Search* s, hipStream_t st, int mode) {
     const SortPlan P = sort_plan(s);
     const int arc = alloc_sort_buckets(s);
     if (arc) return arc;
-    const uint32_t* off = sort_bucket_offsets(s);
+    uint32_t* off = sort_bucket_offsets(s);
     uint32_t* cursor = sort_bucket_cursors(s);
     const Genome* g = s->genome;
+    // A separate launch, not pair_kernel's last block: publishing the counts inside the pair
+    // kernel needs an agent-scope release per block (buffer_wbl2 of the XCD's L2, several
+    // us each across the persistent grid), measured +65 us on a 1/8 c3 step.
+    hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, sort_bucket_counts(s), P.nb, off, cursor);
+    MP_HIP_CHECK(hipGetLastError());
     if (mode == 0) {
         hipLaunchKernelGGL(sort_decode_slots, dim3((P.nb + kSlotWaves - 1) / kSlotWaves), dim3(64 * kSlotWaves), 0, st,
                            s->slots, P.slot_cap, off, P.nb, P.try_bits, P.low_bits, g->d_base, g->d_len, g->n_seq,

@@ -24,6 +24,7 @@
 //      wave (primer_ok: bit-sliced accept planes, exception bases resolved through the
 //      run index; lanes split the amplicon-end offsets) and emit 128-bit order keys.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 
@@ -53,8 +54,10 @@ struct ScanArgs {
     const uint32_t* filt;   // W >= 14: hashed presence filter
     uint32_t filt_log2;
     const uint2* rk;        // W <= 13: rank bitmap
-    const uint2* kgrp;      // W 11..13, I = 0: key groups (u64 per 16 keys, see kKgrpKeys)
+    const uint2* kgrp;      // W 11..13: key groups (u64 per 16 keys, see kKgrpKeys)
     uint32_t kgrp_F;
+    int kgrp_wild;          // I = 1 field form (kgrp_pass)
+    uint32_t sched_short;   // super-steps per claim in short scans (SuperSched)
     const Entry* dents;     // W <= 13: bucket heads by rank
     const uint2* dents8;    // W <= 13: 8-B heads
     const uint4* dents16;   // W <= 13, Table::h16: 16-B heads (primers with IUPAC bases after the seed)
@@ -92,8 +95,6 @@ struct ScanArgs {
     uint64_t* sort_keys;
     uint32_t* sort_cnt;
     uint32_t sort_nb, sort_shift, sort_try_bits, sort_low_bits;
-    uint32_t* sort_off;     // pair_kernel's last block writes the bucket offsets / cursors here
-    uint32_t* sort_cursor;
     uint64_t* sort_slots;   // order mode 0: keys straight into their bucket slot (null: mode 1)
     uint32_t slot_cap;
 };
@@ -118,8 +119,7 @@ __device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x > 
 constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
 constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;  // pair_kernel batch counters, 8 x 256 B
 constexpr int kSchedBase = kPairQBase + 8 * kStatStride;  // scan super-step chunk counters, 8 x 256 B
-constexpr int kDoneBase = kSchedBase + 8 * kStatStride;   // pair_kernel blocks finished (fused offsets)
-constexpr size_t kCounterBytes = (size_t)(kDoneBase + kStatStride) * 8;
+constexpr size_t kCounterBytes = (size_t)(kSchedBase + 8 * kStatStride) * 8;
 #ifndef MP_PDYN_BATCH
 #define MP_PDYN_BATCH 64
 #endif
@@ -1236,9 +1236,25 @@ __device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, 
 // the group's first three present keys with a compact head, primer-1 bases W..W+F-1 (see
 // kKgrpKeys).  `pk`: the window's bases W..W+F-1 << 4 | the key's low 4 bits.  True = the
 // seed goes on.
+//
+// I = 1 tables (kgrp_wild): two 24-bit fields {2-bit codes of bases W..W+F-1; at the even
+// bits of the next 12, the bases that are not plain}.  The count covers the plain bases
+// only, so it is a lower bound on primer-1 mismatches when every genome base of the window's
+// first W + F is one of A/C/G/T/U (under I = 1 a genome IUPAC base may match anything, and
+// it reads as 'A' in the 2-bit plane); bit 31 of pk marks a window where that fails, which
+// then passes on presence alone.
 __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
     const uint32_t bit = pk & 15u;
     if (!((rw.x >> bit) & 1u)) return false;
+    if (a.kgrp_wild) {
+        if (pk >> 31) return true;
+        const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
+        if (j >= kKgrpWildFields) return true;
+        const uint64_t w64 = ((uint64_t)rw.y << 32) | rw.x;
+        const uint32_t field = (uint32_t)(w64 >> (16u + 24u * j));
+        const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
+        return (uint32_t)__popc((x | (x >> 1)) & 0x555u & ~(field >> 12)) <= (uint32_t)a.N;
+    }
     const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
     if (j >= kKgrpFields) return true;
     const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
@@ -1277,7 +1293,8 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
     uint32_t stride;           // 0: dynamic; else the static round-robin stride
     uint32_t chunk;            // super-steps per claim
     unsigned int* ctr;
-    __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint64_t n_supers, int w, int kW, int lane) {
+    __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint64_t n_supers, int w, int kW, int lane,
+                                              uint32_t short_chunk) {
         // short scans (under 64 super-steps per wave, e.g. c2) keep the static order: their
         // per-wave totals average out and the claims would only add latency
         const uint32_t waves = gridDim.x * (uint32_t)kW;
@@ -1286,7 +1303,7 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
             return (uint64_t)blockIdx.x * (uint64_t)kW + (uint64_t)w;
         }
         stride = 0;
-        chunk = n_supers < (uint64_t)waves * kSChunkShort ? (uint32_t)MP_SCHUNK_SHORT : kSChunk;
+        chunk = n_supers < (uint64_t)waves * kSChunkShort ? short_chunk : kSChunk;
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
         ctr = reinterpret_cast<unsigned int*>(counters + kSchedBase + x * kStatStride);
@@ -1341,7 +1358,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     SurvChunk TC{0, 64u, 0u};
 
     SuperSched sch;
-    uint64_t ss = sch.first(a.counters, n_supers, w, kWaves, lane);
+    uint64_t ss = sch.first(a.counters, n_supers, w, kWaves, lane, a.sched_short);
     // span of the super-step being prefetched, cached in registers (wave-uniform): the
     // common path of the prefetch issues only the four plane loads, no waits
     SeqSpan pf{};
@@ -1398,6 +1415,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // pass -- full lanes, all passes' rank-word loads in flight together -- and the
             // seeds are compacted back into the same arrays as {offset, rank}
             const uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
+            // I = 1 key groups: windows whose first W + F bases are not all A/C/G/T/U
+            const uint32_t fbad = (kRkf && a.kgrp_wild) ? ~window_ok_mask(R.iv, W + a.kgrp_F) : 0u;
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
@@ -1411,7 +1430,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         m &= ~(0x80000000u >> i);
                         if (qi - r0 < kSeedQR) {
                             if constexpr (kRkf) {  // the offset only: the probe shuffles the window from its lane
-                                L.rq.q[qi - r0] = (uint16_t)((uint32_t)lane * kLanePos + i);
+                                L.rq.q[qi - r0] = (uint16_t)(((uint32_t)lane * kLanePos + i) |
+                                                             (((fbad << i) >> 31) << 15));
                             } else {
                                 L.rq.r[qi - r0] = kmer_dyn(d0, d1, d2, i) >> shw;
                                 L.rq.q[qi - r0] = (uint16_t)((uint32_t)lane * kLanePos + i);
@@ -1436,14 +1456,16 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         if constexpr (kRkf) {
                             // bases [i, i + W + F) of window i of lane src: three shuffles of the
                             // lane's 48 bases; pk = the F filter bases << 4 | the key's low 4 bits
-                            po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
+                            const uint32_t qe = v ? (uint32_t)L.rq.q[e] : 0u;
+                            po[q] = qe & 0x7FFu;
                             const int sa = (int)((po[q] >> 5) << 2);
                             const uint32_t A = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d0);
                             const uint32_t B = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d1);
                             const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d2);
                             const uint32_t i = po[q] & 31u;
                             const uint32_t key = funnel3(A, B, C, i) >> shw;
-                            pk[q] = ((funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F)) << 4) | (key & 15u);
+                            pk[q] = ((funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F)) << 4) | (key & 15u) |
+                                    ((qe >> 15) << 31);
                             rw[q] = a.kgrp[v ? (key >> 4) : 0u];
                         } else {
                             pk[q] = v ? L.rq.r[e] : 0u;
@@ -1686,7 +1708,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     SurvChunk C{0, 64u, 0u};
 
     SuperSched sch;
-    uint64_t ss = sch.first(a.counters, n_supers, w, kDenseWaves, lane);
+    uint64_t ss = sch.first(a.counters, n_supers, w, kDenseWaves, lane, a.sched_short);
     SeqSpan pf{};
     pf.super0 = 1;
     uint64_t pf_end = 0, pf_sbase = 0;
@@ -2028,23 +2050,6 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     uint64_t off = s_base;
     for (int q = 0; q < w; ++q) off += s_st[q].n;
     write_hits(a, S, off, lane);
-    if (a.sort_off) {
-        // bucket_offsets fused: the last block to finish scans the bucket counts (every other
-        // block's count atomics precede its fence and its arrival), in the batch stages' LDS
-        __threadfence();
-        __syncthreads();
-        __shared__ uint32_t s_last;
-        if (threadIdx.x == 0)
-            s_last = atomicAdd(reinterpret_cast<unsigned int*>(&a.counters[kDoneBase]), 1u) == gridDim.x - 1u;
-        __syncthreads();
-        if (s_last) {
-            __threadfence();
-            static_assert(sizeof(s_pst) >= (kOffTile / 4) * sizeof(uint4) + 16 * sizeof(uint32_t), "offset tile fits");
-            uint4* tile = reinterpret_cast<uint4*>(&s_pst[0][0]);
-            bucket_offsets_block(a.sort_cnt, a.sort_nb, a.sort_off, a.sort_cursor, tile,
-                                 reinterpret_cast<uint32_t*>(tile + kOffTile / 4));
-        }
-    }
 }
 
 // The run's last kernel: counters[0..8) into the device-mapped pinned words the host polls
@@ -2055,8 +2060,10 @@ __global__ __launch_bounds__(1024) void finish_kernel(unsigned long long* __rest
     if (threadIdx.x < 8) v = counters[threadIdx.x];
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n_words; i += blockDim.x) counters[i] = 0ull;
-    if (threadIdx.x < 8) h_out[threadIdx.x] = v;
-    __threadfence_system();
+    if (threadIdx.x < 8) {
+        h_out[threadIdx.x] = v;
+        __threadfence_system();  // one wave: the host polls the run's event, then reads these
+    }
 }
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
@@ -2200,6 +2207,7 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
                                   (const void*)dense_kernel<2>, (const void*)dense_kernel<-1>})
                 (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->dense_lds);
         occ = 0;
+        if (const char* e = std::getenv("MP_SCHUNK_SHORT")) s->sched_short = (uint32_t)std::max(1, std::atoi(e));
         s->dense_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dense_kernel<1>, kDenseBlock, s->dense_lds) ==
                                hipSuccess && occ > 0) ? (uint32_t)occ : 1u;
         if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
@@ -2246,15 +2254,12 @@ static int set_lists(Search* s, ScanArgs& a, int mode) {
     a.tails_cap = s->tails_cap;
     a.sort_cnt = nullptr;
     a.sort_keys = nullptr;
-    a.sort_off = a.sort_cursor = nullptr;
     a.sort_slots = nullptr;
     a.sort_nb = a.sort_shift = a.sort_try_bits = a.sort_low_bits = a.slot_cap = 0;
     if (mode < 2) {  // after a hit-list regrowth too: the plan follows the capacity
         const SortPlan P = sort_plan(s);
         a.sort_cnt = sort_bucket_counts(s);
         a.sort_keys = s->tmp_lo;
-        a.sort_off = sort_bucket_offsets(s);
-        a.sort_cursor = sort_bucket_cursors(s);
         a.sort_nb = P.nb;
         a.sort_shift = P.shift;
         a.sort_try_bits = P.try_bits;
@@ -2271,7 +2276,7 @@ static int set_lists(Search* s, ScanArgs& a, int mode) {
 
 // Every kernel of one run, back to back on the stream with no host wait: scan -> fingerprint
 // survivors (+ bucket-tail references -> tail survivors) -> pair check -> hit keys and bucket
-// counts (+ offsets, from pair_kernel's last block) -> hit order (modes 0 and 1) ->
+// counts -> hit order (modes 0 and 1: bucket offsets, then the sort) ->
 // finish_kernel (counters into the mapped host words, then zeroed) -> the completion event.
 static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStream_t st, int mode) {
     Table* t = s->table;
@@ -2287,8 +2292,9 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     const bool dense = (uint32_t)t->prm.wordsize <= kDenseMaxW && !s->opt.no_dense;
     // level-2 filter of the filtered rank groups: I = 0 (the 2-bit mismatch count is then a
     // lower bound), compact 8-B heads (not h16)
-    const bool rkf = t->kgrp_F >= 2 && !t->h16 && a.I == 0 && !s->opt.no_rank_filter && t->filt_direct &&
-                     !t->lds_exact && a.W >= 11 && a.W <= 13;
+    // (I = 1: the field form with the non-plain bases marked, kgrp_wild)
+    const bool rkf = t->kgrp_F >= 2 && (a.I == 0 ? !t->h16 && !t->kgrp_wild : t->kgrp_wild != 0) &&
+                     !s->opt.no_rank_filter && t->filt_direct && !t->lds_exact && a.W >= 11 && a.W <= 13;
     const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
     if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
     if (dense) {
@@ -2306,13 +2312,13 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
     } else {
         if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
-        else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h16)
-            hipLaunchKernelGGL((scan_kernel<1, false, 2, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full && rkf)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h16)
+            hipLaunchKernelGGL((scan_kernel<1, false, 2, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
-        else if (t->filt_direct && a.defer_full && rkf)
+        else if (t->filt_direct && t->lds_k != 2 && a.defer_full && rkf)
             hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && a.defer_full && t->h16)
             hipLaunchKernelGGL((scan_kernel<1, false, 1, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -2534,7 +2540,7 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
         a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
         a.defer_full = t->defer_full && !s->opt.no_defer;
-        a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F;
+        a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F; a.kgrp_wild = t->kgrp_wild;
         a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.lfilt = t->lfilt;
         a.slots = t->slots; a.slot_log2 = t->slot_log2;
         a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
@@ -2542,6 +2548,7 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         a.W = t->prm.wordsize; a.M = t->prm.margin; a.N = t->prm.mismatches;
         a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
         a.g_lo = g_lo; a.g_hi = g_hi;
+        a.sched_short = s->sched_short;
         // keys over 64 bits, or a forced rocPRIM sort: mode 2
         const int mode = sort_hits_device_ok(s) ? s->order_mode : 2;
         s->pend_mode = mode;

@@ -7,6 +7,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstring>
 #include <unordered_map>
@@ -424,10 +425,12 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             t->h16 = W >= 10 && n_full16 * 20 < (uint64_t)nb && n_full8 * 20 >= (uint64_t)nb;
             if (t->h16) dents16.resize(std::max<uint32_t>(nb, 1));
             uint64_t n_full = 0;
+            std::vector<uint32_t> rank_bucket(std::max<uint32_t>(nb, 1));
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint32_t k = bkey[b];
                 const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
                 const Entry& e = ents[boff[b]];
+                rank_bucket[rank] = b;
                 dents[rank] = e;
                 // a full head names its bucket's first entry: the ranked drain can hand the whole
                 // bucket to tail_kernel without reading the 32-B head
@@ -452,7 +455,62 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             // key groups (kKgrpKeys keys per u64) for the scan's level-2 probe: it shuffles
             // bases [i, i + 17) of window i from the owning lane (i < 32 of its 48), so
             // F <= 17 - W, and a field holds <= 7 bases
-            if (W >= 11 && W <= 13) {
+            if (W >= 11 && W <= 13 && p.iupac_mode) {
+                // I = 1 (c4: degenerate primers): two 24-bit fields per group, one per present
+                // key, each the 2-bit codes of primer-1 bases W..W+F-1 (12 bits) and, at the
+                // even bit positions of the next 12, the bases that are not plain (an IUPAC
+                // base: any genome base may match it) -- skipped by the mismatch count.  A key
+                // with no field (a bucket of several records, a seed inside the primer, a
+                // primer shorter than W + F, or the third present key of the group) has every
+                // base marked: it always passes.
+                const uint32_t F = std::min<uint32_t>(6u, 17u - W);
+                t->kgrp_F = F;
+                const uint32_t m2 = (1u << (2 * F)) - 1u;
+                // expected pass rate of a random window's field test: P(<= N mismatches over
+                // the field's plain bases, each a mismatch with p = 3/4); absent fields pass
+                auto pass_rate = [&](uint32_t plain_bases) {
+                    double pr = 0.0, c = 1.0;
+                    for (uint32_t k = 0; k <= plain_bases && k <= (uint32_t)p.mismatches; ++k) {
+                        if (k) c = c * (double)(plain_bases - k + 1) / (double)k;
+                        pr += c * std::pow(0.75, (double)k) * std::pow(0.25, (double)(plain_bases - k));
+                    }
+                    return pr;
+                };
+                double pass_sum = 0.0;
+                uint64_t pass_n = 0;
+                const uint64_t nkeys = 1ull << (2 * W);
+                kgrp.assign(nkeys / kKgrpKeys, 0ull);
+                for (uint64_t g = 0; g < kgrp.size(); ++g) {
+                    const uint32_t pres = (uint32_t)((filt[g >> 1] >> ((g & 1) * 16)) & 0xFFFFu);
+                    uint64_t w = pres;
+                    uint32_t j = 0;
+                    for (uint32_t bit = 0; bit < 16 && j < kKgrpWildFields; ++bit) {
+                        if (!((pres >> bit) & 1u)) continue;
+                        const uint32_t k = (uint32_t)(g * kKgrpKeys + bit);
+                        const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
+                        const uint32_t b = rank_bucket[rank];
+                        const Entry& e = ents[boff[b]];
+                        uint32_t field = (m2 & 0x555u) << 12;  // every base wild: always passes
+                        double pr = 1.0;
+                        if (bcount[b] == 1 && e.hash_off == 0 && e.l1 >= W + F) {
+                            const uint32_t codes = (uint32_t)((e.code << (2 * W)) >> (64 - 2 * F));
+                            const uint32_t plain = (uint32_t)(((e.pmask & kEven) << (2 * W)) >> (64 - 2 * F));
+                            field = codes | ((~plain & m2 & 0x555u) << 12);
+                            pr = pass_rate((uint32_t)__builtin_popcount(plain & m2 & 0x555u));
+                        }
+                        pass_sum += pr;
+                        ++pass_n;
+                        w |= (uint64_t)field << (16u + 24u * j);
+                        ++j;
+                    }
+                    for (; j < kKgrpWildFields; ++j) w |= (uint64_t)((m2 & 0x555u) << 12) << (16u + 24u * j);
+                    kgrp[g] = w;
+                }
+                // the scan takes the key groups only when they reject most seeds (c3's fields
+                // pass ~0.5%); c4's (N = 2, ~30% IUPAC bases after the seed) pass ~30% and stay
+                // on the 16-B heads, which test 16 bases
+                t->kgrp_wild = pass_n && pass_sum / (double)pass_n < 0.08 ? 1 : 0;
+            } else if (W >= 11 && W <= 13) {
                 const uint32_t F = std::min<uint32_t>(7u, 17u - W);
                 t->kgrp_F = F;
                 const uint64_t nkeys = 1ull << (2 * W);
