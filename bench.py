@@ -316,6 +316,8 @@ def main():
                          "one-GPU box); the JSON line is then not the metric")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one search handle: every step waits for the previous one (no run queued ahead)")
+    ap.add_argument("--handles", type=int, default=2,
+                    help="search handles (and streams) of the pipeline: steps in flight")
     ap.add_argument("--one-stream", action="store_true",
                     help="pipelined handles share one stream (no kernel of step i+1 overlaps step i)")
     ap.add_argument("--shard-of", type=int, default=0,
@@ -386,7 +388,7 @@ def main():
     # the host waits for step i, so the host turnaround between runs is off the GPU's path.
     # With N > 1 each completed step's RCCL gather runs on a stream of its own, and the
     # handle's next run waits (on the device) for its gather to have sent the hits.
-    nbuf = 1 if args.no_pipeline else 2
+    nbuf = 1 if args.no_pipeline else max(2, args.handles)
     handles = [search] + [_native.Search(table, genome) for _ in range(nbuf - 1)]
     # one stream per handle (--one-stream: all on the default stream): step i+1's scan may then
     # start on the CUs that step i's latency-bound tail / pair / order kernels leave idle

@@ -74,7 +74,7 @@ MP_EXPORT int mp_format_hits(const mp_hit* hits, uint64_t n_hits, const uint8_t*
             return fail(MP_E_ARG, "mp_format_hits: hit " + std::to_string(i) + " names an unknown sequence or record");
 
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const uint64_t per = 1u << 16;
+    const uint64_t per = 1u << 13;  // hits per thread at least (c3: 200k hits over every core)
     const unsigned nt = (unsigned)std::min<uint64_t>(std::min(hw, 32u), (n_hits + per - 1) / per);
     std::vector<uint64_t> part(nt + 1, 0);
     auto bound = [&](unsigned t) { return n_hits * t / std::max(1u, nt); };

@@ -389,7 +389,10 @@ SortPlan sort_plan(const Search* s);
 // pair_kernel already wrote the packed keys (tmp_lo) and the bucket counts; mode 0: the keys
 // also in their bucket slots.  Bucket offsets, then the sort.  Hit count read on the device;
 // writes s->out.
-int sort_hits_device(Search* s, hipStream_t st, int mode);
+// finish: the offsets launch also copies counters[0..8) to the mapped host words and zeroes
+// the counters (the run's end; see bucket_offsets).
+int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish);
+size_t counter_bytes();  // the run counters' size (mp_search.hip)
 uint32_t* sort_bucket_counts(Search* s);          // the bucket count array (zeroed by the scan kernels)
 uint32_t* sort_bucket_offsets(Search* s);         // nb + 1 offsets
 uint32_t* sort_bucket_cursors(Search* s);

@@ -24,7 +24,7 @@ static unsigned bits_for(uint64_t v) {
 // hits spread over the genome), counted, scattered, and each bucket is ranked in LDS by
 // one workgroup that writes the decoded mp_hit records straight to the output.  A bucket
 // larger than kSortCap (hits piled on a few positions, e.g. a dense repeat) sets
-// counters[kSortOverflow]; the host then sorts with rocPRIM instead.
+// h_out[kSortOverflow]; the host then sorts with rocPRIM instead.
 constexpr uint32_t kSortCap = 2048;
 constexpr unsigned kMaxBucketBits = 16;
 
@@ -50,18 +50,39 @@ __global__ void bucket_hist(const uint64_t* __restrict__ hi, const uint64_t* __r
     }
 }
 
-// exclusive scan of the bucket counts by one 1024-thread workgroup (bucket_offsets_block,
-// mp_internal.h).
+// Exclusive scan of the bucket counts by one 1024-thread workgroup (bucket_offsets_block,
+// mp_internal.h).  With h_out it is also the run's finish: pair_kernel, the last producer of
+// the counters, is complete, so counters[0..8) go to the device-mapped host words the host
+// polls and every counter is zeroed for the next run (the sort after it reports an overflow
+// straight to h_out[kSortOverflow]; the scatter takes the hit count from off[nb]).
 __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restrict__ cnt, uint32_t nb,
-                                                       uint32_t* __restrict__ off, uint32_t* __restrict__ cursor) {
+                                                       uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
+                                                       unsigned long long* __restrict__ counters, uint32_t n_words,
+                                                       unsigned long long* __restrict__ h_out) {
     __shared__ uint4 s_v4[kOffTile / 4];
     __shared__ uint32_t s_w[16];
+    if (h_out) {
+        unsigned long long v = 0;
+        if (threadIdx.x < 8) v = counters[threadIdx.x];
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n_words; i += blockDim.x) counters[i] = 0ull;
+        if (threadIdx.x < 8) {
+            h_out[threadIdx.x] = v;
+            __threadfence_system();
+        }
+    }
     bucket_offsets_block(cnt, nb, off, cursor, s_v4, s_w);
 }
 
-__global__ void bucket_scatter(const uint64_t* __restrict__ keys, const unsigned long long* __restrict__ counters,
+// A bucket the device order cannot hold: flagged in the host word (the device counters are
+// already zeroed for the next run).
+__device__ __forceinline__ void flag_overflow(unsigned long long* h_out) {
+    __hip_atomic_store(&h_out[kSortOverflow], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void bucket_scatter(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off, uint32_t nb,
                                uint64_t cap, unsigned shift, uint32_t* __restrict__ cursor, uint64_t* __restrict__ out) {
-    const uint64_t n = counters[0] < cap ? counters[0] : cap;
+    const uint64_t n = off[nb] < cap ? off[nb] : cap;  // the hit count (bucket_offsets' total)
     const int lane = threadIdx.x & 63;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
@@ -116,7 +137,7 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
                                                           uint32_t nb, unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
                                                           const uint64_t* __restrict__ seq_len, uint32_t n_seq,
                                                           const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
-                                                          mp_hit* __restrict__ out, unsigned long long* __restrict__ counters) {
+                                                          mp_hit* __restrict__ out, unsigned long long* __restrict__ h_out) {
     __shared__ uint64_t s_k[kSortCap];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t b0 = blockIdx.x * kBucketsPerBlock;
@@ -138,7 +159,7 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
         const uint32_t start = off[b0 + q], m = off[b0 + q + 1] - start;
         if (m <= 64) continue;  // done by its wave above
         if (m > kSortCap) {
-            if (threadIdx.x == 0) atomicOr(&counters[kSortOverflow], 1ull);
+            if (threadIdx.x == 0) flag_overflow(h_out);
             continue;
         }
         for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
@@ -182,14 +203,14 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
 // in arrival order) and, from its last block, the bucket offsets.  One wave per bucket ranks
 // the bucket's keys -- up to 64 by shuffles, up to slot_cap by counting through the wave's
 // LDS -- and writes the decoded records at off[b] + rank.  No scatter pass, no block barrier.
-// A bucket over slot_cap (its keys did not all fit) sets counters[kSortOverflow]; the host
+// A bucket over slot_cap (its keys did not all fit) sets h_out[kSortOverflow]; the host
 // then orders the run in mode 1 from the linear keys.
 constexpr uint32_t kSlotWaves = 4;
 __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
     const uint64_t* __restrict__ slots, uint32_t slot_cap, const uint32_t* __restrict__ off, uint32_t nb,
     unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
     uint32_t n_seq, const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs, mp_hit* __restrict__ out,
-    unsigned long long* __restrict__ counters) {
+    unsigned long long* __restrict__ h_out) {
     __shared__ uint64_t s_k[kSlotWaves][kSlotCap];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t b = blockIdx.x * kSlotWaves + wave;
@@ -197,7 +218,7 @@ __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
     const uint32_t start = off[b], m = off[b + 1] - start;
     if (m == 0) return;
     if (m > slot_cap) {
-        if (lane == 0) atomicOr(&counters[kSortOverflow], 1ull);
+        if (lane == 0) flag_overflow(h_out);
         return;
     }
     const uint64_t* src = slots + (uint64_t)b * slot_cap;
@@ -267,7 +288,7 @@ int alloc_sort_slots(Search* s, const SortPlan& P) {
     return MP_OK;
 }
 
-int sort_hits_device(Search* s, hipStream_t st, int mode) {
+int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     const SortPlan P = sort_plan(s);
     const int arc = alloc_sort_buckets(s);
     if (arc) return arc;
@@ -277,22 +298,23 @@ int sort_hits_device(Search* s, hipStream_t st, int mode) {
     // A separate launch, not pair_kernel's last block: publishing the counts inside the pair
     // kernel needs an agent-scope release per block (buffer_wbl2 of the XCD's L2, several
     // us each across the persistent grid), measured +65 us on a 1/8 c3 step.
-    hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, sort_bucket_counts(s), P.nb, off, cursor);
+    hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, sort_bucket_counts(s), P.nb, off, cursor,
+                       s->counters, (uint32_t)(counter_bytes() / 8), finish ? s->d_hcnt : nullptr);
     MP_HIP_CHECK(hipGetLastError());
     if (mode == 0) {
         hipLaunchKernelGGL(sort_decode_slots, dim3((P.nb + kSlotWaves - 1) / kSlotWaves), dim3(64 * kSlotWaves), 0, st,
                            s->slots, P.slot_cap, off, P.nb, P.try_bits, P.low_bits, g->d_base, g->d_len, g->n_seq,
-                           s->table->inv_rank, s->table->recs, s->out, s->counters);
+                           s->table->inv_rank, s->table->recs, s->out, s->d_hcnt);
         MP_HIP_CHECK(hipGetLastError());
         return MP_OK;
     }
     const uint32_t grid = (uint32_t)std::min<uint64_t>((s->cap + 255) / 256, 2048);
-    hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, s->counters, s->cap, P.shift, cursor,
+    hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, off, P.nb, s->cap, P.shift, cursor,
                        s->tmp_hi);
     MP_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
                        s->tmp_hi, off, P.nb, P.try_bits, P.low_bits,
-                       g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->counters);
+                       g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->d_hcnt);
     MP_HIP_CHECK(hipGetLastError());
     return MP_OK;
 }

@@ -120,6 +120,7 @@ constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
 constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;  // pair_kernel batch counters, 8 x 256 B
 constexpr int kSchedBase = kPairQBase + 8 * kStatStride;  // scan super-step chunk counters, 8 x 256 B
 constexpr size_t kCounterBytes = (size_t)(kSchedBase + 8 * kStatStride) * 8;
+size_t counter_bytes() { return kCounterBytes; }
 #ifndef MP_PDYN_BATCH
 #define MP_PDYN_BATCH 64
 #endif
@@ -1341,9 +1342,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ WaveLds s_wl[kWaves];
 
     zero_sort_counts(a);
-    // stage the seed prefilter in LDS (once per persistent workgroup)
-    for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)
-        reinterpret_cast<uint4*>(s_lf)[i] = reinterpret_cast<const uint4*>(a.lfilt)[i];
+    // stage the seed prefilter in LDS (once per persistent workgroup): all eight 16-B loads of
+    // a thread in flight before the first LDS store (one L2 round trip, not eight)
+    {
+        static_assert(kLdsFilterWords / 4 == 8 * kBlock, "eight uint4 per thread");
+        const uint4* src = reinterpret_cast<const uint4*>(a.lfilt);
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = src[threadIdx.x + k * kBlock];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) reinterpret_cast<uint4*>(s_lf)[threadIdx.x + k * kBlock] = v[k];
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -1677,7 +1686,10 @@ __device__ __forceinline__ uint32_t oct_spares(const uint4 q) {
     return (uint32_t)__popc((q.x & m) | ((q.y & m) << 1) | ((q.z & m) << 2) | ((q.w & m) << 3));
 }
 
-template <int kN>
+// kSum: the per-key summary's form (Table::dsum_mode: 0 none, 1 N = 0, 2 N = 1), a template
+// parameter so the window's two LDS reads (group word, summary) issue together with one wait
+// and no branch between them.
+template <int kN, int kSum>
 __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     extern __shared__ uint2 s_grp[];
     const uint32_t W = (uint32_t)a.W;
@@ -1689,7 +1701,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         s_grp[i] = a.dgrp[i];
         s_esc[i] = a.dgesc[i];
     }
-    if (a.dsum_mode) {
+    if (kSum) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.dsum);
         for (uint32_t i = threadIdx.x; i < (1u << (2 * W)) / 2; i += kDenseBlock) s_sum[i] = src[i];
     }
@@ -1774,20 +1786,24 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
                 const uint32_t r = 2u * ((TB + (uint32_t)T) & 15u);
                 const uint32_t h = (r ? __builtin_amdgcn_alignbit(dh, dl, 32u - r) : dh) >> shw;
                 const uint2 L = s_grp[h >> 5];
+                const uint32_t smw = kSum ? s_sum[h >> 1] : 0u;  // issued beside the group word
                 const uint32_t bq = h & 31u;
                 const uint32_t wb = 31u - (TB + (uint32_t)T);
                 const bool ok = (okm >> wb) & 1u;
-                bool inl = ok && ((L.x >> bq) & 1u);
-                if (a.dsum_mode) {  // the key's summary: no record can pass -> no oct load
-                    const uint32_t sm = s_sum[h >> 1] >> ((h & 1u) << 4);
+                // bitwise, not short-circuit: no branch may sink the summary read below the
+                // group word's wait
+                uint32_t inlb = (okm >> wb) & (L.x >> bq) & 1u;
+                if constexpr (kSum != 0) {  // the key's summary: no record can pass -> no oct load
+                    const uint32_t sm = smw >> ((h & 1u) << 4);
                     const uint32_t key = r ? __builtin_amdgcn_alignbit(dh, dl, 32u - r) : dh;
                     const uint32_t gf = (key << (2 * W)) >> (32u - 2u * sumF);  // bases W..W+F-1
-                    const uint32_t sb = a.dsum_mode == 1
+                    const uint32_t sb = kSum == 1
                                             ? sm >> dsum_hash4(gf)
                                             : (sm >> dsum_hash3(gf >> (2u * sumFB))) |
                                                   (sm >> (8u + dsum_hash3(gf & ((1u << (2u * sumFB)) - 1u))));
-                    inl = inl && ((sb & 1u) || ((slowm >> wb) & 1u));
+                    inlb &= sb | (slowm >> wb);
                 }
+                const bool inl = inlb != 0u;
                 if ((int32_t)L.y < 0 && ok)  // the group holds a key of more than eight records
                     escm |= ((s_esc[h >> 5] >> bq) & 1u) << wb;
                 live |= (uint32_t)inl << T;
@@ -2203,12 +2219,13 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
                        std::max<size_t>(1, ((size_t)1 << (2 * std::min<int>(t->prm.wordsize, kDenseMaxW))) / 32);
         if (t->dsum_mode) s->dense_lds += sizeof(uint16_t) * ((size_t)1 << (2 * t->prm.wordsize));
         if (s->dense_lds > 64 * 1024)
-            for (const void* k : {(const void*)dense_kernel<0>, (const void*)dense_kernel<1>,
-                                  (const void*)dense_kernel<2>, (const void*)dense_kernel<-1>})
+            for (const void* k : {(const void*)dense_kernel<0, 0>, (const void*)dense_kernel<0, 1>,
+                                  (const void*)dense_kernel<1, 0>, (const void*)dense_kernel<1, 2>,
+                                  (const void*)dense_kernel<2, 0>, (const void*)dense_kernel<-1, 0>})
                 (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->dense_lds);
         occ = 0;
         if (const char* e = std::getenv("MP_SCHUNK_SHORT")) s->sched_short = (uint32_t)std::max(1, std::atoi(e));
-        s->dense_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dense_kernel<1>, kDenseBlock, s->dense_lds) ==
+        s->dense_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dense_kernel<1, 2>, kDenseBlock, s->dense_lds) ==
                                hipSuccess && occ > 0) ? (uint32_t)occ : 1u;
         if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
             hipEventCreate(&s->ev2) != hipSuccess || hipEventCreate(&s->ev3) != hipSuccess ||
@@ -2301,10 +2318,13 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
                                                             (uint64_t)s->n_cu * (uint64_t)s->dense_per_cu);
         const size_t lds = s->dense_lds;
-        if (a.N == 0) hipLaunchKernelGGL(dense_kernel<0>, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
-        else if (a.N == 1) hipLaunchKernelGGL(dense_kernel<1>, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
-        else if (a.N == 2) hipLaunchKernelGGL(dense_kernel<2>, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
-        else hipLaunchKernelGGL(dense_kernel<-1>, dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        // the summary exists only for N <= 1 (mp_table.hip): N = 0 form 1, N = 1 form 2
+        if (a.N == 0 && a.dsum_mode == 1) hipLaunchKernelGGL((dense_kernel<0, 1>), dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        else if (a.N == 0) hipLaunchKernelGGL((dense_kernel<0, 0>), dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        else if (a.N == 1 && a.dsum_mode == 2) hipLaunchKernelGGL((dense_kernel<1, 2>), dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        else if (a.N == 1) hipLaunchKernelGGL((dense_kernel<1, 0>), dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        else if (a.N == 2) hipLaunchKernelGGL((dense_kernel<2, 0>), dim3(dgrid), dim3(kDenseBlock), lds, st, a);
+        else hipLaunchKernelGGL((dense_kernel<-1, 0>), dim3(dgrid), dim3(kDenseBlock), lds, st, a);
     } else if (inl) {
         if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -2340,13 +2360,15 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, a);
     MP_HIP_CHECK(hipGetLastError());
     MID_EVENT(hipEventRecord(s->ev2, st));
-    if (mode < 2) {  // hit order on the device count: no host round trip before it
-        const int rc = sort_hits_device(s, st, mode);
+    if (mode < 2) {  // hit order on the device count: no host round trip before it; its offsets
+                     // launch also finishes the run (counters to the host words, then zeroed)
+        const int rc = sort_hits_device(s, st, mode, true);
         if (rc) return rc;
+    } else {
+        hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(1024), 0, st, s->counters, (uint32_t)(kCounterBytes / 8), s->d_hcnt);
+        MP_HIP_CHECK(hipGetLastError());
     }
     MID_EVENT(hipEventRecord(s->ev3, st));
-    hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(1024), 0, st, s->counters, (uint32_t)(kCounterBytes / 8), s->d_hcnt);
-    MP_HIP_CHECK(hipGetLastError());
     MP_HIP_CHECK(hipEventRecord(s->evd, st));
     return MP_OK;
 }
@@ -2366,18 +2388,14 @@ static int redo_order(Search* s, hipStream_t st, int from, uint64_t nh) {
     for (int mode = from + 1; mode <= 2; ++mode) {
         s->order_mode = std::max(s->order_mode, mode);
         if (mode == 1) {
-            // bucket_scatter reads the hit count on the device; finish_kernel zeroed it
-            s->h_cnt[8] = nh;
-            MP_HIP_CHECK(hipMemcpyAsync(s->counters, (const void*)&s->h_cnt[8], sizeof(unsigned long long),
-                                        hipMemcpyHostToDevice, st));
-            const int rc = sort_hits_device(s, st, 1);
+            // the bucket counts and keys are intact; the offsets again (no finish: the host
+            // words hold this run's counters), then scatter and sort; an overflow shows in
+            // the host word
+            s->h_cnt[kSortOverflow] = 0;
+            const int rc = sort_hits_device(s, st, 1, false);
             if (rc) return rc;
-            unsigned long long ovf = 0;
-            MP_HIP_CHECK(hipMemcpyAsync(&s->h_cnt[9], s->counters + kSortOverflow, sizeof(ovf), hipMemcpyDeviceToHost, st));
             MP_HIP_CHECK(hipStreamSynchronize(st));
-            ovf = s->h_cnt[9];
-            MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
-            if (!ovf) break;
+            if (!s->h_cnt[kSortOverflow]) break;
             continue;
         }
         const int rc = sort_hits(s, nh, st);

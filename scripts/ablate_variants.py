@@ -9,6 +9,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
   3   level 1, the list and the level-2 loads (consumed, nothing more)
   30  no super-step loop (launch, LDS staging, statistics)
   31  no LDS staging and no loop
+  40  per-wave wall-clock stamps (entry, LDS staged, loop end, exit) of scan_kernel, read back
+      with mp_debug_wave_times (a function only this variant exports)
   50  pair_kernel without the lane-parallel try loop
   51  pair_kernel without any try (prologue, primer-1 compare and staging only)
 """
@@ -20,11 +22,16 @@ _L2 = "                constexpr int kP = (kSeedQR + 63) / 64;\n"
 _L3 = "                if constexpr (kRkf) {\n                    // the few seeds that pass the key groups"
 _LOOP = ("    while (ss < n_supers) {\n        const SeqSpan sp = pf;\n        const uint64_t sbase = pf_sbase;\n"
          "        const uint32_t n = pf_n;\n        SuperRegs R;")
-_STAGE = ("    for (uint32_t i = threadIdx.x; i < kLdsFilterWords / 4; i += kBlock)\n"
-          "        reinterpret_cast<uint4*>(s_lf)[i] = reinterpret_cast<const uint4*>(a.lfilt)[i];\n")
+_STAGE = "    {\n        static_assert(kLdsFilterWords / 4 == 8 * kBlock, \"eight uint4 per thread\");\n"
 
 _LP = "    if (__any(lp)) {\n"
 _TODO = "    uint64_t todo = __ballot(keep && !lp);\n"
+
+_T_ENTRY = "    zero_sort_counts(a);\n    // stage the seed prefilter in LDS (once per persistent workgroup)"
+_T_STAGED = "    const int lane = threadIdx.x & 63;\n    const int w = threadIdx.x >> 6;\n    const uint64_t stride = (uint64_t)gridDim.x * kWaves;"
+_T_END = "    close_chunked(a.surv, a.surv_cap, lane, C);\n    close_chunked<2>(a.tails, a.tails_cap, lane, TC);"
+_T_TAIL = "MP_EXPORT int mp_search_set_stage_timing(void* search, int32_t on) {"
+_T_GLOBAL = ("}  // namespace mp\n\nusing namespace mp;\n\nMP_EXPORT int mp_search_set_stage_timing")
 
 VARIANTS = {
     1: [(_L1, "            if constexpr (kMode == 1) {  // ablation 1\n"
@@ -38,6 +45,19 @@ VARIANTS = {
               "                r0 += kSeedQR;\n                continue;\n")],
     30: [(_LOOP, "    ss = n_supers;  // ablation 30\n")],
     31: [(_LOOP, "    ss = n_supers;  // ablation 31\n"), (_STAGE, "    if (false)  // ablation 31\n")],
+    40: [(_T_ENTRY, "    const uint64_t wt0 = wall_clock64();  // ablation 40\n"),
+         (_T_STAGED, "    const uint64_t wt1 = wall_clock64();  // ablation 40\n"),
+         (_T_END, "    const uint64_t wt2 = wall_clock64();  // ablation 40\n"),
+         ("        const uint64_t nx = sch.next(ss, n_supers, lane);\n        (void)stride;\n        if constexpr (kMode == 1) {",
+          "        ++n_ss;  // ablation 40\n"),
+         ("    SuperSched sch;\n    uint64_t ss = sch.first(a.counters, n_supers, w, kWaves, lane, a.sched_short);",
+          "    uint32_t n_ss = 0;  // ablation 40\n"),
+         ("    // candidate statistics\n    add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);\n}\n",
+          "    if ((threadIdx.x & 63) == 0 && blockIdx.x * kWaves + (threadIdx.x >> 6) < 8192)  // ablation 40\n"
+          "        g_wave_times[blockIdx.x * kWaves + (threadIdx.x >> 6)] = make_ulonglong4(wt0, wt1, wt2, n_ss);\n"),
+         ("struct SuperSched {", "__device__ ulonglong4 g_wave_times[8192];  // ablation 40\n"),
+         (_T_TAIL, "MP_EXPORT int mp_debug_wave_times(ulonglong4* out, uint32_t n) {  // ablation 40\n"
+                   "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_times), n * sizeof(ulonglong4)) == hipSuccess ? 0 : -1;\n}\n\n")],
     50: [(_LP, "    if (false)  // ablation 50\n")],
     51: [(_LP, "    if (false)  // ablation 51\n"), (_TODO, "    keep = false;  // ablation 51\n")],
 }

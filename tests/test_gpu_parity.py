@@ -655,3 +655,48 @@ def test_two_ranks_on_one_gpu():
     ref = C.search(table, [np.frombuffer(x.encode(), dtype=np.uint8) for x in seqs], O.params(wordsize=11, mismatches=1), 8)
     assert len(whole) > 100 and got == whole.tobytes() == ref.tobytes()
     assert all(p.exitcode == 0 for p in procs)
+
+
+def test_iupac_wide_key_groups_with_genome_ambiguity():
+    """I = 1 tables whose primers carry IUPAC bases right after the seed (c4's shape) take
+    the wide 13-base key groups (kgrp_pass_wide).  Genome IUPAC characters inside those 13
+    bases match under I = 1 although the 2-bit plane reads them as 'A': such windows must
+    pass on presence alone.  Planted amplicons put N/R/Y/K into exactly those positions."""
+    rng = random.Random(41)
+    W, N, M, glen = 11, 2, 50, 250_000
+    seq = [rng.choice("ACGT") for _ in range(glen)]
+    sts = []
+    for s in range(300):
+        p1 = [rng.choice("ACGT") for _ in range(rng.randint(20, 25))]
+        p2 = [rng.choice("ACGT") for _ in range(rng.randint(20, 25))]
+        for p in (p1, p2):  # IUPAC bases among primer bases W..W+12, none in the seed
+            for _ in range(2):
+                p[rng.randrange(W, min(len(p) - 3, W + 13))] = rng.choice("RYSWKMN")
+        p1, p2 = "".join(p1), "".join(p2)
+        size = rng.randint(120, 400)
+        sts.append(f"W{s}\t{p1}\t{p2}\t{size}\tw{s}")
+        for form in (0, 1):
+            a_, b_ = (p1, p2) if form == 0 else (p2, O.revcomp(p1))
+            a_ = list(a_.replace("R", "A").replace("Y", "C").replace("S", "G").replace("W", "T")
+                      .replace("K", "G").replace("M", "C").replace("N", "T"))
+            for _ in range(rng.randint(0, 2)):  # genome ambiguity characters after the seed
+                a_[rng.randrange(W, min(len(a_), W + 13))] = rng.choice("NRYK")
+            fill = "".join(rng.choice("ACGT") for _ in range(max(0, size - len(a_) - len(b_) + rng.randint(-M, M))))
+            amp = "".join(a_) + fill + b_
+            at = rng.randrange(glen - len(amp))
+            seq[at:at + len(amp)] = list(amp)
+    for _ in range(40):  # N runs
+        at = rng.randrange(glen - 200)
+        seq[at:at + rng.randint(1, 150)] = "N" * 150
+    seq = "".join(seq)[:glen]
+    sts_text = "\n".join(sts) + "\n"
+    prm = dict(wordsize=W, mismatches=N, iupac_mode=1, margin=M)
+    eng = MerPCR(**prm)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    recs = [FASTARecord(defline=">chrW", sequence=seq)]
+    got = _device_lines(eng, recs)
+    table = O.load_sts_lines(sts_text.splitlines(True), W, 240)
+    exp = O.search_lines([("chrW", seq)], table, O.params(**prm))
+    assert len(exp) > 200
+    assert got == exp
