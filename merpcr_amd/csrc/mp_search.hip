@@ -1288,11 +1288,22 @@ constexpr uint32_t kSChunkShort = 128;
 #ifndef MP_SCHED_MIN
 #define MP_SCHED_MIN 4u
 #endif
+// Claims are positions, not tickets: a wave adds the size it wants to its group's counter.
+// The size shrinks with the group's remaining range (about the range left / twice the
+// group's waves, from the wave's last claim: "guided"), and is halved for the two youngest
+// waves of each SIMD.  Per-wave stamps (scripts/wave_times.py, ablation 40) on a 1/8 c3
+// scan: a SIMD issues for its oldest wave first, so waves 12-15 of a block did 29
+// super-steps at ~11 us each and waves 0-3 did 60 at ~5 us; with fixed chunks of 4 and one
+// chunk claimed ahead the young waves ended 20 us after the old ones and the last wave 47 us
+// after the first.
 struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives beside the scan's registers
     uint32_t lo, hi, nw, end;  // XCD group range, waves of the group, end of the current chunk
-    uint32_t pending;          // lane 0: counter value claimed for the next chunk
+    uint32_t S;                // end of the static first chunks: dynamic positions count from here
+    uint32_t pending, psize;   // lane 0: position claimed for the next chunk, and its size
     uint32_t stride;           // 0: dynamic; else the static round-robin stride
-    uint32_t chunk;            // super-steps per claim
+    uint32_t chunk;            // largest claim
+    uint32_t young;            // the SIMD's two youngest waves (w >= kW / 2) claim half
+    uint32_t hint;             // start of this wave's last chunk (the guided size's estimate)
     unsigned int* ctr;
     __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint64_t n_supers, int w, int kW, int lane,
                                               uint32_t short_chunk) {
@@ -1311,26 +1322,36 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         lo = (uint32_t)(n_supers * x / g);
         hi = (uint32_t)(n_supers * (x + 1) / g);
         nw = ((gridDim.x - x + g - 1u) / g) * (uint32_t)kW;
+        S = min(lo + nw * chunk, hi);
+        young = (uint32_t)w >= (uint32_t)kW / 2u;
         const uint32_t st = lo + ((blockIdx.x / g) * (uint32_t)kW + (uint32_t)w) * chunk;
         end = min(st + chunk, hi);
+        hint = st;
         claim(lane);
         return st < hi ? st : n_supers;
     }
     __device__ __forceinline__ void claim(int lane) {
+        const uint32_t from = max(hint, S);
+        const uint32_t left = hi > from ? hi - from : 0u;
+        uint32_t sz = min(chunk, max(1u, left / (2u * nw)));
+        if (young) sz = max(1u, sz >> 1);
+        psize = sz;
         pending = 0;
-        if (lane == 0) pending = atomicAdd(ctr, 1u);
+        if (lane == 0) pending = atomicAdd(ctr, sz);
     }
     __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane) {
         if (stride) return ss + stride;
         if (ss + 1 < end) return ss + 1;
-        // lane 0 holds the claimed counter value: broadcast from lane 0 explicitly (called
-        // wave-uniformly, but readfirstlane would read another lane under divergence)
-        const uint32_t st = lo + (nw + (uint32_t)__shfl((int)pending, 0, 64)) * chunk;
+        // lane 0 holds the claimed position; next() runs at the top of the super-step loop
+        // with every lane active, so the first active lane is lane 0 and the broadcast is a
+        // readfirstlane (the scheduler state then stays in scalar registers)
+        const uint32_t st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);
         if (st >= hi) {
             end = 0;
             return n_supers;
         }
-        end = min(st + chunk, hi);
+        end = min(st + psize, hi);
+        hint = st;
         claim(lane);
         return st;
     }
