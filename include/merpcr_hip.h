@@ -105,11 +105,11 @@ int mp_genome_put_device(void* genome, uint32_t seq, uint64_t offset, const uint
 int mp_genome_seal(void* genome, void* stream);
 int mp_genome_stats(void* genome, uint64_t* total_bases, uint64_t* n_exc_runs, uint64_t* dev_bytes);
 /* Diagnostic (tests): copy the packed planes of a sealed genome to host memory -- g2
- * (total/32 words), gexc and ginv (total/64 words each; total = padded bases, the sum of
- * each length rounded up to 64) and the sorted exception-run index (n_exc_runs starts and
+ * (total/32 words), gexc, ginv and gwild (total/64 words each; total = padded bases, the sum
+ * of each length rounded up to 64) and the sorted exception-run index (n_exc_runs starts and
  * characters).  Any pointer may be NULL to skip that array. */
-int mp_genome_download(void* genome, uint64_t* g2, uint64_t* gexc, uint64_t* ginv, uint64_t* xr_start,
-                       uint8_t* xr_char);
+int mp_genome_download(void* genome, uint64_t* g2, uint64_t* gexc, uint64_t* ginv, uint64_t* gwild,
+                       uint64_t* xr_start, uint8_t* xr_char);
 /* Re-lay the handle out for a new set of sequences (the next search() call of the
  * engine): device planes are reused when the new layout fits them, else regrown.  The
  * handle is unsealed and empty afterwards; searches created on it stay valid. */

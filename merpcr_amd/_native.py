@@ -92,7 +92,7 @@ def _sig(lib):
     lib.mp_genome_put_device.argtypes = [P, c_uint32, c_uint64, P, c_uint64, P]
     lib.mp_genome_seal.argtypes = [P, P]
     lib.mp_genome_stats.argtypes = [P, u64p, u64p, u64p]
-    lib.mp_genome_download.argtypes = [P, P, P, P, P, P]
+    lib.mp_genome_download.argtypes = [P, P, P, P, P, P, P]
     lib.mp_genome_reset.argtypes = [P, c_uint32, P]
     lib.mp_genome_destroy.argtypes = [P]
     lib.mp_genome_destroy.restype = None
@@ -269,16 +269,17 @@ class Genome:
         return {"bases": a.value, "exc_runs": b.value, "dev_bytes": c.value}
 
     def download(self):
-        """(g2, gexc, ginv, xr_start, xr_char) of the sealed genome (diagnostic, tests)."""
+        """(g2, gexc, ginv, gwild, xr_start, xr_char) of the sealed genome (diagnostic, tests)."""
         total = int(sum((int(n) + 63) // 64 * 64 for n in self.lengths))
         n_xr = self.stats()["exc_runs"]
         g2 = np.empty(total // 32, dtype=np.uint64)
         ge = np.empty(total // 64, dtype=np.uint64)
         gi = np.empty(total // 64, dtype=np.uint64)
+        gw = np.empty(total // 64, dtype=np.uint64)
         xs = np.empty(max(n_xr, 1), dtype=np.uint64)
         xc = np.empty(max(n_xr, 1), dtype=np.uint8)
-        check(lib().mp_genome_download(self._h, ptr(g2), ptr(ge), ptr(gi), ptr(xs), ptr(xc)))
-        return g2, ge, gi, xs[:n_xr], xc[:n_xr]
+        check(lib().mp_genome_download(self._h, ptr(g2), ptr(ge), ptr(gi), ptr(gw), ptr(xs), ptr(xc)))
+        return g2, ge, gi, gw, xs[:n_xr], xc[:n_xr]
 
     def close(self):
         if self._h:

@@ -3,7 +3,7 @@
 // Stands in for the sequence strings that MerPCR.search walks per record
 // (src/merpcr/core/engine.py:373-411, upper-cased at engine.py:455) after
 // FASTALoader's character filter (src/merpcr/io/fasta.py:60).  pack_kernel turns each
-// 64-base group into two 2-bit words, one ginv word and one gexc word, and lists the
+// 64-base group into two 2-bit words, one ginv, one gexc and one gwild word, and lists the
 // heads of exception runs (maximal same-character stretches of non-ACGT bases inside
 // its put) for the sparse character index.
 #include <algorithm>
@@ -33,6 +33,7 @@ __device__ __forceinline__ uint32_t nib4(uint32_t m) {
 struct Cls4 {
     uint32_t code8;  // the 4 bases' 2-bit codes, first base on top
     uint32_t exc, inv;  // per-byte flags (bit 7)
+    uint32_t wild;   // per-byte flag: 'N' (either case), which every IUPAC primer base matches
     uint32_t up;     // upper-cased bytes
 };
 __device__ __forceinline__ Cls4 classify4(uint32_t w) {
@@ -46,6 +47,7 @@ __device__ __forceinline__ Cls4 classify4(uint32_t w) {
     r.code8 = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) | (c >> 24);
     r.exc = ~acgt & 0x80808080u;
     r.inv = ~acgtu & 0x80808080u;
+    r.wild = zbytes(l ^ 0x6E6E6E6Eu);
     const uint32_t t = w & 0x7F7F7F7Fu;  // a-z: t >= 0x61, t <= 0x7A and the byte is ASCII
     const uint32_t lower = (t + 0x1F1F1F1Fu) & (0xFAFAFAFAu - t) & ~w & 0x80808080u;
     r.up = w - (lower >> 2);
@@ -71,6 +73,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ s
                                                    uint64_t gstart, uint64_t* __restrict__ g2,
                                                    uint64_t* __restrict__ gexc,
                                                    uint64_t* __restrict__ ginv,
+                                                   uint64_t* __restrict__ gwild,
                                                    uint64_t* __restrict__ xr_start,
                                                    uint8_t* __restrict__ xr_char,
                                                    unsigned long long* __restrict__ xr_count,
@@ -118,6 +121,8 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ s
             uint32_t inv16 = (nib4(c0.inv) << 12) | (nib4(c1.inv) << 8) | (nib4(c2.inv) << 4) | nib4(c3.inv);
             exc16 |= ~valid16 & 0xFFFFu;  // padding: ambiguous
             inv16 |= ~valid16 & 0xFFFFu;
+            const uint32_t wild16 =
+                ((nib4(c0.wild) << 12) | (nib4(c1.wild) << 8) | (nib4(c2.wild) << 4) | nib4(c3.wild)) & valid16;
             n_u += (uint32_t)__popc(exc16 & ~inv16 & valid16);
             // run heads: an exception byte whose predecessor (in this put) is not the same
             // exception character
@@ -138,6 +143,8 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ s
                            e3 = (uint32_t)__shfl_down((int)exc16, 3, 64);
             const uint32_t i1 = (uint32_t)__shfl_down((int)inv16, 1, 64), i2 = (uint32_t)__shfl_down((int)inv16, 2, 64),
                            i3 = (uint32_t)__shfl_down((int)inv16, 3, 64);
+            const uint32_t n1 = (uint32_t)__shfl_down((int)wild16, 1, 64), n2 = (uint32_t)__shfl_down((int)wild16, 2, 64),
+                           n3 = (uint32_t)__shfl_down((int)wild16, 3, 64);
             const uint64_t grp0 = o - (uint64_t)q * 16u;  // the group's first byte in the put
             if (grp0 < nbytes) {
                 const uint64_t gb = gstart + grp0;
@@ -145,6 +152,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ s
                 if (q == 0) {
                     gexc[gb >> 6] = ((uint64_t)exc16 << 48) | ((uint64_t)e1 << 32) | ((uint64_t)e2 << 16) | e3;
                     ginv[gb >> 6] = ((uint64_t)inv16 << 48) | ((uint64_t)i1 << 32) | ((uint64_t)i2 << 16) | i3;
+                    gwild[gb >> 6] = ((uint64_t)wild16 << 48) | ((uint64_t)n1 << 32) | ((uint64_t)n2 << 16) | n3;
                 }
             }
             // wave-aggregated reservation of run-index entries (rare: N runs, IUPAC bases)
@@ -199,7 +207,7 @@ __global__ void run_dir_kernel(const uint64_t* __restrict__ xr_start, uint64_t n
 static void free_genome(Genome* g) {
     if (!g) return;
     hipFree(g->xr_dir); hipFree(g->d_ucount);
-    hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv); hipFree(g->d_base); hipFree(g->d_len);
+    hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv); hipFree(g->gwild); hipFree(g->d_base); hipFree(g->d_len);
     hipFree(g->xr_start); hipFree(g->xr_char); hipFree(g->d_counter); hipFree(g->staging);
     delete g;
 }
@@ -239,7 +247,7 @@ static int put_device_bytes(Genome* g, uint32_t seq, uint64_t offset, const uint
     for (int attempt = 0; attempt < 2; ++attempt) {
         MP_HIP_CHECK(hipMemsetAsync(g->d_counter, 0, sizeof(unsigned long long), st));
         hipLaunchKernelGGL(pack_kernel, dim3(blocks), dim3(256), 0, st, dsrc, nbytes,
-                           g->base[seq] + offset, g->g2, g->gexc, g->ginv, g->xr_start, g->xr_char,
+                           g->base[seq] + offset, g->g2, g->gexc, g->ginv, g->gwild, g->xr_start, g->xr_char,
                            g->d_counter, g->xr_cap, g->n_xr, g->d_ucount);
         MP_HIP_CHECK(hipGetLastError());
         unsigned long long cnt = 0;
@@ -281,11 +289,11 @@ static int place(Genome* g) {
     const uint64_t off = g->total;
     const uint64_t w2 = off / 32 + 4, w1 = off / 64 + 4;
     if (off > g->plane_cap || !g->g2) {
-        hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv);
-        g->g2 = g->gexc = g->ginv = nullptr;
+        hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv); hipFree(g->gwild);
+        g->g2 = g->gexc = g->ginv = g->gwild = nullptr;
         g->plane_cap = 0;
         if (hipMalloc(&g->g2, w2 * 8) != hipSuccess || hipMalloc(&g->gexc, w1 * 8) != hipSuccess ||
-            hipMalloc(&g->ginv, w1 * 8) != hipSuccess)
+            hipMalloc(&g->ginv, w1 * 8) != hipSuccess || hipMalloc(&g->gwild, w1 * 8) != hipSuccess)
             return fail(MP_E_NOMEM, "mp_genome: device allocation failed");
         g->plane_cap = off;
     }
@@ -300,9 +308,10 @@ static int place(Genome* g) {
     }
     if (!g->d_counter && (hipMalloc(&g->d_counter, 64) != hipSuccess || hipMalloc(&g->d_ucount, 64) != hipSuccess))
         return fail(MP_E_NOMEM, "mp_genome: device allocation failed");
-    g->dev_bytes = (g->plane_cap / 32 + 4) * 8 + 2 * (g->plane_cap / 64 + 4) * 8 + g->xr_cap * 9;
+    g->dev_bytes = (g->plane_cap / 32 + 4) * 8 + 3 * (g->plane_cap / 64 + 4) * 8 + g->xr_cap * 9;
     if (hipMemset(g->d_ucount, 0, 64) != hipSuccess || hipMemset(g->g2, 0, w2 * 8) != hipSuccess ||
-        hipMemset(g->gexc, 0xFF, w1 * 8) != hipSuccess || hipMemset(g->ginv, 0xFF, w1 * 8) != hipSuccess)
+        hipMemset(g->gexc, 0xFF, w1 * 8) != hipSuccess || hipMemset(g->ginv, 0xFF, w1 * 8) != hipSuccess ||
+        hipMemset(g->gwild, 0, w1 * 8) != hipSuccess)
         return fail(MP_E_HIP, "mp_genome: memset failed");
     if (g->n_seq && (hipMemcpy(g->d_base, g->base.data(), g->n_seq * 8, hipMemcpyHostToDevice) != hipSuccess ||
                      hipMemcpy(g->d_len, g->len.data(), g->n_seq * 8, hipMemcpyHostToDevice) != hipSuccess))
@@ -403,8 +412,8 @@ MP_EXPORT int mp_genome_stats(void* genome, uint64_t* total_bases, uint64_t* n_e
     return MP_OK;
 }
 
-MP_EXPORT int mp_genome_download(void* genome, uint64_t* g2, uint64_t* gexc, uint64_t* ginv, uint64_t* xr_start,
-                                 uint8_t* xr_char) {
+MP_EXPORT int mp_genome_download(void* genome, uint64_t* g2, uint64_t* gexc, uint64_t* ginv, uint64_t* gwild,
+                                 uint64_t* xr_start, uint8_t* xr_char) {
     Genome* g = (Genome*)genome;
     if (!g) return fail(MP_E_ARG, "mp_genome_download: null genome");
     if (!g->sealed) return fail(MP_E_STATE, "mp_genome_download: genome not sealed");
@@ -412,6 +421,7 @@ MP_EXPORT int mp_genome_download(void* genome, uint64_t* g2, uint64_t* gexc, uin
     if (g2) MP_HIP_CHECK(hipMemcpy(g2, g->g2, g->total / 32 * 8, hipMemcpyDeviceToHost));
     if (gexc) MP_HIP_CHECK(hipMemcpy(gexc, g->gexc, g->total / 64 * 8, hipMemcpyDeviceToHost));
     if (ginv) MP_HIP_CHECK(hipMemcpy(ginv, g->ginv, g->total / 64 * 8, hipMemcpyDeviceToHost));
+    if (gwild) MP_HIP_CHECK(hipMemcpy(gwild, g->gwild, g->total / 64 * 8, hipMemcpyDeviceToHost));
     if (xr_start && g->n_xr) MP_HIP_CHECK(hipMemcpy(xr_start, g->xr_start, g->n_xr * 8, hipMemcpyDeviceToHost));
     if (xr_char && g->n_xr) MP_HIP_CHECK(hipMemcpy(xr_char, g->xr_char, g->n_xr, hipMemcpyDeviceToHost));
     return MP_OK;

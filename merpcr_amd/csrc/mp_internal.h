@@ -8,6 +8,9 @@
 //                  (engine.py:464-503)
 //           gexc : 1 bit/base, set where the base is not exactly A/C/G/T: the
 //                  primer compare must look the character up (engine.py:599-642)
+//           gwild: 1 bit/base, set where the base is 'N' (either case): under I = 1 every
+//                  IUPAC primer base matches it (engine.py:613-631), so the pair check
+//                  treats it as a wildcard without looking the character up
 //           xr_* : sorted run index of the exception characters (start, char)
 //   Sequences are laid end to end, each padded to a multiple of 64 bases; the
 //   padding is marked ginv = gexc = 1.  A "global" coordinate is the index in
@@ -160,6 +163,7 @@ struct Genome {
     uint64_t total = 0;               // padded bases
     uint64_t* g2 = nullptr;
     uint64_t* gexc = nullptr;
+    uint64_t* gwild = nullptr;                // 'N' bases (pair check under I = 1: they match any primer base)
     uint64_t* ginv = nullptr;
     uint64_t* d_base = nullptr;
     uint64_t* d_len = nullptr;

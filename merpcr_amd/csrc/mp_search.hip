@@ -43,6 +43,7 @@ struct ScanArgs {
     const uint64_t* g2;
     const uint64_t* gexc;
     const uint64_t* ginv;
+    const uint64_t* gwild;  // 'N' bases: under I = 1 they match every primer base with an IUPAC meaning
     const uint64_t* xr_start;
     const uint8_t* xr_char;
     const uint32_t* xr_dir;
@@ -368,9 +369,9 @@ __device__ __forceinline__ void stage_try_hit(const ScanArgs& a, HitStage& S, in
     if (S.n >= 64) stage_flush(a, S, lane);
 }
 
-// Pair-check staging per survivor: kPW 2-bit words, kPE exception words and
-// the four primer-2 accept planes, [slot][survivor] in the wave's LDS.  At M=50 and
-// primers of <= 25 bases every survivor fits (the tries span <= 125 bases).
+// Pair-check staging per survivor: kPW 2-bit words, kPE exception words (I = 0) or 'N'
+// words (I = 1) and the four primer-2 accept planes, [slot][survivor] in the wave's LDS.
+// At M=50 and primers of <= 25 bases every survivor fits (the tries span <= 125 bases).
 constexpr int kPW = 6, kPE = 4, kPSlots = kPW + kPE + 4;
 static_assert(MP_PBATCH <= 64, "pair-check batch is one survivor per lane");
 
@@ -434,12 +435,23 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         if (fast) {
 #pragma unroll
             for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[w0 + t] : 0ull;
-            // exception bits of the stretch [P0l, lastl] (at most 4 words of 64 bases)
+            // exception bits of the stretch [P0l, lastl] (at most 4 words of 64 bases).  Under
+            // I = 1 an 'N' matches every primer base with an IUPAC meaning (char_match,
+            // engine.py:613-631) -- exactly the positions with an accept-plane bit -- so the
+            // lane-parallel tries take 'N' as a wildcard from the staged 'N' words, and only
+            // the other exception characters make a stretch unclean
             uint64_t ew[kPE];
 #pragma unroll
             for (int t = 0; t < kPE; ++t) {
-                ew[t] = e0 + t <= el ? a.gexc[e0 + t] : 0ull;
-                pst[(kPW + t) * MP_PBATCH + lane] = ew[t];
+                const bool in = e0 + t <= el;
+                ew[t] = in ? a.gexc[e0 + t] : 0ull;
+                if (a.I) {
+                    const uint64_t wd = in ? a.gwild[e0 + t] : 0ull;
+                    ew[t] &= ~wd;
+                    pst[(kPW + t) * MP_PBATCH + lane] = wd;
+                } else {
+                    pst[(kPW + t) * MP_PBATCH + lane] = ew[t];
+                }
             }
             const uint32_t f0 = (uint32_t)(P0l & 63), f1 = (uint32_t)(lastl - (e0 << 6));  // stretch bits in word order
             uint64_t any = 0;
@@ -505,6 +517,18 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         uint64_t G = fun(sj[w0 * MP_PBATCH], sj[(w0 + 1) * MP_PBATCH]);
         uint64_t F = fun(sj[(w0 + 1) * MP_PBATCH], sj[min(w0 + 2, kPW - 1) * MP_PBATCH]);
         int nw = w0 + 2;
+        // I = 1: the 'N' bits of the same window, 64 bases per register (bit 63 = first base)
+        const uint64_t anyq = (Q0 | Q1 | Q2 | Q3) & kEven;
+        uint64_t WH = 0, WF = 0;
+        int nwe = 0;
+        if (a.I) {
+            const uint32_t v0 = (uint32_t)(sP0 & 63) + (uint32_t)t0, b6 = v0 & 63u;
+            const int e0w = min((int)(v0 >> 6), kPE - 2);
+            auto f1 = [&](uint64_t x0, uint64_t x1) { return b6 ? (x0 << b6) | (x1 >> (64 - b6)) : x0; };
+            WH = f1(sj[(kPW + e0w) * MP_PBATCH], sj[(kPW + e0w + 1) * MP_PBATCH]);
+            WF = f1(sj[(kPW + e0w + 1) * MP_PBATCH], sj[(kPW + min(e0w + 2, kPE - 1)) * MP_PBATCH]);
+            nwe = e0w + 2;
+        }
         const bool all_plain = __all(!slp || plain2);
         for (int32_t k = 0; k < chunk; ++k) {  // wave-uniform trip count
             const int32_t t = t0 + k;
@@ -516,6 +540,18 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
                 const uint64_t glo = G & kEven, ghi = (G >> 1) & kEven;
                 const uint64_t nlo = glo ^ kEven, nhi = ghi ^ kEven;
                 mm = ~((nhi & nlo & Q0) | (nhi & glo & Q1) | (ghi & nlo & Q2) | (ghi & glo & Q3)) & in2;
+            }
+            if (a.I) {
+                mm &= ~(spread32((uint32_t)(WH >> 32)) & anyq);
+                WH = (WH << 1) | (WF >> 63);
+                WF <<= 1;
+                if ((k & 63) == 63) {  // the next 64 bases
+                    const int w = min(nwe, kPE - 2);
+                    const uint64_t x0 = sj[(kPW + w) * MP_PBATCH], x1 = sj[(kPW + w + 1) * MP_PBATCH];
+                    const uint32_t b6 = (uint32_t)((sP0 & 63) + (uint64_t)t0) & 63u;
+                    WF = b6 ? (x0 << b6) | (x1 >> (64 - b6)) : x0;
+                    ++nwe;
+                }
             }
             const bool hit = t >= ta && t <= tb && !(mm & prot2) && __popcll(mm) <= a.N;
             stage_try_hit(a, S, lane, hit, sgk, srk, t - slo);
@@ -539,7 +575,7 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         const int jlo = (int)rl32((uint32_t)lo, j), jhi = (int)rl32((uint32_t)hi, j);
         const int ntry = jlo + jhi + 1;
         const uint64_t P0 = jgk + je - jl2 - (uint32_t)jlo;            // global start of the first try
-        if (rl32((uint32_t)fast, j)) {
+        if (rl32((uint32_t)fast, j) && !a.I) {  // I = 1: the staged words are 'N' bits, not exceptions
             const uint64_t* sj = pst + j;
             const uint64_t Q0 = sj[(kPW + kPE) * MP_PBATCH], Q1 = sj[(kPW + kPE + 1) * MP_PBATCH];
             const uint64_t Q2 = sj[(kPW + kPE + 2) * MP_PBATCH], Q3 = sj[(kPW + kPE + 3) * MP_PBATCH];
@@ -2571,7 +2607,7 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         }
         ScanArgs& a = *reinterpret_cast<ScanArgs*>(s->pend_args);
         a = ScanArgs{};
-        a.g2 = g->g2; a.gexc = g->gexc; a.ginv = g->ginv;
+        a.g2 = g->g2; a.gexc = g->gexc; a.ginv = g->ginv; a.gwild = g->gwild;
         a.xr_start = g->xr_start; a.xr_char = g->xr_char; a.xr_dir = g->xr_dir; a.n_xr = g->n_xr;
         a.has_u = g->has_u ? 1 : 0;
         a.seq_base = g->d_base; a.seq_len = g->d_len;

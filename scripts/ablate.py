@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--no-build", action="store_true", help="use variant libraries built beforehand (CPU side)")
     ap.add_argument("--shard-of", type=int, default=1, help="search only rank 0's owned range of an N-way split")
     args = ap.parse_args()
     from merpcr_amd import _build
@@ -54,6 +55,9 @@ def main():
                                                       os.path.join(tempfile.gettempdir(), f"mp_ablate_{v}"))
             src_tag = f"_ablate{v}"
         path = _build.LIB if v == "0" or v.startswith("opt:") else os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{tag}.so")
+        if args.no_build and os.path.exists(path):
+            libs[v] = path
+            continue
         saved = _build.SOURCE_FLAGS
         if flags is not None:
             _build.SOURCE_FLAGS = flags
@@ -103,6 +107,10 @@ def main():
         st = s.last_stats()
         out[v] = {"scan_ms": round(sum(ms) / len(ms), 3), "tail_ms": round(st["tail_ms"], 3), "pair_ms": round(st["pair_ms"], 3),
                   "hits": n, "candidates": st["candidates"], "survivors": st["survivors"]}
+        if hasattr(lib, "mp_debug_pair_counts"):  # variant 52: cumulative over all runs
+            pc = (ctypes.c_ulonglong * 8)()
+            lib.mp_debug_pair_counts(pc)
+            out[v]["pair_counts_cum"] = list(pc)
         print(f"variant {v}: {out[v]}", flush=True)
         s.close(); genome.close(); table.close()
         eng._dev_table = None

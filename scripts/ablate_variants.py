@@ -13,6 +13,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       with mp_debug_wave_times (a function only this variant exports)
   50  pair_kernel without the lane-parallel try loop
   51  pair_kernel without any try (prologue, primer-1 compare and staging only)
+  52  pair_kernel counting its per-survivor (non-lane-parallel) survivors by reason, read back
+      with mp_debug_pair_counts (a function only this variant exports)
 """
 import os
 import shutil
@@ -60,6 +62,17 @@ VARIANTS = {
                    "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_times), n * sizeof(ulonglong4)) == hipSuccess ? 0 : -1;\n}\n\n")],
     50: [(_LP, "    if (false)  // ablation 50\n")],
     51: [(_LP, "    if (false)  // ablation 51\n"), (_TODO, "    keep = false;  // ablation 51\n")],
+    52: [(_TODO, "    if (keep && !lp) {  // ablation 52\n"
+                 "        atomicAdd(&g_pair_counts[0], 1ull);\n"
+                 "        atomicAdd(&g_pair_counts[fast ? 2 : 1], 1ull);\n"
+                 "        if (r.l2 > 32u) atomicAdd(&g_pair_counts[3], 1ull);\n"
+                 "        if (lo + hi + 1 > 101) atomicAdd(&g_pair_counts[4], 1ull);\n"
+                 "    }\n"
+                 "    if (keep) atomicAdd(&g_pair_counts[5], 1ull);  // ablation 52\n"
+                 "    if (keep && lp) atomicAdd(&g_pair_counts[6], 1ull);  // ablation 52\n"),
+         ("// Pair-check staging per survivor", "__device__ unsigned long long g_pair_counts[8];  // ablation 52\n"),
+         (_T_TAIL, "MP_EXPORT int mp_debug_pair_counts(unsigned long long* out) {  // ablation 52\n"
+                   "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_counts), 8 * 8) == hipSuccess ? 0 : -1;\n}\n\n")],
 }
 
 

@@ -6,6 +6,7 @@ src/merpcr/io/fasta.py:60).  Per base u = upper-case(byte) (a-z only):
   g2    2 bits, A=0 C=1 G=2 T=U=3, every other byte 0; base j of a word at bits 63-2j..62-2j
   ginv  1 bit (bit 63-j): u not in A/C/G/T/U
   gexc  1 bit: u not exactly A/C/G/T
+  gwild 1 bit: u is 'N' (padding: 0)
   padding to 64 bases: code 0, ginv = gexc = 1
   run index: (global position, u) of every exception byte whose predecessor inside the
   same put is not the same exception character (sorted by position at seal).
@@ -35,6 +36,7 @@ def _reference(seqs, puts):
     code = np.zeros(total, dtype=np.uint64)
     exc = np.ones(total, dtype=bool)
     inv = np.ones(total, dtype=bool)
+    wild = np.zeros(total, dtype=bool)
     runs = []
     for q, s in enumerate(seqs):
         u = _upper(s)
@@ -47,6 +49,7 @@ def _reference(seqs, puts):
         code[b0:b0 + len(u)] = c
         exc[b0:b0 + len(u)] = ~acgt
         inv[b0:b0 + len(u)] = ~acgtu
+        wild[b0:b0 + len(u)] = u == ord("N")
     for q, off, n in puts:
         u = _upper(seqs[q][off:off + n])
         e = ~np.isin(u, np.frombuffer(b"ACGT", dtype=np.uint8))
@@ -60,7 +63,8 @@ def _reference(seqs, puts):
     bits = np.arange(63, -1, -1, dtype=np.uint64)
     ge = np.bitwise_or.reduce(exc.reshape(-1, 64).astype(np.uint64) << bits, axis=1)
     gi = np.bitwise_or.reduce(inv.reshape(-1, 64).astype(np.uint64) << bits, axis=1)
-    return g2, ge, gi, runs
+    gw = np.bitwise_or.reduce(wild.reshape(-1, 64).astype(np.uint64) << bits, axis=1)
+    return g2, ge, gi, gw, runs
 
 
 def _check(seqs, puts, device_src=False, misalign=0):
@@ -79,12 +83,13 @@ def _check(seqs, puts, device_src=False, misalign=0):
             g.put(q, chunk, offset=off, stream=stream)
     g.seal(stream)
     torch.cuda.synchronize()
-    g2, ge, gi, xs, xc = g.download()
+    g2, ge, gi, gw, xs, xc = g.download()
     g.close()
-    r2, re_, ri, runs = _reference(seqs, puts)
+    r2, re_, ri, rw, runs = _reference(seqs, puts)
     assert np.array_equal(g2, r2), np.nonzero(g2 != r2)[0][:5]
     assert np.array_equal(ge, re_), np.nonzero(ge != re_)[0][:5]
     assert np.array_equal(gi, ri), np.nonzero(gi != ri)[0][:5]
+    assert np.array_equal(gw, rw), np.nonzero(gw != rw)[0][:5]
     got = sorted(zip(xs.tolist(), xc.tolist()))
     assert got == runs, (len(got), len(runs), got[:5], runs[:5])
 
