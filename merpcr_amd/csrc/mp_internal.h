@@ -379,7 +379,9 @@ __host__ __device__ __forceinline__ int32_t try_offset(uint32_t r) {
 inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
 // internal entry points shared across TUs
-int sort_hits(Search* s, uint64_t n, hipStream_t st);
+// rocPRIM order of the run's n hits (the regions compacted first); the sorted (hi, lo)
+// arrays are returned for decode_kernel
+int sort_hits(Search* s, uint64_t n, hipStream_t st, const uint64_t** hi_out, const uint64_t** lo_out);
 bool sort_hits_device_ok(const Search* s);
 // The device sort's packing and bucketing of the 64-bit order key (k << low_bits | record
 // rank << try_bits | try rank; bucket = key >> shift), fixed per search before the scan.
@@ -400,6 +402,7 @@ size_t counter_bytes();  // the run counters' size (mp_search.hip)
 uint32_t* sort_bucket_counts(Search* s);          // the bucket count array (zeroed by the scan kernels)
 uint32_t* sort_bucket_offsets(Search* s);         // nb + 1 offsets
 uint32_t* sort_bucket_cursors(Search* s);
+unsigned long long* sort_region_counts(Search* s);  // the run's hit-region counts (finish_fold)
 int alloc_sort_slots(Search* s, const SortPlan& P);  // mode 0's slot array for plan P
 
 // Raw hits arrive in runs of one bucket (a survivor's tries, a wave's batch of nearby
@@ -480,6 +483,58 @@ __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32
 
 int alloc_sort_buckets(Search* s);                // the device sort's bucket arrays (at create)
 constexpr int kSortOverflow = 6;                  // counters[6]: a device-sort bucket overflowed
+
+// Run counters (Search::counters, uint64 words).  Statistics and work queues live 256 B apart
+// (kStatStride words): thousands of waves on one address serialise (~88 returning atomics per
+// microsecond, MI355X_MICROARCH.md "dequeue").
+//   [0..8)          run results, copied to the host words at the run's finish
+//   kStatBase       64 candidate / survivor statistic slots
+//   kPairQBase      8 pair_kernel batch counters (one per XCD group)
+//   kSchedBase      8 scan super-step chunk counters
+//   kHitBase        8 hit-list reservation counters: region x of the hit list (hit_hi / hit_lo /
+//                   sort_keys at [x * cap_r, (x + 1) * cap_r)) belongs to the pair blocks of
+//                   XCD group x, so the hit flushes of a run spread over eight words (c4: 25k
+//                   flushes on one word were ~0.28 ms of serialised atomics)
+constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
+constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;
+constexpr int kSchedBase = kPairQBase + 8 * kStatStride;
+constexpr int kHitBase = kSchedBase + 8 * kStatStride;
+constexpr int kHitRegions = 8;
+constexpr size_t kCounterBytes = (size_t)(kHitBase + kHitRegions * kStatStride) * 8;
+constexpr int kHitMaxRegion = 8;                  // host word 8: the largest region count of the run
+constexpr int kHostWords = 16;                    // device-mapped host words per search
+
+// The run's finish, by one workgroup after the last producer (pair_kernel): counters[0..8)
+// to the host words with word 0 = the hit total (the sum of the region counts) and word
+// kHitMaxRegion = the largest region count (capacity check), the region counts to rcount
+// (device copy for the order kernels), then every counter zeroed for the next run.
+__device__ __forceinline__ void finish_fold(unsigned long long* __restrict__ counters, uint32_t n_words,
+                                            unsigned long long* __restrict__ h_out,
+                                            unsigned long long* __restrict__ rcount) {
+    unsigned long long v = 0, r = 0;
+    if (threadIdx.x < 8) {
+        v = counters[threadIdx.x];
+        r = counters[kHitBase + threadIdx.x * kStatStride];
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n_words; i += blockDim.x) counters[i] = 0ull;
+    if (threadIdx.x < 64) {  // wave 0: the region sum and maximum over lanes 0..7
+        unsigned long long sum = r, mx = r;
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const unsigned long long ys = (unsigned long long)__shfl_xor((long long)sum, o, 64);
+            const unsigned long long ym = (unsigned long long)__shfl_xor((long long)mx, o, 64);
+            sum += ys;
+            mx = ym > mx ? ym : mx;
+        }
+        if (threadIdx.x < 8) {
+            rcount[threadIdx.x] = r;
+            h_out[threadIdx.x] = threadIdx.x == 0 ? sum : v;
+            if (threadIdx.x == 0) h_out[kHitMaxRegion] = mx;
+            __threadfence_system();  // the host polls the run's event, then reads these
+        }
+    }
+}
 int sort_runs(Genome* g, hipStream_t st);
 
 }  // namespace mp

@@ -19,7 +19,7 @@ static unsigned bits_for(uint64_t v) {
 
 // ---------------------------------------------------------------- device-count bucket sort
 // The common case (the order key fits 64 bits) sorts without the host knowing the hit
-// count: it is read from counters[0] on the device, so the sort follows pair_kernel on
+// count: pair_kernel counts every key's bucket as it writes it, so the sort follows it on
 // the stream with no host round trip.  Keys are bucketed by their top bits (global k:
 // hits spread over the genome), counted, scattered, and each bucket is ranked in LDS by
 // one workgroup that writes the decoded mp_hit records straight to the output.  A bucket
@@ -28,49 +28,19 @@ static unsigned bits_for(uint64_t v) {
 constexpr uint32_t kSortCap = 2048;
 constexpr unsigned kMaxBucketBits = 16;
 
-__global__ void bucket_hist(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
-                            const unsigned long long* __restrict__ counters, uint64_t cap, unsigned try_bits,
-                            unsigned low_bits, unsigned shift, uint64_t* __restrict__ keys, uint32_t* __restrict__ cnt) {
-    const uint64_t n = counters[0] < cap ? counters[0] : cap;
-    const int lane = threadIdx.x & 63;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
-        const uint64_t i = base + (uint64_t)lane;  // wave-uniform loop: the ballots see every lane
-        const bool on = i < n;
-        uint32_t b = 0xFFFFFFFFu;
-        if (on) {
-            const uint64_t l = lo[i];
-            const uint64_t key = (hi[i] << low_bits) | ((l >> 32) << try_bits) | (l & 0xFFFFFFFFull);
-            keys[i] = key;
-            b = (uint32_t)(key >> shift);
-        }
-        uint32_t head, len;
-        bucket_runs(b, on, lane, head, len);
-        if (on && head == (uint32_t)lane) atomicAdd(&cnt[b], len);
-    }
-}
-
 // Exclusive scan of the bucket counts by one 1024-thread workgroup (bucket_offsets_block,
-// mp_internal.h).  With h_out it is also the run's finish: pair_kernel, the last producer of
-// the counters, is complete, so counters[0..8) go to the device-mapped host words the host
-// polls and every counter is zeroed for the next run (the sort after it reports an overflow
-// straight to h_out[kSortOverflow]; the scatter takes the hit count from off[nb]).
+// mp_internal.h).  With h_out it is also the run's finish (finish_fold): pair_kernel, the
+// last producer of the counters, is complete, so they go to the device-mapped host words the
+// host polls, the hit-region counts to rcount for the scatter, and every counter is zeroed
+// for the next run (the sort after it reports an overflow straight to h_out[kSortOverflow]).
 __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restrict__ cnt, uint32_t nb,
                                                        uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
                                                        unsigned long long* __restrict__ counters, uint32_t n_words,
-                                                       unsigned long long* __restrict__ h_out) {
+                                                       unsigned long long* __restrict__ h_out,
+                                                       unsigned long long* __restrict__ rcount) {
     __shared__ uint4 s_v4[kOffTile / 4];
     __shared__ uint32_t s_w[16];
-    if (h_out) {
-        unsigned long long v = 0;
-        if (threadIdx.x < 8) v = counters[threadIdx.x];
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < n_words; i += blockDim.x) counters[i] = 0ull;
-        if (threadIdx.x < 8) {
-            h_out[threadIdx.x] = v;
-            __threadfence_system();
-        }
-    }
+    if (h_out) finish_fold(counters, n_words, h_out, rcount);
     bucket_offsets_block(cnt, nb, off, cursor, s_v4, s_w);
 }
 
@@ -80,15 +50,17 @@ __device__ __forceinline__ void flag_overflow(unsigned long long* h_out) {
     __hip_atomic_store(&h_out[kSortOverflow], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void bucket_scatter(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off, uint32_t nb,
-                               uint64_t cap, unsigned shift, uint32_t* __restrict__ cursor, uint64_t* __restrict__ out) {
-    const uint64_t n = off[nb] < cap ? off[nb] : cap;  // the hit count (bucket_offsets' total)
+// The keys of every hit-list region (its first min(rcount[x], cap_r) slots) into bucket order.
+__global__ void bucket_scatter(const uint64_t* __restrict__ keys, const unsigned long long* __restrict__ rcount,
+                               uint64_t cap_r, unsigned shift, uint32_t* __restrict__ cursor, uint64_t* __restrict__ out) {
     const int lane = threadIdx.x & 63;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n; base += stride) {
+    for (uint32_t x = 0; x < (uint32_t)kHitRegions; ++x)
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u), n = rcount[x] < cap_r ? rcount[x] : cap_r;
+         base < n; base += stride) {
         const uint64_t i = base + (uint64_t)lane;
         const bool on = i < n;
-        const uint64_t key = on ? keys[i] : 0ull;
+        const uint64_t key = on ? keys[x * cap_r + i] : 0ull;
         const uint32_t b = on ? (uint32_t)(key >> shift) : 0xFFFFFFFFu;
         uint32_t head, len;
         bucket_runs(b, on, lane, head, len);
@@ -252,7 +224,8 @@ bool sort_hits_device_ok(const Search* s) {
 }
 
 int alloc_sort_buckets(Search* s) {
-    if (!s->bucket) MP_HIP_CHECK(hipMalloc(&s->bucket, (3ull << kMaxBucketBits) * 4 + 16));
+    // counts, nb + 1 offsets, cursors, then the hit-region counts (16-B aligned)
+    if (!s->bucket) MP_HIP_CHECK(hipMalloc(&s->bucket, (3ull << kMaxBucketBits) * 4 + 16 + kHitRegions * 8));
     return MP_OK;
 }
 
@@ -276,6 +249,9 @@ SortPlan sort_plan(const Search* s) {
 uint32_t* sort_bucket_counts(Search* s) { return s->bucket; }
 uint32_t* sort_bucket_offsets(Search* s) { return s->bucket + (1u << kMaxBucketBits); }
 uint32_t* sort_bucket_cursors(Search* s) { return s->bucket + 2 * (1u << kMaxBucketBits) + 1; }
+unsigned long long* sort_region_counts(Search* s) {
+    return reinterpret_cast<unsigned long long*>(s->bucket + 3 * (1u << kMaxBucketBits) + 4);
+}
 
 int alloc_sort_slots(Search* s, const SortPlan& P) {
     const size_t need = (size_t)P.nb * P.slot_cap * sizeof(uint64_t);
@@ -299,7 +275,7 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     // kernel needs an agent-scope release per block (buffer_wbl2 of the XCD's L2, several
     // us each across the persistent grid), measured +65 us on a 1/8 c3 step.
     hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, sort_bucket_counts(s), P.nb, off, cursor,
-                       s->counters, (uint32_t)(counter_bytes() / 8), finish ? s->d_hcnt : nullptr);
+                       s->counters, (uint32_t)(counter_bytes() / 8), finish ? s->d_hcnt : nullptr, sort_region_counts(s));
     MP_HIP_CHECK(hipGetLastError());
     if (mode == 0) {
         hipLaunchKernelGGL(sort_decode_slots, dim3((P.nb + kSlotWaves - 1) / kSlotWaves), dim3(64 * kSlotWaves), 0, st,
@@ -309,8 +285,8 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
         return MP_OK;
     }
     const uint32_t grid = (uint32_t)std::min<uint64_t>((s->cap + 255) / 256, 2048);
-    hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, off, P.nb, s->cap, P.shift, cursor,
-                       s->tmp_hi);
+    hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, sort_region_counts(s),
+                       s->cap / kHitRegions, P.shift, cursor, s->tmp_hi);
     MP_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
                        s->tmp_hi, off, P.nb, P.try_bits, P.low_bits,

@@ -87,6 +87,7 @@ struct ScanArgs {
     uint64_t* hit_lo;
     unsigned long long* counters;
     uint64_t cap;
+    uint64_t cap_r;         // hit-list region capacity (cap / kHitRegions), see kHitBase
     uint4* surv;
     uint64_t surv_cap;
     uint4* tails;           // bucket-tail references (2 x uint4 each), see tail_kernel
@@ -114,13 +115,10 @@ __device__ __forceinline__ uint64_t umin64(uint64_t x, uint64_t y) { return x < 
 __device__ __forceinline__ uint64_t umax64(uint64_t x, uint64_t y) { return x > y ? x : y; }
 
 // Candidate / survivor statistics (counters[1], counters[3]) are summed from 64 slots
-// 256 B apart: thousands of waves ending together serialise on one address (~11 ns per
-// atomic, MI355X_MICROARCH.md) -- measured ~0.1 ms on tail_kernel's exit.  pair_kernel
-// folds the slots into counters[1] and counters[3] before the host reads them.
-constexpr int kStatBase = 32, kStatSlots = 64, kStatStride = 32;
-constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;  // pair_kernel batch counters, 8 x 256 B
-constexpr int kSchedBase = kPairQBase + 8 * kStatStride;  // scan super-step chunk counters, 8 x 256 B
-constexpr size_t kCounterBytes = (size_t)(kSchedBase + 8 * kStatStride) * 8;
+// 256 B apart (counter layout: mp_internal.h): thousands of waves ending together serialise
+// on one address (~11 ns per atomic, MI355X_MICROARCH.md) -- measured ~0.1 ms on
+// tail_kernel's exit.  pair_kernel folds the slots into counters[1] and counters[3] before
+// the host reads them.
 size_t counter_bytes() { return kCounterBytes; }
 #ifndef MP_PDYN_BATCH
 #define MP_PDYN_BATCH 64
@@ -217,13 +215,21 @@ __device__ __forceinline__ uint32_t compress_even(uint64_t x) {
 // protected mismatch or more than N.
 __device__ __forceinline__ bool chunk_ok(const ScanArgs& a, uint64_t G, uint32_t ex, uint64_t P0, uint64_t P1,
                                          uint64_t P2, uint64_t P3, uint64_t gpos_c, uint32_t ch_c, int len, uint32_t c,
-                                         uint32_t L, bool plus, int& mm) {
+                                         uint32_t L, bool plus, int& mm, uint32_t wild = 0u) {
     const uint64_t lo = G & kEven, hi = (G >> 1) & kEven;
     const uint64_t nlo = lo ^ kEven, nhi = hi ^ kEven;
     const uint64_t match = (nhi & nlo & P0) | (nhi & lo & P1) | (hi & nlo & P2) | (hi & lo & P3);
     const uint64_t inside = sp_lt(len);
     uint64_t mmv = ~match & inside;
     if (len < 32) ex &= ~(0xFFFFFFFFu >> len);
+    if (a.I && (ex & wild)) {
+        // I = 1: a genome 'N' (wild, a subset of ex) matches exactly the primer bases with an
+        // IUPAC meaning -- the positions with an accept-plane bit (char_match) -- so it
+        // needs no run lookup; its 2-bit code (A) already left the other positions mismatched
+        wild &= ex;
+        mmv &= ~(spread32(wild) & (P0 | P1 | P2 | P3) & kEven);
+        ex &= ~wild;
+    }
     if (ex && !a.I) {
         // literal compare (I=0): where the primer base is one of A/C/G/T (a plane bit set),
         // a genome exception character (never exactly A/C/G/T) cannot equal it -- a
@@ -256,8 +262,9 @@ __device__ __forceinline__ bool primer_ok(const ScanArgs& a, uint64_t gpos, uint
         const int len = (int)min(32u, L - c);
         const uint64_t G = ext2(a.g2, gpos + c);
         const uint32_t ex = (uint32_t)(ext1(a.gexc, gpos + c) >> 32);
+        const uint32_t wl = a.I && ex ? (uint32_t)(ext1(a.gwild, gpos + c) >> 32) : 0u;
         const uint64_t* P = a.planes + (uint64_t)(pl + (c >> 5)) * 4;
-        if (!chunk_ok(a, G, ex, P[0], P[1], P[2], P[3], gpos + c, ch + c, len, c, L, plus, mm)) return false;
+        if (!chunk_ok(a, G, ex, P[0], P[1], P[2], P[3], gpos + c, ch + c, len, c, L, plus, mm, wl)) return false;
     }
     return true;
 }
@@ -305,22 +312,26 @@ struct HitStage {
     uint32_t n;
 };
 
-// The stage's hits at hit list slots off, off + 1, ...: the raw (hi, lo) pair and, for the
-// fused device sort, the packed order key and its bucket count (bucket_hist's work).
+// The block's hit-list region (kHitBase): one per XCD group of pair blocks.
+__device__ __forceinline__ uint32_t hit_region() { return blockIdx.x & (uint32_t)(kHitRegions - 1); }
+
+// The stage's hits at slots off, off + 1, ... of the block's hit-list region: the raw
+// (hi, lo) pair and, for the fused device sort, the packed order key and its bucket count.
 // Wave-uniform (the bucket runs ballot).
 __device__ __forceinline__ void write_hits(const ScanArgs& a, const HitStage& S, uint64_t off, int lane) {
+    const uint64_t r0 = (uint64_t)hit_region() * a.cap_r;
     for (uint32_t b0 = 0; b0 < S.n; b0 += 64) {
         const uint32_t i = b0 + (uint32_t)lane;
-        const bool on = i < S.n && off + i < a.cap;
+        const bool on = i < S.n && off + i < a.cap_r;
         uint32_t bk = 0xFFFFFFFFu;
         uint64_t key = 0;
         if (on) {
             const uint64_t hi = S.hi[i], lo = S.lo[i];
-            a.hit_hi[off + i] = hi;
-            a.hit_lo[off + i] = lo;
+            a.hit_hi[r0 + off + i] = hi;
+            a.hit_lo[r0 + off + i] = lo;
             if (a.sort_cnt) {
                 key = (hi << a.sort_low_bits) | ((lo >> 32) << a.sort_try_bits) | (lo & 0xFFFFFFFFull);
-                a.sort_keys[off + i] = key;
+                a.sort_keys[r0 + off + i] = key;
                 bk = (uint32_t)(key >> a.sort_shift);
             }
         }
@@ -343,7 +354,7 @@ __device__ __forceinline__ void stage_flush(const ScanArgs& a, HitStage& S, int 
     const uint32_t cnt = S.n;
     if (!cnt) return;
     unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(&a.counters[0], (unsigned long long)cnt);
+    if (lane == 0) base = atomicAdd(&a.counters[kHitBase + hit_region() * kStatStride], (unsigned long long)cnt);
     base = (unsigned long long)__shfl((long long)base, 0, 64);
     write_hits(a, S, base, lane);
     wave_sync_lds();
@@ -2116,7 +2127,7 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
         for (int q = 0; q < kPairWaves; ++q) tot += s_st[q].n;
-        s_base = tot ? atomicAdd(&a.counters[0], (unsigned long long)tot) : 0ull;
+        s_base = tot ? atomicAdd(&a.counters[kHitBase + hit_region() * kStatStride], (unsigned long long)tot) : 0ull;
     }
     __syncthreads();
     const int w = threadIdx.x >> 6;
@@ -2125,18 +2136,12 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     write_hits(a, S, off, lane);
 }
 
-// The run's last kernel: counters[0..8) into the device-mapped pinned words the host polls
-// (no copy), then every counter zeroed for the next run (no fill before it).
+// The run's last kernel in order mode 2 (finish_fold: the counters into the device-mapped
+// pinned words the host polls, then zeroed for the next run).
 __global__ __launch_bounds__(1024) void finish_kernel(unsigned long long* __restrict__ counters, uint32_t n_words,
-                                                      unsigned long long* __restrict__ h_out) {
-    unsigned long long v = 0;
-    if (threadIdx.x < 8) v = counters[threadIdx.x];
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n_words; i += blockDim.x) counters[i] = 0ull;
-    if (threadIdx.x < 8) {
-        h_out[threadIdx.x] = v;
-        __threadfence_system();  // one wave: the host polls the run's event, then reads these
-    }
+                                                      unsigned long long* __restrict__ h_out,
+                                                      unsigned long long* __restrict__ rcount) {
+    finish_fold(counters, n_words, h_out, rcount);
 }
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
@@ -2193,6 +2198,7 @@ static void free_search(Search* s) {
 }
 
 static int alloc_hits(Search* s, uint64_t cap) {
+    cap = (cap + kHitRegions - 1) / kHitRegions * kHitRegions;  // whole regions
     hipFree(s->keys); hipFree(s->tmp_hi); hipFree(s->tmp_lo); hipFree(s->out);
     s->keys = s->tmp_hi = s->tmp_lo = nullptr;
     s->out = nullptr;
@@ -2292,12 +2298,12 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
             break;
         }
         // device-mapped pinned words: finish_kernel writes the run's counters straight into them
-        if (hipHostMalloc((void**)&s->h_cnt, 16 * sizeof(unsigned long long), hipHostMallocMapped) != hipSuccess ||
+        if (hipHostMalloc((void**)&s->h_cnt, kHostWords * sizeof(unsigned long long), hipHostMallocMapped) != hipSuccess ||
             hipHostGetDevicePointer((void**)&s->d_hcnt, (void*)s->h_cnt, 0) != hipSuccess) {
             rc = fail(MP_E_NOMEM, "pinned counter allocation failed");
             break;
         }
-        std::memset((void*)s->h_cnt, 0, 16 * sizeof(unsigned long long));
+        std::memset((void*)s->h_cnt, 0, kHostWords * sizeof(unsigned long long));
         if (hipMemset(s->counters, 0, kCounterBytes) != hipSuccess) { rc = fail(MP_E_HIP, "counter reset failed"); break; }
         rc = alloc_hits(s, kDefaultHitCap);
         if (!rc) rc = alloc_surv(s, kDefaultSurvCap);
@@ -2322,6 +2328,7 @@ static int set_lists(Search* s, ScanArgs& a, int mode) {
     a.hit_lo = s->keys + s->cap;
     a.counters = s->counters;
     a.cap = s->cap;
+    a.cap_r = s->cap / kHitRegions;
     a.surv = s->surv;
     a.surv_cap = s->surv_cap;
     a.tails = s->tails;
@@ -2422,7 +2429,8 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         const int rc = sort_hits_device(s, st, mode, true);
         if (rc) return rc;
     } else {
-        hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(1024), 0, st, s->counters, (uint32_t)(kCounterBytes / 8), s->d_hcnt);
+        hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(1024), 0, st, s->counters, (uint32_t)(kCounterBytes / 8), s->d_hcnt,
+                           sort_region_counts(s));
         MP_HIP_CHECK(hipGetLastError());
     }
     MID_EVENT(hipEventRecord(s->ev3, st));
@@ -2433,7 +2441,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
 // Wait for the enqueued run and read its counters (written by finish_kernel).
 static int wait_counts(Search* s, unsigned long long* cnt) {
     MP_HIP_CHECK(poll_event(s->evd));
-    std::memcpy(cnt, (const void*)s->h_cnt, 8 * sizeof(unsigned long long));
+    std::memcpy(cnt, (const void*)s->h_cnt, kHostWords * sizeof(unsigned long long));
     return MP_OK;
 }
 
@@ -2455,11 +2463,13 @@ static int redo_order(Search* s, hipStream_t st, int from, uint64_t nh) {
             if (!s->h_cnt[kSortOverflow]) break;
             continue;
         }
-        const int rc = sort_hits(s, nh, st);
+        const uint64_t* hi = nullptr;
+        const uint64_t* lo = nullptr;
+        const int rc = sort_hits(s, nh, st, &hi, &lo);
         if (rc) return rc;
         if (nh) {
             const uint32_t blocks = (uint32_t)((nh + 255) / 256);
-            hipLaunchKernelGGL(decode_kernel, dim3(blocks), dim3(256), 0, st, s->keys, s->keys + s->cap, nh,
+            hipLaunchKernelGGL(decode_kernel, dim3(blocks), dim3(256), 0, st, hi, lo, nh,
                                g->d_base, g->d_len, g->n_seq, t->inv_rank, t->recs, s->out);
             MP_HIP_CHECK(hipGetLastError());
         }
@@ -2473,7 +2483,7 @@ static int search_complete(Search* s, uint64_t* n_hits) {
     ScanArgs& a = *reinterpret_cast<ScanArgs*>(s->pend_args);
     const int mode0 = s->pend_mode;
     int mode = mode0;
-    unsigned long long cnt[8];
+    unsigned long long cnt[kHostWords];
     int rc = wait_counts(s, cnt);
     if (rc) return rc;
     if (s->scan_timing || s->stage_timing) MP_HIP_CHECK(hipEventElapsedTime(&s->scan_ms, s->ev0, s->evt));
@@ -2481,12 +2491,17 @@ static int search_complete(Search* s, uint64_t* n_hits) {
     MID_EVENT(hipEventElapsedTime(&s->tail_ms, s->evt, s->ev1));
     // A list that overflowed is grown and the whole run enqueued again (rare: the first runs of
     // a handle); kernels never write past a capacity.
-    for (int attempt = 0; cnt[2] > s->surv_cap || cnt[4] > s->tails_cap || cnt[0] > s->cap; ++attempt) {
+    // (the hit list overflows when one of its regions does: cnt[kHitMaxRegion] > cap / kHitRegions)
+    for (int attempt = 0;
+         cnt[2] > s->surv_cap || cnt[4] > s->tails_cap || cnt[kHitMaxRegion] > s->cap / kHitRegions; ++attempt) {
         if (attempt == 3) return fail(MP_E_STATE, "mp_search_run: list overflow after growth");
         ++s->n_regrowths;
         if (cnt[4] > s->tails_cap) rc = alloc_tails(s, cnt[4] + cnt[4] / 4 + 1024);
         if (!rc && cnt[2] > s->surv_cap) rc = alloc_surv(s, cnt[2] + cnt[2] / 2 + 1024);
-        if (!rc && cnt[0] > s->cap) rc = alloc_hits(s, cnt[0] + cnt[0] / 4 + 1024);
+        if (!rc && cnt[kHitMaxRegion] > s->cap / kHitRegions) {
+            const uint64_t mx = cnt[kHitMaxRegion];
+            rc = alloc_hits(s, kHitRegions * (mx + mx / 4 + 1024));
+        }
         mode = sort_hits_device_ok(s) ? s->order_mode : 2;
         if (!rc) rc = set_lists(s, a, mode);
         if (!rc) rc = enqueue_kernels(s, a, s->pend_tiles, st, mode);

@@ -15,6 +15,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
   51  pair_kernel without any try (prologue, primer-1 compare and staging only)
   52  pair_kernel counting its per-survivor (non-lane-parallel) survivors by reason, read back
       with mp_debug_pair_counts (a function only this variant exports)
+  54  pair_kernel without the primer-1 compare (every fingerprint survivor kept)
+  55  pair_kernel's lane-parallel tries computed but never staged (no hits written)
 """
 import os
 import shutil
@@ -29,6 +31,8 @@ _STAGE = "    {\n        static_assert(kLdsFilterWords / 4 == 8 * kBlock, \"eigh
 _LP = "    if (__any(lp)) {\n"
 _TODO = "    uint64_t todo = __ballot(keep && !lp);\n"
 
+_P1 = "    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);\n"
+_LPHIT = "            stage_try_hit(a, S, lane, hit, sgk, srk, t - slo);\n"
 _T_ENTRY = "    zero_sort_counts(a);\n    // stage the seed prefilter in LDS (once per persistent workgroup)"
 _T_STAGED = "    const int lane = threadIdx.x & 63;\n    const int w = threadIdx.x >> 6;\n    const uint64_t stride = (uint64_t)gridDim.x * kWaves;"
 _T_END = "    close_chunked(a.surv, a.surv_cap, lane, C);\n    close_chunked<2>(a.tails, a.tails_cap, lane, TC);"
@@ -73,6 +77,8 @@ VARIANTS = {
          ("// Pair-check staging per survivor", "__device__ unsigned long long g_pair_counts[8];  // ablation 52\n"),
          (_T_TAIL, "MP_EXPORT int mp_debug_pair_counts(unsigned long long* out) {  // ablation 52\n"
                    "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_counts), 8 * 8) == hipSuccess ? 0 : -1;\n}\n\n")],
+    54: [(_P1, "    if (true) {} else  // ablation 54\n")],
+    55: [(_LPHIT, "            if (hit && t < -1000000) // ablation 55\n")],
 }
 
 
