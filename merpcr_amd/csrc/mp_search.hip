@@ -505,11 +505,14 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         const uint64_t* sj = pst + s;
         const uint64_t Q0 = sj[(kPW + kPE) * MP_PBATCH], Q1 = sj[(kPW + kPE + 1) * MP_PBATCH];
         const uint64_t Q2 = sj[(kPW + kPE + 2) * MP_PBATCH], Q3 = sj[(kPW + kPE + 3) * MP_PBATCH];
-        const uint64_t in2 = sp_lt((int)sl2);
-        const uint64_t two = (Q0 & Q1) | (Q0 & Q2) | (Q0 & Q3) | (Q1 & Q2) | (Q1 & Q3) | (Q2 & Q3);
-        const bool plain2 = two == 0 && ((Q0 | Q1 | Q2 | Q3) & in2) == in2;
-        const uint64_t code2 = ((Q1 | Q3) & kEven) | (((Q2 | Q3) & kEven) << 1);
-        const uint64_t prot2 = sp_lt(min(a.X, (int)sl2));  // '-' strand: positions < X
+        // per-base 32-bit masks (bit 31-i = primer-2 position i): the accept planes, the
+        // positions compared, the protected ones ('-' strand: positions < X)
+        const uint32_t q0 = compress_even(Q0), q1 = compress_even(Q1), q2 = compress_even(Q2),
+                       q3 = compress_even(Q3);
+        const uint32_t in32 = sl2 >= 32u ? ~0u : ~(~0u >> sl2);
+        const uint32_t px = (uint32_t)min(a.X, (int)sl2);
+        const uint32_t prot32 = px >= 32u ? ~0u : ~(~0u >> px);
+        const uint32_t anyq = (q0 | q1 | q2 | q3) & in32;
         // try t (d = t - lo) is in bounds for t in [ta, lo + hi] (engine.py:548-560: a
         // non-positive offset needs the product to end past primer 1, and the window inside
         // the sequence, which hi already guarantees)
@@ -521,56 +524,66 @@ __device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_su
         for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o, 64));
         const int32_t chunk = (tmax + (int32_t)ngrp - 1) / (int32_t)ngrp;
         const int32_t t0 = (int32_t)grp * chunk;
-        const uint32_t u0 = (uint32_t)(sP0 & 31) + (uint32_t)t0;  // first base of try t0 in the staged words
+        // The window of try t0 + k is bases u0 + k .. u0 + k + 31 of the staged stretch, held as
+        // three bit planes -- the low and high bit of each base's 2-bit code and (I = 1) its
+        // 'N' bit -- in 64-bit shift registers whose top 32 bits are the window: one shift per
+        // plane per try, 32 new bases every 32 tries.  Compared through the planes with three
+        // bit selects (match = hi ? (lo ? q3 : q2) : (lo ? q1 : q0)), where the 2-bit form
+        // spent ~70 VALU per try (c4's pair kernel was VALU-bound, 80% of its issue cycles).
+        const uint32_t u0 = (uint32_t)(sP0 & 31) + (uint32_t)t0;  // staged-word base of try t0
         const uint32_t a5 = u0 & 31u;
         const int w0 = min((int)(u0 >> 5), kPW - 2);
-        auto fun = [&](uint64_t x0, uint64_t x1) { return a5 ? (x0 << (2 * a5)) | (x1 >> (64 - 2 * a5)) : x0; };
-        uint64_t G = fun(sj[w0 * MP_PBATCH], sj[(w0 + 1) * MP_PBATCH]);
-        uint64_t F = fun(sj[(w0 + 1) * MP_PBATCH], sj[min(w0 + 2, kPW - 1) * MP_PBATCH]);
-        int nw = w0 + 2;
-        // I = 1: the 'N' bits of the same window, 64 bases per register (bit 63 = first base)
-        const uint64_t anyq = (Q0 | Q1 | Q2 | Q3) & kEven;
-        uint64_t WH = 0, WF = 0;
-        int nwe = 0;
-        if (a.I) {
-            const uint32_t v0 = (uint32_t)(sP0 & 63) + (uint32_t)t0, b6 = v0 & 63u;
-            const int e0w = min((int)(v0 >> 6), kPE - 2);
-            auto f1 = [&](uint64_t x0, uint64_t x1) { return b6 ? (x0 << b6) | (x1 >> (64 - b6)) : x0; };
-            WH = f1(sj[(kPW + e0w) * MP_PBATCH], sj[(kPW + e0w + 1) * MP_PBATCH]);
-            WF = f1(sj[(kPW + e0w + 1) * MP_PBATCH], sj[(kPW + min(e0w + 2, kPE - 1)) * MP_PBATCH]);
-            nwe = e0w + 2;
+        // 'N' words are 64-base words from (P0 >> 6) << 6: 32-base word w of the 2-bit grid is
+        // half wd of them, wd = w + ((P0 >> 5) & 1)
+        const int wdel = (int)((sP0 >> 5) & 1u);
+        auto word32 = [&](int w, uint32_t& lo_, uint32_t& hi_, uint32_t& wi_) {
+            const uint64_t x = sj[min(w, kPW - 1) * MP_PBATCH];
+            lo_ = compress_even(x);
+            hi_ = compress_even(x >> 1);
+            wi_ = 0u;
+            if (a.I) {
+                const int wd = min(w + wdel, 2 * kPE - 1);
+                const uint64_t y = sj[(kPW + (wd >> 1)) * MP_PBATCH];
+                wi_ = (wd & 1) ? (uint32_t)y : (uint32_t)(y >> 32);
+            }
+        };
+        // 32 bases starting a5 into word w: the refill value of each plane
+        auto fill = [&](int w, uint32_t& lo_, uint32_t& hi_, uint32_t& wi_) {
+            uint32_t l0, h0, n0, l1, h1, n1;
+            word32(w, l0, h0, n0);
+            word32(w + 1, l1, h1, n1);
+            lo_ = a5 ? (l0 << a5) | (l1 >> (32u - a5)) : l0;
+            hi_ = a5 ? (h0 << a5) | (h1 >> (32u - a5)) : h0;
+            wi_ = a5 ? (n0 << a5) | (n1 >> (32u - a5)) : n0;
+        };
+        uint64_t SL, SH, SW;
+        {
+            uint32_t l0, h0, n0, l1, h1, n1;
+            fill(w0, l0, h0, n0);
+            fill(w0 + 1, l1, h1, n1);
+            SL = ((uint64_t)l0 << 32) | l1;
+            SH = ((uint64_t)h0 << 32) | h1;
+            SW = ((uint64_t)n0 << 32) | n1;
         }
-        const bool all_plain = __all(!slp || plain2);
+        int nw = w0 + 2;
         for (int32_t k = 0; k < chunk; ++k) {  // wave-uniform trip count
             const int32_t t = t0 + k;
-            uint64_t mm;
-            if (all_plain) {
-                const uint64_t x = G ^ code2;
-                mm = (x | (x >> 1)) & in2;
-            } else {
-                const uint64_t glo = G & kEven, ghi = (G >> 1) & kEven;
-                const uint64_t nlo = glo ^ kEven, nhi = ghi ^ kEven;
-                mm = ~((nhi & nlo & Q0) | (nhi & glo & Q1) | (ghi & nlo & Q2) | (ghi & glo & Q3)) & in2;
-            }
-            if (a.I) {
-                mm &= ~(spread32((uint32_t)(WH >> 32)) & anyq);
-                WH = (WH << 1) | (WF >> 63);
-                WF <<= 1;
-                if ((k & 63) == 63) {  // the next 64 bases
-                    const int w = min(nwe, kPE - 2);
-                    const uint64_t x0 = sj[(kPW + w) * MP_PBATCH], x1 = sj[(kPW + w + 1) * MP_PBATCH];
-                    const uint32_t b6 = (uint32_t)((sP0 & 63) + (uint64_t)t0) & 63u;
-                    WF = b6 ? (x0 << b6) | (x1 >> (64 - b6)) : x0;
-                    ++nwe;
-                }
-            }
-            const bool hit = t >= ta && t <= tb && !(mm & prot2) && __popcll(mm) <= a.N;
+            const uint32_t glo = (uint32_t)(SL >> 32), ghi = (uint32_t)(SH >> 32);
+            const uint32_t m01 = (glo & q1) | (~glo & q0), m23 = (glo & q3) | (~glo & q2);
+            uint32_t match = (ghi & m23) | (~ghi & m01);
+            if (a.I) match |= (uint32_t)(SW >> 32) & anyq;  // 'N': every base with an IUPAC meaning
+            const uint32_t mm = ~match & in32;
+            const bool hit = t >= ta && t <= tb && !(mm & prot32) && __popc(mm) <= a.N;
             stage_try_hit(a, S, lane, hit, sgk, srk, t - slo);
-            G = (G << 2) | (F >> 62);
-            F <<= 2;
+            SL <<= 1;
+            SH <<= 1;
+            SW <<= 1;
             if ((k & 31) == 31) {  // the next 32 bases
-                const int w = min(nw, kPW - 2);
-                F = fun(sj[w * MP_PBATCH], sj[(w + 1) * MP_PBATCH]);
+                uint32_t l, h, n;
+                fill(nw, l, h, n);
+                SL |= l;
+                SH |= h;
+                SW |= n;
                 ++nw;
             }
         }
