@@ -351,6 +351,7 @@ __host__ __device__ __forceinline__ uint32_t lds_block_mask(uint32_t x, uint32_t
     // x: the key left-aligned in 32 bits (x >> shw = key)
     uint32_t m = 1u << ((x >> (32 - kLdsFilterLog2)) & 31u);
     if (k >= 2) m |= 1u << ((x >> shw) & 31u);
+    if (k >= 3) m |= 1u << (((((x >> shw) & 127u) * 37u) >> 2) & 31u);  // a third function of the word's 7 free key bits
     return m;
 }
 

@@ -1260,6 +1260,7 @@ __device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds
                 const uint32_t wv = lds[x >> (37 - kLdsFilterLog2)];
                 uint32_t on = __builtin_amdgcn_ubfe(wv, (x >> (32 - kLdsFilterLog2)) & 31u, 1u);
                 if constexpr (kK >= 2) on &= __builtin_amdgcn_ubfe(wv, (x >> shw) & 31u, 1u);
+                if constexpr (kK >= 3) on &= __builtin_amdgcn_ubfe(wv, (((x >> shw) & 127u) * 37u) >> 2, 1u);
                 lmask |= on << (31 - T);
             }()),
          ...);
@@ -2411,11 +2412,15 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full && rkf)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 3 && a.defer_full && rkf)  // MP_LDS_K=3 (A/B)
+            hipLaunchKernelGGL((scan_kernel<1, false, 3, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 3 && a.defer_full && t->h16)
+            hipLaunchKernelGGL((scan_kernel<1, false, 3, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h16)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
-        else if (t->filt_direct && t->lds_k != 2 && a.defer_full && rkf)
+        else if (t->filt_direct && t->lds_k == 1 && a.defer_full && rkf)
             hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && a.defer_full && t->h16)
             hipLaunchKernelGGL((scan_kernel<1, false, 1, true, true>), dim3(grid), dim3(kBlock), 0, st, a);

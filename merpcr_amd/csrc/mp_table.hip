@@ -168,6 +168,9 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         std::vector<uint32_t> lfilt(kLdsFilterWords, 0);
         const bool blocked = !t->lds_exact && t->filt_direct;  // W 11..13: lds_block_mask
         t->lds_k = blocked && nb > kLdsK2Keys ? 2 : 1;
+        // MP_LDS_K=1..3 forces the bits per key (the level-1 A/B of DESIGN 4.2; the scan
+        // launches k = 3 only on its key-group and 16-B-head paths)
+        if (const char* e = std::getenv("MP_LDS_K"); e && blocked) t->lds_k = std::min(3, std::max(1, std::atoi(e)));
         for (uint32_t b = 0; b < nb; ++b) {
             const uint32_t idx = lds_bit(bkey[b], W, t->lds_exact);
             if (blocked) {
