@@ -374,7 +374,7 @@ def main():
         rng = shard_ranges(lens, world)[rank]
     setup_s = time.time() - t_setup
     log(f"[rank {rank}] setup {setup_s:.1f}s (pack {pack_s:.2f}s) records={len(lens)} bases={sum(lens)} "
-        f"sts={n_sts} recs={table.n_rec} planted={planted} table={table.stats()} genome={genome.stats()} "
+        f"sts={n_sts} recs={table.n_rec} planted={planted} table={table.stats()} split={table.split()} genome={genome.stats()} "
         f"range={rng}")
 
     gathered = None
@@ -524,6 +524,16 @@ def main():
     kern_s = float(np.mean(scan_ms)) / 1e3
     alg_bytes = BYTES_PER_BASE * st["windows"] + BYTES_PER_HIT * search.last_hits()  # rank 0's scan launch
     achieved = alg_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
+    # the scan stage's kernels (events around all of them): a split W 7..9 table scans its two
+    # exact seeds with scan_kernel (plus dense_kernel over the records they cannot carry)
+    sp = table.split()
+    if sp["seed_tables"]:
+        scan_label = (f"mp::scan_kernel x{sp['seed_tables']} (split seeds: exact [0, W+4)"
+                      + (" + gapped [0, W) ++ [W+4, 16)" if sp["seed_tables"] > 1 else "")
+                      + (f" + dense_kernel over {sp['rest_records']} records" if sp["rest_records"] else "")
+                      + "; one stage, HIP events around all of it)")
+    else:
+        scan_label = "mp::dense_kernel" if cfg["W"] <= 9 else "mp::scan_kernel"
     workload = (f"{args.config}: {n_sts} STS vs {bases / 1e9:.3f} Gbp ({len(lens)} records), "
                 f"W={cfg['W']} N={cfg['N']} M={cfg['M']} I={cfg['I']}")
     if world > 1 and weak:
@@ -562,7 +572,7 @@ def main():
                      "traffic": int(traffic) if traffic else None,
                      "traffic_source": f"profiles/{pmc_tag}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, "
                                        "gfx950-corrected; includes Infinity-Cache hits)" if traffic else None,
-                     "kernel": "mp::dense_kernel" if cfg["W"] <= 9 else "mp::scan_kernel",
+                     "kernel": scan_label,
                      "alg_bytes_per_launch": int(alg_bytes),
                      "issue": (dict(issue_bound(pmc), source=f"profiles/{pmc_tag}_pmc.json") if pmc else None)},
         "setup_s": round(setup_s, 2),

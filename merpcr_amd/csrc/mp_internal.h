@@ -154,7 +154,26 @@ struct Table {
     uint64_t planes_words = 0;
     uint8_t* pchars = nullptr;
     uint32_t rank_bits = 1;
+    // Split seeds (W 7..9, I = 0, N <= 1; see kSplitSpan): the dense table's search as scans of
+    // longer exact seeds.  Sub-tables hold only the scan side; their Entry::rec are this
+    // table's record indices, and the pair check, ranks and decode use this table's arrays.
+    Table* split_a = nullptr;     // seed = primer-1 bases [0, W + 4)
+    Table* split_b = nullptr;     // N = 1: the gapped seed [0, W) ++ [W + 4, kSplitSpan)
+    Table* split_rest = nullptr;  // records neither seed can carry: dense_kernel on them alone
+    uint32_t gap_at = 0, gap_len = 0;  // gapped table: key = bases [0, gap_at) ++ [gap_at + gap_len, ...)
 };
+
+// Split seeds.  Under I = 0 a window within N <= 1 mismatches of a record seeded at its
+// primer start, plain over bases [0, kSplitSpan), matches the key [0, W) exactly and has at
+// most one mismatch in [W, kSplitSpan).  Cut that stretch into A = [W, W + 4) and B =
+// [W + 4, kSplitSpan): one of them is exact (pigeonhole), so the window is found by an exact
+// seed [0, W + 4) or by the gapped seed [0, W) ++ B.  Both seeds are 11-13 bases long, and
+// scan_kernel's prefilter and key groups handle them as c3 handles W = 11: two scans of ~1%
+// seed windows each, where dense_kernel loads a filter oct for ~60% of all windows.  The
+// gapped scan keeps only windows whose A has a mismatch (or an invalid base), so no window
+// is found twice.  Every genome base in a 16-base funnel: B ends at base 16.
+constexpr uint32_t kSplitSpan = 16;
+constexpr uint32_t kSplitA = 4;  // bases of A
 
 struct Genome {
     int device = 0;
@@ -501,7 +520,11 @@ constexpr int kPairQBase = kStatBase + kStatSlots * kStatStride;
 constexpr int kSchedBase = kPairQBase + 8 * kStatStride;
 constexpr int kHitBase = kSchedBase + 8 * kStatStride;
 constexpr int kHitRegions = 8;
-constexpr size_t kCounterBytes = (size_t)(kHitBase + kHitRegions * kStatStride) * 8;
+//   kSchedSplit     two more sets of 8 chunk counters: the gapped and the rest scans of a split
+//                   run (kSplitSpan) -- every scan of a run claims from counters zeroed by the
+//                   previous run's finish
+constexpr int kSchedSplit = kHitBase + kHitRegions * kStatStride;
+constexpr size_t kCounterBytes = (size_t)(kSchedSplit + 2 * 8 * kStatStride) * 8;
 constexpr int kHitMaxRegion = 8;                  // host word 8: the largest region count of the run
 constexpr int kHostWords = 16;                    // device-mapped host words per search
 

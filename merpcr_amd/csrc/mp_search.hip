@@ -99,7 +99,20 @@ struct ScanArgs {
     uint32_t sort_nb, sort_shift, sort_try_bits, sort_low_bits;
     uint64_t* sort_slots;   // order mode 0: keys straight into their bucket slot (null: mode 1)
     uint32_t slot_cap;
+    // gapped seed (split tables, kSplitSpan): key = bases [0, gap_at) ++ the W - gap_at bases
+    // after the gap_len-base gap; gap_len 0: contiguous
+    uint32_t gap_at, gap_len;
+    uint32_t tail_ctr;      // counters[] slot of this scan's bucket-tail list (4; 5 for the gapped scan)
+    uint32_t sched_base;    // counters[] index of this scan's 8 chunk counters (kSchedBase, kSchedSplit...)
 };
+
+// The gapped key of a 16-base funnel x (base 0 on top), left-aligned like a contiguous key:
+// the top gap_at bases, then the bases after the gap (the low bits below the key are junk,
+// as in the contiguous form).  One shift and one bit-field insert.
+__device__ __forceinline__ uint32_t gap_key(uint32_t x, uint32_t gap_at, uint32_t gap_len) {
+    const uint32_t hm = ~(0xFFFFFFFFu >> (2u * gap_at));
+    return (x & hm) | ((x << (2u * gap_len)) & ~hm);
+}
 
 // Bucket counts of the fused device sort, zeroed by every block of a scan kernel.
 __device__ __forceinline__ void zero_sort_counts(const ScanArgs& a) {
@@ -963,7 +976,7 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
         // (window, exception bits, bases left in the sequence), so that tail_kernel tests
         // records seeded at their primer start without touching the genome again
         const uint64_t gp = sbase + pos;
-        append_chunked<2>(&a.counters[4], a.tails, a.tails_cap, tail,
+        append_chunked<2>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, tail,
                           make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), e0.xstart, R.seq), lane, TC,
                           make_uint4((uint32_t)Gp, (uint32_t)(Gp >> 32), exp_, n - pos));
     }
@@ -1085,7 +1098,7 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
         defer = any;
     }
     const uint64_t gp = sbase + p;
-    append_chunked<2>(&a.counters[4], a.tails, a.tails_cap, defer,
+    append_chunked<2>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, defer,
                       make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), c.x, R.seq), lane, TC,
                       make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
 }
@@ -1249,14 +1262,15 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
 
 // Level 1 only, kMode 1: the blocked LDS filter bits of the lane's 32 windows (bit 31-T):
 // all kK bits of lds_block_mask set in the key's word.
-template <int kK>
+template <int kK, bool kGap = false>
 __device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds, uint32_t d0, uint32_t d1, uint32_t d2,
-                                                uint32_t shw) {
+                                                uint32_t shw, uint32_t gap_at = 0u, uint32_t gap_len = 0u) {
     uint32_t lmask = 0;
     [&]<int... T>(std::integer_sequence<int, T...>) {
         ((
             [&] {
-                const uint32_t x = kmer_top<T>(d0, d1, d2);
+                uint32_t x = kmer_top<T>(d0, d1, d2);
+                if constexpr (kGap) x = gap_key(x, gap_at, gap_len);
                 const uint32_t wv = lds[x >> (37 - kLdsFilterLog2)];
                 uint32_t on = __builtin_amdgcn_ubfe(wv, (x >> (32 - kLdsFilterLog2)) & 31u, 1u);
                 if constexpr (kK >= 2) on &= __builtin_amdgcn_ubfe(wv, (x >> shw) & 31u, 1u);
@@ -1305,9 +1319,22 @@ __device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, 
 // first W + F is one of A/C/G/T/U (under I = 1 a genome IUPAC base may match anything, and
 // it reads as 'A' in the 2-bit plane); bit 31 of pk marks a window where that fails, which
 // then passes on presence alone.
+// Gapped seed (kGap, split tables): the field holds the record's gap bases; a window passes
+// when they differ in 1..N positions, or when it has an invalid base in its gap (bit 31 of
+// pk) -- with none of either, the contiguous seed of the split finds the window.
+template <bool kGap = false>
 __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
     const uint32_t bit = pk & 15u;
     if (!((rw.x >> bit) & 1u)) return false;
+    if constexpr (kGap) {
+        const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
+        if (j >= kKgrpFields) return true;
+        const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
+        if (!(field & kKgrpFlag)) return true;
+        const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
+        const uint32_t mm = (uint32_t)__popc((x | (x >> 1)) & 0x55555555u);
+        return mm <= (uint32_t)a.N && (mm != 0u || (pk >> 31) != 0u);
+    }
     if (a.kgrp_wild) {
         if (pk >> 31) return true;
         const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
@@ -1366,8 +1393,8 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
     uint32_t young;            // the SIMD's two youngest waves (w >= kW / 2) claim half
     uint32_t hint;             // start of this wave's last chunk (the guided size's estimate)
     unsigned int* ctr;
-    __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint64_t n_supers, int w, int kW, int lane,
-                                              uint32_t short_chunk) {
+    __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint32_t sched_base, uint64_t n_supers, int w,
+                                              int kW, int lane, uint32_t short_chunk) {
         // short scans (under 64 super-steps per wave, e.g. c2) keep the static order: their
         // per-wave totals average out and the claims would only add latency
         const uint32_t waves = gridDim.x * (uint32_t)kW;
@@ -1379,7 +1406,7 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         chunk = n_supers < (uint64_t)waves * kSChunkShort ? short_chunk : kSChunk;
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
-        ctr = reinterpret_cast<unsigned int*>(counters + kSchedBase + x * kStatStride);
+        ctr = reinterpret_cast<unsigned int*>(counters + sched_base + x * kStatStride);
         lo = (uint32_t)(n_supers * x / g);
         hi = (uint32_t)(n_supers * (x + 1) / g);
         nw = ((gridDim.x - x + g - 1u) / g) * (uint32_t)kW;
@@ -1418,8 +1445,10 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
     }
 };
 
-template <int kMode, bool kInline, int kK = 1, bool kDefer = false, bool kH16 = false, bool kRkf = false>
+template <int kMode, bool kInline, int kK = 1, bool kDefer = false, bool kH16 = false, bool kRkf = false,
+          bool kGap = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
+    static_assert(!kGap || (kMode == 1 && kRkf), "gapped seeds take the key-group path");
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
 
@@ -1449,7 +1478,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     SurvChunk TC{0, 64u, 0u};
 
     SuperSched sch;
-    uint64_t ss = sch.first(a.counters, n_supers, w, kWaves, lane, a.sched_short);
+    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kWaves, lane, a.sched_short);
     // span of the super-step being prefetched, cached in registers (wave-uniform): the
     // common path of the prefetch issues only the four plane loads, no waits
     SeqSpan pf{};
@@ -1496,7 +1525,10 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         R.owned = (a.g_lo == 0 || sbase + R.base >= a.g_lo + 65536u) && sbase + R.base + kSuper <= a.g_hi;
         const uint32_t pb = R.base + (uint32_t)lane * kLanePos;
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
-        const uint32_t okm = window_ok_mask(R.iv, W) &
+        // a gapped seed's windows: both of its pieces clean
+        const uint32_t okm = (kGap ? window_ok_mask(R.iv, a.gap_at) &
+                                         window_ok_mask(R.iv << (a.gap_at + a.gap_len), W - a.gap_at)
+                                   : window_ok_mask(R.iv, W)) &
                              bit_range((int)sp.p_lo - (int)pb, (int)smin64((int64_t)sp.p_hi - pb, 32));
         const uint64_t nx = sch.next(ss, n_supers, lane);
         (void)stride;
@@ -1505,9 +1537,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // {key, offset} (the queue's arrays), then every lane probes one list entry per
             // pass -- full lanes, all passes' rank-word loads in flight together -- and the
             // seeds are compacted back into the same arrays as {offset, rank}
-            const uint32_t rem = lds_probe32<kK>(s_lf, d0, d1, d2, shw) & okm;
-            // I = 1 key groups: windows whose first W + F bases are not all A/C/G/T/U
-            const uint32_t fbad = (kRkf && a.kgrp_wild) ? ~window_ok_mask(R.iv, W + a.kgrp_F) : 0u;
+            const uint32_t rem = lds_probe32<kK, kGap>(s_lf, d0, d1, d2, shw, a.gap_at, a.gap_len) & okm;
+            // I = 1 key groups: windows whose first W + F bases are not all A/C/G/T/U; gapped
+            // seeds: windows with an invalid base in the gap
+            const uint32_t fbad = kGap ? ~window_ok_mask(R.iv << a.gap_at, a.gap_len)
+                                       : ((kRkf && a.kgrp_wild) ? ~window_ok_mask(R.iv, W + a.kgrp_F) : 0u);
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
@@ -1554,9 +1588,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                             const uint32_t B = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d1);
                             const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d2);
                             const uint32_t i = po[q] & 31u;
-                            const uint32_t key = funnel3(A, B, C, i) >> shw;
-                            pk[q] = ((funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F)) << 4) | (key & 15u) |
-                                    ((qe >> 15) << 31);
+                            const uint32_t key = (kGap ? gap_key(funnel3(A, B, C, i), a.gap_at, a.gap_len)
+                                                       : funnel3(A, B, C, i)) >> shw;
+                            // the field's bases: after the key, or a gapped seed's gap
+                            pk[q] = ((funnel3(A, B, C, i + (kGap ? a.gap_at : W)) >> (32u - 2u * a.kgrp_F)) << 4) |
+                                    (key & 15u) | ((qe >> 15) << 31);
                             rw[q] = a.kgrp[v ? (key >> 4) : 0u];
                         } else {
                             pk[q] = v ? L.rq.r[e] : 0u;
@@ -1582,7 +1618,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     for (int q = 0; q < kP; ++q) {
                         if ((uint32_t)q * 64u < nr) {
                             const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
-                            const bool hit = e < nr && kgrp_pass(a, rw[q], pk[q]);
+                            const bool hit = e < nr && kgrp_pass<kGap>(a, rw[q], pk[q]);
                             const uint64_t hm = __ballot(hit);
                             if (hit) L.rq.q[qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint16_t)po[q];
                             qn += (uint32_t)__popcll(hm);
@@ -1597,7 +1633,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         uint32_t x;
                         window_from_regs(a, R, sbase, p, true, G, x);
                         const uint64_t gp = sbase + p;
-                        append_chunked<2>(&a.counters[4], a.tails, a.tails_cap, on,
+                        append_chunked<2>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
                                           make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), kKeyRef, R.seq), lane, TC,
                                           make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
                     }
@@ -1802,7 +1838,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     SurvChunk C{0, 64u, 0u};
 
     SuperSched sch;
-    uint64_t ss = sch.first(a.counters, n_supers, w, kDenseWaves, lane, a.sched_short);
+    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kDenseWaves, lane, a.sched_short);
     SeqSpan pf{};
     pf.super0 = 1;
     uint64_t pf_end = 0, pf_sbase = 0;
@@ -1981,6 +2017,9 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
     __syncthreads();
 }
 
+// kGap: the references of a gapped seed scan (split tables): the key is the gapped one, and a
+// window whose gap matches the record exactly is left to the contiguous seed's scan.
+template <bool kGap = false>
 __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     __shared__ uint4 s_buf[kTailBuf];
     __shared__ uint32_t s_n;
@@ -1988,7 +2027,7 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const uint64_t n_refs = umin64(a.counters[4], a.tails_cap);
+    const uint64_t n_refs = umin64(a.counters[a.tail_ctr], a.tails_cap);
     const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
     uint32_t ncand = 0, nsurv = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
@@ -2007,7 +2046,8 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
             Entry e;
             if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
                 const uint32_t W = (uint32_t)a.W;
-                const uint32_t h = (uint32_t)(Gs >> (64u - 2u * W));
+                const uint32_t h = kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
+                                        : (uint32_t)(Gs >> (64u - 2u * W));
                 const uint2 rw = a.rk[h >> 5];
                 const uint2 c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
                 if (c.y & kHead8Full) {
@@ -2045,6 +2085,13 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                     if (gp - sbase < e.hash_off) continue;  // k < 0
                     G = ext2(a.g2, gk);
                     ex = (uint32_t)(ext1(exc, gk) >> 32);
+                }
+                if constexpr (kGap) {  // a window whose gap matches exactly is the contiguous seed's
+                    const uint64_t gm = sp_lt((int)(a.gap_at + a.gap_len)) & ~sp_lt((int)a.gap_at);
+                    const uint64_t xg = G ^ e.code;
+                    const uint32_t inv = a.has_u ? (uint32_t)(ext1(a.ginv, gk) >> 32) : ex;  // A/C/G/T/U are valid
+                    const uint32_t im = (0xFFFFFFFFu >> a.gap_at) & ~(0xFFFFFFFFu >> (a.gap_at + a.gap_len));
+                    if (((xg | (xg >> 1)) & gm) == 0 && (inv & im) == 0) continue;
                 }
                 ++ncand;
                 bool exact = false;
@@ -2243,6 +2290,15 @@ static int alloc_tails(Search* s, uint64_t cap) {
     return MP_OK;
 }
 
+// dense_kernel's dynamic LDS for table t: the per-32-key index and escape words, plus the
+// per-key summary when the table has one.
+static size_t dense_lds_of(const Table* t) {
+    size_t b = (sizeof(uint2) + sizeof(uint32_t)) *
+               std::max<size_t>(1, ((size_t)1 << (2 * std::min<int>(t->prm.wordsize, kDenseMaxW))) / 32);
+    if (t->dsum_mode) b += sizeof(uint16_t) * ((size_t)1 << (2 * t->prm.wordsize));
+    return b;
+}
+
 constexpr uint64_t kDefaultHitCap = 1 << 16, kDefaultSurvCap = 1 << 20, kDefaultTailCap = 1 << 18;
 
 }  // namespace mp
@@ -2292,9 +2348,8 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
         int occ = 0;  // persistent pair check: every resident block slot once
         s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel, kPairBlock, 0) == hipSuccess && occ > 0)
                              ? (uint32_t)occ : 1u;
-        s->dense_lds = (sizeof(uint2) + sizeof(uint32_t)) *
-                       std::max<size_t>(1, ((size_t)1 << (2 * std::min<int>(t->prm.wordsize, kDenseMaxW))) / 32);
-        if (t->dsum_mode) s->dense_lds += sizeof(uint16_t) * ((size_t)1 << (2 * t->prm.wordsize));
+        s->dense_lds = dense_lds_of(t);
+        if (t->split_rest) s->dense_lds = std::max(s->dense_lds, dense_lds_of(t->split_rest));
         if (s->dense_lds > 64 * 1024)
             for (const void* k : {(const void*)dense_kernel<0, 0>, (const void*)dense_kernel<0, 1>,
                                   (const void*)dense_kernel<1, 0>, (const void*)dense_kernel<1, 2>,
@@ -2373,13 +2428,35 @@ static int set_lists(Search* s, ScanArgs& a, int mode) {
 // survivors (+ bucket-tail references -> tail survivors) -> pair check -> hit keys and bucket
 // counts -> hit order (modes 0 and 1: bucket offsets, then the sort) ->
 // finish_kernel (counters into the mapped host words, then zeroed) -> the completion event.
-static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStream_t st, int mode) {
-    Table* t = s->table;
-    if (s->dirty) {  // an abandoned run may have left counts behind
-        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
-        s->dirty = false;
-    }
+// The scan-side fields of table t (its seeds, filters and heads); the record side (recs,
+// ranks, primer planes) stays the searched table's.
+static void scan_fields(ScanArgs& a, const Table* t, const Search* s) {
+    a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
+    a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
+    a.defer_full = t->defer_full && (!s->opt.no_defer || t->gap_len);
+    a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F; a.kgrp_wild = t->kgrp_wild;
+    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.lfilt = t->lfilt;
+    a.slots = t->slots; a.slot_log2 = t->slot_log2;
+    a.ents = t->ents;
+    a.W = t->prm.wordsize;
+    a.gap_at = t->gap_at;
+    a.gap_len = t->gap_len;
+}
+
+// The scan kernel of table t (dense_kernel, or scan_kernel in the form the table and the
+// handle's options select).  *tail: the run needs tail_kernel over this scan's references.
+static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t tiles, hipStream_t st, bool* tail) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU);
+    *tail = false;
+    if (t->gap_len) {  // gapped seed: the key-group path, every passing seed deferred to tail_kernel
+        if (!(t->filt_direct && !t->lds_exact && t->kgrp_F >= 2 && a.W >= 11 && a.W <= 13 && a.defer_full))
+            return fail(MP_E_STATE, "gapped seed table without key groups");
+        if (t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        MP_HIP_CHECK(hipGetLastError());
+        *tail = true;
+        return MP_OK;
+    }
     bool inl = t->n_rec > t->n_keys + t->n_keys / 4;  // bucket tails inline vs tail_kernel
     if (s->opt.tails == MP_TAILS_INLINE) inl = true;
     if (s->opt.tails == MP_TAILS_KERNEL) inl = false;
@@ -2390,12 +2467,10 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     // (I = 1: the field form with the non-plain bases marked, kgrp_wild)
     const bool rkf = t->kgrp_F >= 2 && (a.I == 0 ? !t->h16 && !t->kgrp_wild : t->kgrp_wild != 0) &&
                      !s->opt.no_rank_filter && t->filt_direct && !t->lds_exact && a.W >= 11 && a.W <= 13;
-    const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
-    if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
     if (dense) {
         const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
                                                             (uint64_t)s->n_cu * (uint64_t)s->dense_per_cu);
-        const size_t lds = s->dense_lds;
+        const size_t lds = dense_lds_of(t);
         // the summary exists only for N <= 1 (mp_table.hip): N = 0 form 1, N = 1 form 2
         if (a.N == 0 && a.dsum_mode == 1) hipLaunchKernelGGL((dense_kernel<0, 1>), dim3(dgrid), dim3(kDenseBlock), lds, st, a);
         else if (a.N == 0) hipLaunchKernelGGL((dense_kernel<0, 0>), dim3(dgrid), dim3(kDenseBlock), lds, st, a);
@@ -2431,10 +2506,63 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         else hipLaunchKernelGGL((scan_kernel<2, false>), dim3(grid), dim3(kBlock), 0, st, a);
     }
     MP_HIP_CHECK(hipGetLastError());
-    if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
-    if (!dense && !inl && (t->max_bucket > 1 || a.defer_full)) {  // defer_full: single-record full heads too
-        hipLaunchKernelGGL(tail_kernel, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, a);
-        MP_HIP_CHECK(hipGetLastError());
+    *tail = !dense && !inl && (t->max_bucket > 1 || a.defer_full);  // defer_full: single-record full heads too
+    return MP_OK;
+}
+
+// Split seeds in use for this handle (kSplitSpan): the table has them and the options leave
+// the dense path alone (no_dense or no_split keep the unsplit table's scan).
+static bool use_split(const Search* s) {
+    return s->table->split_a && !s->opt.no_dense && !s->opt.no_split;
+}
+
+// Every kernel of one run, back to back on the stream with no host wait: scan -> fingerprint
+// survivors (+ bucket-tail references -> tail survivors) -> pair check -> hit keys and bucket
+// counts -> hit order (modes 0 and 1: bucket offsets, then the sort) ->
+// finish_kernel (counters into the mapped host words, then zeroed) -> the completion event.
+// A split table scans its seeds one after another (the contiguous seed, the gapped seed, the
+// rest's dense scan), each appending to the one survivor list; the two seed scans keep their
+// bucket-tail references in the two halves of the tail list (counters 4 and 5).
+static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStream_t st, int mode) {
+    Table* t = s->table;
+    if (s->dirty) {  // an abandoned run may have left counts behind
+        MP_HIP_CHECK(hipMemsetAsync(s->counters, 0, kCounterBytes, st));
+        s->dirty = false;
+    }
+    const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
+    if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
+    if (!use_split(s)) {
+        bool tail = false;
+        const int rc = launch_scan(s, t, a, tiles, st, &tail);
+        if (rc) return rc;
+        if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
+        if (tail) {
+            hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, a);
+            MP_HIP_CHECK(hipGetLastError());
+        }
+    } else {
+        const Table* sub[3] = {t->split_a, t->split_b, t->split_rest};
+        ScanArgs pa[3];
+        bool tail[3] = {false, false, false};
+        const uint64_t half = s->tails_cap / 2;
+        for (int i = 0; i < 3; ++i) {
+            if (!sub[i]) continue;
+            pa[i] = a;
+            scan_fields(pa[i], sub[i], s);
+            pa[i].tails = s->tails + (i == 1 ? 2 * half : 0);
+            pa[i].tails_cap = half;
+            pa[i].tail_ctr = i == 1 ? 5u : 4u;
+            pa[i].sched_base = i == 0 ? (uint32_t)kSchedBase : (uint32_t)(kSchedSplit + (i - 1) * 8 * kStatStride);
+            const int rc = launch_scan(s, sub[i], pa[i], tiles, st, &tail[i]);
+            if (rc) return rc;
+        }
+        if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
+        for (int i = 0; i < 3; ++i) {
+            if (!sub[i] || !tail[i]) continue;
+            if (sub[i]->gap_len) hipLaunchKernelGGL(tail_kernel<true>, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, pa[i]);
+            else hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, pa[i]);
+            MP_HIP_CHECK(hipGetLastError());
+        }
     }
     MID_EVENT(hipEventRecord(s->ev1, st));
     const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
@@ -2510,11 +2638,13 @@ static int search_complete(Search* s, uint64_t* n_hits) {
     // A list that overflowed is grown and the whole run enqueued again (rare: the first runs of
     // a handle); kernels never write past a capacity.
     // (the hit list overflows when one of its regions does: cnt[kHitMaxRegion] > cap / kHitRegions)
+    // (a split run's two seed scans each hold half the tail list: counters 4 and 5)
+    auto tails_need = [&]() { return use_split(s) ? 2 * std::max(cnt[4], cnt[5]) : cnt[4]; };
     for (int attempt = 0;
-         cnt[2] > s->surv_cap || cnt[4] > s->tails_cap || cnt[kHitMaxRegion] > s->cap / kHitRegions; ++attempt) {
+         cnt[2] > s->surv_cap || tails_need() > s->tails_cap || cnt[kHitMaxRegion] > s->cap / kHitRegions; ++attempt) {
         if (attempt == 3) return fail(MP_E_STATE, "mp_search_run: list overflow after growth");
         ++s->n_regrowths;
-        if (cnt[4] > s->tails_cap) rc = alloc_tails(s, cnt[4] + cnt[4] / 4 + 1024);
+        if (tails_need() > s->tails_cap) rc = alloc_tails(s, tails_need() + tails_need() / 4 + 1024);
         if (!rc && cnt[2] > s->surv_cap) rc = alloc_surv(s, cnt[2] + cnt[2] / 2 + 1024);
         if (!rc && cnt[kHitMaxRegion] > s->cap / kHitRegions) {
             const uint64_t mx = cnt[kHitMaxRegion];
@@ -2645,15 +2775,12 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         a.has_u = g->has_u ? 1 : 0;
         a.seq_base = g->d_base; a.seq_len = g->d_len;
         a.spans = s->spans; a.n_spans = n_real_spans;
-        a.binfo = t->binfo; a.dfilt = t->dfilt; a.dgrp = t->dgrp; a.dgesc = t->dgesc; a.dents_pad = t->dents_pad; a.dense_M = t->dense_M;
-        a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
-        a.defer_full = t->defer_full && !s->opt.no_defer;
-        a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F; a.kgrp_wild = t->kgrp_wild;
-        a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.lfilt = t->lfilt;
-        a.slots = t->slots; a.slot_log2 = t->slot_log2;
-        a.ents = t->ents; a.recs = t->recs; a.rank = t->rank;
+        scan_fields(a, t, s);
+        a.tail_ctr = 4;
+        a.sched_base = kSchedBase;
+        a.recs = t->recs; a.rank = t->rank;
         a.planes = t->planes; a.pchars = t->pchars;
-        a.W = t->prm.wordsize; a.M = t->prm.margin; a.N = t->prm.mismatches;
+        a.M = t->prm.margin; a.N = t->prm.mismatches;
         a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
         a.g_lo = g_lo; a.g_hi = g_hi;
         a.sched_short = s->sched_short;

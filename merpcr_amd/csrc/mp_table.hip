@@ -50,6 +50,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 
 static void free_table(Table* t) {
     if (!t) return;
+    free_table(t->split_a); free_table(t->split_b); free_table(t->split_rest);
     hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->kgrp); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
@@ -97,28 +98,22 @@ MP_EXPORT int mp_device_count(int32_t* n) {
     return MP_OK;
 }
 
-MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_rec,
-                              const uint32_t* key, const uint32_t* hash_off,
-                              const uint64_t* pcr_size, const uint8_t* primer1,
-                              const uint64_t* p1_off, const uint8_t* primer2,
-                              const uint64_t* p2_off, void** table_out) {
-    if (!prm || !table_out) return fail(MP_E_ARG, "mp_table_create: null pointer");
-    *table_out = nullptr;
-    const mp_params& p = *prm;
-    if (p.wordsize < 3 || p.wordsize > 16) return fail(MP_E_ARG, "Word size must be between 3 and 16");
-    if (p.mismatches < 0 || p.mismatches > 10)
-        return fail(MP_E_ARG, "Number of mismatches must be between 0 and 10");
-    if (p.margin < 0 || p.margin > 10000) return fail(MP_E_ARG, "Margin must be between 0 and 10000");
-    if (p.three_prime_match < 0) return fail(MP_E_ARG, "Three prime match must be at least 0");
-    if (p.iupac_mode != 0 && p.iupac_mode != 1) return fail(MP_E_ARG, "iupac_mode must be 0 or 1");
-    if (n_rec >= 0x80000000u) return fail(MP_E_ARG, "too many records (max 2^31 - 1)");
-    if (n_rec && (!key || !hash_off || !pcr_size || !primer1 || !p1_off || !primer2 || !p2_off))
-        return fail(MP_E_ARG, "mp_table_create: null record array");
-
+// Builds one table.  rec_map (sub-tables of a split, see kSplitSpan): record r of these
+// arrays is record rec_map[r] of the parent, which Entry::rec names.  gap_len > 0: the keys
+// are gapped seeds (bases [0, gap_at) ++ [gap_at + gap_len, gap_at + gap_len + W - gap_at)):
+// no compact heads (they restate a primer from a contiguous key), and the key groups hold
+// the gap's bases for the gapped scan's one-mismatch test (kgrp_pass).
+static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const uint32_t* key,
+                       const uint32_t* hash_off, const uint64_t* pcr_size, const uint8_t* primer1,
+                       const uint64_t* p1_off, const uint8_t* primer2, const uint64_t* p2_off,
+                       const uint32_t* rec_map, uint32_t gap_at, uint32_t gap_len, Table** table_out) {
     Table* t = new Table();
     t->prm = p;
     t->device = device;
     t->n_rec = n_rec;
+    t->gap_at = gap_at;
+    t->gap_len = gap_len;
+    const bool gapped = gap_len != 0;
     int rc = MP_OK;
     do {
         if (hipSetDevice(device) != hipSuccess) { rc = fail(MP_E_HIP, "hipSetDevice failed"); break; }
@@ -224,7 +219,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             const uint32_t r = blist[i];
             Entry& e = ents[i];
             std::memset(&e, 0, sizeof(e));
-            e.rec = r;
+            e.rec = rec_map ? rec_map[r] : r;
             e.hash_off = (uint16_t)recs[r].hash_off;
             e.l1 = (uint16_t)recs[r].l1;
             const uint64_t* pl = &planes[(size_t)recs[r].p1_pl * 4];
@@ -252,7 +247,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         auto entry8 = [&](const Entry& e) {
             const uint64_t plain_all = e.l1 >= 32 ? 0x5555555555555555ull
                                                   : (e.l1 ? (0x5555555555555555ull & (~0ull << (64 - 2 * e.l1))) : 0ull);
-            const bool fast = e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 16 && e.pmask == plain_all &&
+            const bool fast = !gapped && e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 16 && e.pmask == plain_all &&
                               e.rec < (1u << kHead8RecBits);
             uint2 c;
             c.x = fast ? (uint32_t)((e.code << (2 * W)) >> 32) : 0u;  // bases W..W+15
@@ -262,7 +257,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
         // kHead8Filt bits of a full head (0 when some record does not qualify)
         auto head8_filter = [&](uint32_t b) -> uint32_t {
             const uint32_t cnt = bcount[b];
-            if (cnt < 1 || cnt > 3) return 0u;
+            if (gapped || cnt < 1 || cnt > 3) return 0u;
             const uint32_t F = head8_filt_bases(cnt);
             const uint64_t fmask = 0x5555555555555555ull & ~(~0ull >> (2 * F));  // bases 0..F-1, spaced
             uint32_t bits = kHead8Filt | ((cnt - 1u) << 28);
@@ -408,7 +403,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             // base under I=1 is neither); {0, 0, 0, kHead8Full} when the record does not fit
             auto entry16 = [&](const Entry& e) {
                 const uint64_t seed = sp_lt((int)W);
-                const bool fits = e.count == 1 && e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 16 &&
+                const bool fits = !gapped && e.count == 1 && e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 16 &&
                                   e.rec < (1u << kHead8RecBits) && (e.pmask & seed) == seed &&
                                   ((e.pmask >> 1) & seed) == 0;
                 if (!fits) return make_uint4(0u, 0u, 0u, kHead8Full);
@@ -454,11 +449,38 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
             }
             // few full heads (multi-record buckets, IUPAC/long/inner-seed primers): the ranked
             // drain tests only compact heads and defers every full-head bucket to tail_kernel
-            t->defer_full = n_full * 20 < (uint64_t)nb;
+            // (a gapped table's heads are all full: its scan sends every seed that passes the key
+            // groups to tail_kernel, the deferring form, whatever the share)
+            t->defer_full = gapped || n_full * 20 < (uint64_t)nb;
             // key groups (kKgrpKeys keys per u64) for the scan's level-2 probe: it shuffles
             // bases [i, i + 17) of window i from the owning lane (i < 32 of its 48), so
             // F <= 17 - W, and a field holds <= 7 bases
-            if (W >= 11 && W <= 13 && p.iupac_mode) {
+            if (gapped && W >= 11 && W <= 13) {
+                // gapped seed: a field per single-record key holding the record's gap bases
+                // [gap_at, gap_at + gap_len); the gapped scan keeps a window only when they
+                // differ from the window's in 1..N positions, or its gap holds an invalid base
+                // (no mismatch there: the contiguous seed finds the window)
+                const uint32_t F = gap_len;
+                t->kgrp_F = F;
+                const uint64_t nkeys = 1ull << (2 * W);
+                kgrp.assign(nkeys / kKgrpKeys, 0ull);
+                const uint64_t gm = sp_lt((int)(gap_at + F)) & ~sp_lt((int)gap_at);  // the gap's plain bits
+                for (uint64_t g = 0; g < kgrp.size(); ++g) {
+                    const uint32_t pres = (uint32_t)((filt[g >> 1] >> ((g & 1) * 16)) & 0xFFFFu);
+                    uint64_t w = pres;
+                    uint32_t j = 0;
+                    for (uint32_t bit = 0; bit < 16 && j < kKgrpFields; ++bit) {
+                        if (!((pres >> bit) & 1u)) continue;
+                        const uint32_t k = (uint32_t)(g * kKgrpKeys + bit);
+                        const uint32_t b = rank_bucket[rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u))];
+                        const Entry& e = ents[boff[b]];
+                        if (bcount[b] == 1 && e.hash_off == 0 && (e.pmask & gm) == gm && ((e.pmask >> 1) & gm) == 0)
+                            w |= (uint64_t)(kKgrpFlag | (uint32_t)((e.code << (2 * gap_at)) >> (64 - 2 * F))) << (16u + 16u * j);
+                        ++j;
+                    }
+                    kgrp[g] = w;
+                }
+            } else if (W >= 11 && W <= 13 && p.iupac_mode) {
                 // I = 1 (c4: degenerate primers): two 24-bit fields per group, one per present
                 // key, each the 2-bit codes of primer-1 bases W..W+F-1 (12 bits) and, at the
                 // even bit positions of the next 12, the bases that are not plain (an IUPAC
@@ -595,12 +617,129 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
     return MP_OK;
 }
 
+// Split seeds (kSplitSpan): the sub-tables of a W 7..9, I = 0, N <= 1 table.  A record takes
+// the seeds when it is seeded at its primer start and its primer 1 is plain over the bases
+// the seeds and the pigeonhole cut need (N = 1: [0, kSplitSpan); N = 0: [0, W + 4)); the rest
+// stay in a dense table of their own.  Not split when under half the records qualify.
+static int build_split(Table* t, uint32_t n_rec, const uint32_t* key, const uint32_t* hash_off,
+                       const uint64_t* pcr_size, const uint8_t* primer1, const uint64_t* p1_off,
+                       const uint8_t* primer2, const uint64_t* p2_off) {
+    const mp_params& p = t->prm;
+    const uint32_t W = (uint32_t)p.wordsize;
+    if (W < 7 || W > 9 || p.iupac_mode != 0 || p.mismatches > 1 || n_rec == 0) return MP_OK;
+    if (const char* e = std::getenv("MP_NO_SPLIT"); e && std::atoi(e)) return MP_OK;
+    const uint32_t need = p.mismatches ? kSplitSpan : W + kSplitA;
+    auto code = [](uint8_t c) -> int {
+        switch (upcase(c)) { case 'A': return 0; case 'C': return 1; case 'G': return 2; case 'T': return 3; default: return -1; }
+    };
+    std::vector<uint32_t> yes, rest;
+    for (uint32_t r = 0; r < n_rec; ++r) {
+        bool ok = hash_off[r] == 0 && p1_off[r + 1] - p1_off[r] >= need;
+        for (uint32_t i = 0; ok && i < need; ++i) ok = code(primer1[p1_off[r] + i]) >= 0;
+        (ok ? yes : rest).push_back(r);
+    }
+    if (yes.size() * 2 < n_rec) return MP_OK;
+    // one sub-table's record arrays: the chosen records, in parent order
+    struct Sub {
+        std::vector<uint32_t> key, hoff, map;
+        std::vector<uint64_t> size, o1, o2;
+        std::vector<uint8_t> b1, b2;
+    };
+    auto subset = [&](const std::vector<uint32_t>& recs, int form) {
+        Sub s;
+        s.o1.push_back(0);
+        s.o2.push_back(0);
+        for (uint32_t r : recs) {
+            const uint8_t* q = primer1 + p1_off[r];
+            uint32_t k = 0;
+            if (form == 0) {  // A: [0, W + 4)
+                for (uint32_t i = 0; i < W + kSplitA; ++i) k = (k << 2) | (uint32_t)code(q[i]);
+            } else if (form == 1) {  // B: [0, W) ++ [W + 4, kSplitSpan)
+                for (uint32_t i = 0; i < W; ++i) k = (k << 2) | (uint32_t)code(q[i]);
+                for (uint32_t i = W + kSplitA; i < kSplitSpan; ++i) k = (k << 2) | (uint32_t)code(q[i]);
+            } else {
+                k = key[r];
+            }
+            s.key.push_back(k);
+            s.hoff.push_back(form == 2 ? hash_off[r] : 0u);
+            s.map.push_back(r);
+            s.size.push_back(pcr_size[r]);
+            s.b1.insert(s.b1.end(), primer1 + p1_off[r], primer1 + p1_off[r + 1]);
+            s.b2.insert(s.b2.end(), primer2 + p2_off[r], primer2 + p2_off[r + 1]);
+            s.o1.push_back(s.b1.size());
+            s.o2.push_back(s.b2.size());
+        }
+        return s;
+    };
+    auto make = [&](const Sub& s, uint32_t w, uint32_t gap_at, uint32_t gap_len, Table** out) {
+        mp_params q = p;
+        q.wordsize = (int32_t)w;
+        return build_table(q, t->device, (uint32_t)s.key.size(), s.key.data(), s.hoff.data(), s.size.data(),
+                           s.b1.data(), s.o1.data(), s.b2.data(), s.o2.data(), s.map.data(), gap_at, gap_len, out);
+    };
+    int rc = MP_OK;
+    {
+        const Sub a = subset(yes, 0);
+        rc = make(a, W + kSplitA, 0, 0, &t->split_a);
+    }
+    if (!rc && p.mismatches) {
+        const Sub b = subset(yes, 1);
+        rc = make(b, W + (kSplitSpan - W - kSplitA), W, kSplitA, &t->split_b);
+    }
+    if (!rc && !rest.empty()) {
+        const Sub r = subset(rest, 2);
+        rc = make(r, W, 0, 0, &t->split_rest);
+    }
+    if (rc) {
+        free_table(t->split_a); free_table(t->split_b); free_table(t->split_rest);
+        t->split_a = t->split_b = t->split_rest = nullptr;
+    }
+    return rc;
+}
+
+MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_rec,
+                              const uint32_t* key, const uint32_t* hash_off,
+                              const uint64_t* pcr_size, const uint8_t* primer1,
+                              const uint64_t* p1_off, const uint8_t* primer2,
+                              const uint64_t* p2_off, void** table_out) {
+    if (!prm || !table_out) return fail(MP_E_ARG, "mp_table_create: null pointer");
+    *table_out = nullptr;
+    const mp_params& p = *prm;
+    if (p.wordsize < 3 || p.wordsize > 16) return fail(MP_E_ARG, "Word size must be between 3 and 16");
+    if (p.mismatches < 0 || p.mismatches > 10)
+        return fail(MP_E_ARG, "Number of mismatches must be between 0 and 10");
+    if (p.margin < 0 || p.margin > 10000) return fail(MP_E_ARG, "Margin must be between 0 and 10000");
+    if (p.three_prime_match < 0) return fail(MP_E_ARG, "Three prime match must be at least 0");
+    if (p.iupac_mode != 0 && p.iupac_mode != 1) return fail(MP_E_ARG, "iupac_mode must be 0 or 1");
+    if (n_rec >= 0x80000000u) return fail(MP_E_ARG, "too many records (max 2^31 - 1)");
+    if (n_rec && (!key || !hash_off || !pcr_size || !primer1 || !p1_off || !primer2 || !p2_off))
+        return fail(MP_E_ARG, "mp_table_create: null record array");
+    Table* t = nullptr;
+    int rc = build_table(p, device, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off, nullptr, 0, 0, &t);
+    if (rc) return rc;
+    rc = build_split(t, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off);
+    if (rc) {
+        free_table(t);
+        return rc;
+    }
+    *table_out = t;
+    return MP_OK;
+}
+
 MP_EXPORT int mp_table_stats(void* table, uint64_t* n_keys, uint64_t* max_bucket, uint64_t* dev_bytes) {
     Table* t = (Table*)table;
     if (!t) return fail(MP_E_ARG, "mp_table_stats: null table");
     if (n_keys) *n_keys = t->n_keys;
     if (max_bucket) *max_bucket = t->max_bucket;
     if (dev_bytes) *dev_bytes = t->dev_bytes;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_table_split(void* table, uint32_t* seed_tables, uint32_t* rest_records) {
+    Table* t = (Table*)table;
+    if (!t) return fail(MP_E_ARG, "mp_table_split: null table");
+    if (seed_tables) *seed_tables = (t->split_a ? 1u : 0u) + (t->split_b ? 1u : 0u);
+    if (rest_records) *rest_records = t->split_a ? (t->split_rest ? t->split_rest->n_rec : 0u) : t->n_rec;
     return MP_OK;
 }
 
