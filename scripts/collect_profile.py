@@ -1,7 +1,8 @@
 """Copy a round's rocprofv3 summaries from gpurun_out/ into profiles/ and derive traffic.
 
-usage: python scripts/collect_profile.py <tag> [kernel]   (reads gpurun_out/prof_<tag>; kernel
-default scan_kernel)
+usage: python scripts/collect_profile.py <tag> [kernel [per_step]]   (reads gpurun_out/prof_<tag>;
+kernel default scan_kernel; per_step = launches of it per search step, e.g. 2 for a split
+W 7..9 table's two seed scans: counters and duration are then summed over a step's launches)
 Writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_bench.json (the bench line printed
 under the trace pass) and profiles/<tag>_pmc.json (per-dispatch counter means for the scan
 kernel plus HBM traffic per launch, gfx950-corrected as MI355X_MICROARCH.md prescribes:
@@ -19,6 +20,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
 kern = sys.argv[2] if len(sys.argv) > 2 else "scan_kernel"
+per_step = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
@@ -36,12 +38,36 @@ for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv")))
     for (_, c), v in per.items():
         agg[c].append(v)
     for k, v in agg.items():
-        pmc[k] = sum(v) / len(v)
+        pmc[k] = per_step * sum(v) / len(v)
 trace_ns = None
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
-    if kern in r["Name"]:
-        trace_ns = float(r["AverageNs"])
-out = {"kernel": "mp::" + kern, "avg_duration_ns_trace": trace_ns, "counters_mean_per_dispatch": pmc}
+    if kern in r["Name"]:  # per_step > 1: the kernel's template forms (one row each) summed
+        trace_ns = (trace_ns or 0.0) + float(r["AverageNs"]) if per_step > 1 else float(r["AverageNs"])
+# Per-dispatch durations from the trace: the pipelined bench (two search handles on two
+# streams) starts step i+1's scan while step i's kernels still run, so the timed steps' scans
+# overlap other kernels and their trace durations include that sharing.  The isolated
+# dispatches (no other kernel running at any time during them: warm-up, the bench's
+# scan-timing steps) are what the bench's HIP events time.
+iso, allk = [], []
+trace_csv = os.path.join(src, "trace", "run_kernel_trace.csv")
+if os.path.exists(trace_csv):
+    rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(trace_csv))]
+    rows.sort()
+    for i, (a, b, name) in enumerate(rows):
+        if kern not in name:
+            continue
+        allk.append(b - a)
+        if not any(c < b and d > a for j, (c, d, _) in enumerate(rows) if j != i and abs(j - i) < 64):
+            iso.append(b - a)
+if per_step > 1 and iso:
+    iso_step = per_step * sum(iso) / len(iso)
+else:
+    iso_step = sum(iso) / len(iso) if iso else None
+out = {"kernel": "mp::" + kern, "avg_duration_ns_trace": trace_ns, "counters_mean_per_dispatch": pmc,
+       "avg_duration_ns_trace_isolated": iso_step, "isolated_dispatches": len(iso), "dispatches": len(allk)}
+if per_step > 1:
+    out["per_step"] = (f"{per_step} launches per search step (split seed scans): counters are the mean per "
+                       f"launch x {per_step}, the duration the sum of the forms' average durations")
 if "FETCH_SIZE" in pmc:
     rd = 2 * pmc["FETCH_SIZE"] * 1024
     wr = pmc.get("WRITE_SIZE", 0.0) * 1024
