@@ -528,8 +528,9 @@ def main():
     # exact seeds with scan_kernel (plus dense_kernel over the records they cannot carry)
     sp = table.split()
     if sp["seed_tables"]:
-        scan_label = (f"mp::scan_kernel x{sp['seed_tables']} (split seeds: exact [0, W+4)"
-                      + (" + gapped [0, W) ++ [W+4, 16)" if sp["seed_tables"] > 1 else "")
+        W = cfg["W"]
+        scan_label = (f"mp::scan_kernel x{sp['seed_tables']} (split seeds: exact [0, 11)"
+                      + (f" + gapped [0, {W}) ++ [11, {22 - W})" if sp["seed_tables"] > 1 else "")
                       + (f" + dense_kernel over {sp['rest_records']} records" if sp["rest_records"] else "")
                       + "; one stage, HIP events around all of it)")
     else:

@@ -87,8 +87,8 @@ int mp_table_create(const mp_params* params, int32_t device, uint32_t n_rec,
                     void** table_out);
 /* Table statistics: distinct keys, largest bucket, device bytes. */
 int mp_table_stats(void* table, uint64_t* n_keys, uint64_t* max_bucket, uint64_t* dev_bytes);
-/* Split seeds of a W 7..9, I = 0, N <= 1 table (the dense table's search as exact-seed scans,
- * mp_internal.h kSplitSpan): seed_tables = 0 (not split), 1 (the contiguous seed, N = 0) or 2
+/* Split seeds of a W 7..9, I = 0, N <= 1 table (the dense table's search as 11-base exact-seed
+ * scans, mp_internal.h kSplitSeed): seed_tables = 0 (not split), 1 (the contiguous seed, N = 0) or 2
  * (contiguous + gapped, N = 1); rest_records = records left to the dense scan. */
 int mp_table_split(void* table, uint32_t* seed_tables, uint32_t* rest_records);
 void mp_table_destroy(void* table);
@@ -148,7 +148,7 @@ typedef struct mp_search_options {
     int32_t no_rank_filter;     /* 1: level-2 probes read the plain rank bitmap, without the
                                    filtered rank groups' primer-base filter */
     int32_t no_split;           /* 1: W 7..9 tables keep the dense scan, not the split seeds
-                                   (two exact-seed scans, see mp_internal.h kSplitSpan) */
+                                   (two exact-seed scans, see mp_internal.h kSplitSeed) */
 } mp_search_options;
 /* Replace the handle's options (reallocating the lists to the given capacities). */
 int mp_search_set_options(void* search, const mp_search_options* opt);

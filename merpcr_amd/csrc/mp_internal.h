@@ -154,26 +154,31 @@ struct Table {
     uint64_t planes_words = 0;
     uint8_t* pchars = nullptr;
     uint32_t rank_bits = 1;
-    // Split seeds (W 7..9, I = 0, N <= 1; see kSplitSpan): the dense table's search as scans of
+    // Split seeds (W 7..9, I = 0, N <= 1; see kSplitSeed): the dense table's search as scans of
     // longer exact seeds.  Sub-tables hold only the scan side; their Entry::rec are this
     // table's record indices, and the pair check, ranks and decode use this table's arrays.
-    Table* split_a = nullptr;     // seed = primer-1 bases [0, W + 4)
-    Table* split_b = nullptr;     // N = 1: the gapped seed [0, W) ++ [W + 4, kSplitSpan)
+    Table* split_a = nullptr;     // seed = primer-1 bases [0, kSplitSeed)
+    Table* split_b = nullptr;     // N = 1: the gapped seed [0, W) ++ [kSplitSeed, split_span(W))
     Table* split_rest = nullptr;  // records neither seed can carry: dense_kernel on them alone
-    uint32_t gap_at = 0, gap_len = 0;  // gapped table: key = bases [0, gap_at) ++ [gap_at + gap_len, ...)
+    // gapped table: key = bases [0, gap_at) ++ [gap_at + gap_len, gap_at + 2 gap_len); its key
+    // groups hold the gap's bases and the gap_post bases after the seed's span
+    uint32_t gap_at = 0, gap_len = 0, gap_post = 0;
 };
 
 // Split seeds.  Under I = 0 a window within N <= 1 mismatches of a record seeded at its
-// primer start, plain over bases [0, kSplitSpan), matches the key [0, W) exactly and has at
-// most one mismatch in [W, kSplitSpan).  Cut that stretch into A = [W, W + 4) and B =
-// [W + 4, kSplitSpan): one of them is exact (pigeonhole), so the window is found by an exact
-// seed [0, W + 4) or by the gapped seed [0, W) ++ B.  Both seeds are 11-13 bases long, and
-// scan_kernel's prefilter and key groups handle them as c3 handles W = 11: two scans of ~1%
-// seed windows each, where dense_kernel loads a filter oct for ~60% of all windows.  The
+// primer start, plain over bases [0, S) (S = split_span(W) = W + 2a, a = kSplitSeed - W),
+// matches the key [0, W) exactly and has at most one mismatch in [W, S).  Cut that stretch
+// into A = [W, W + a) and B = [W + a, S): one of them is exact (pigeonhole), so the window is
+// found by the exact seed [0, W + a) or by the gapped seed [0, W) ++ B -- both kSplitSeed = 11
+// bases, the c3 word size: scan_kernel's LDS prefilter and 2 MB key groups (which stay in an
+// XCD's 4 MB L2; 12-base seeds' 8 MB groups did not: 17 GB of L2 fills per scan) handle them
+// as they handle c3, where dense_kernel loads a filter oct for ~60% of all windows.  The
 // gapped scan keeps only windows whose A has a mismatch (or an invalid base), so no window
-// is found twice.  Every genome base in a 16-base funnel: B ends at base 16.
-constexpr uint32_t kSplitSpan = 16;
-constexpr uint32_t kSplitA = 4;  // bases of A
+// is found twice; its key groups also test the split_post(W) bases after S.  Every base the
+// gapped scan reads lies within a lane's 48 (window 31 + S + post <= 48).
+constexpr uint32_t kSplitSeed = 11;
+__host__ __device__ constexpr uint32_t split_span(uint32_t W) { return 2 * kSplitSeed - W; }
+__host__ __device__ constexpr uint32_t split_post(uint32_t W) { return 17 - split_span(W) < 3 ? 17 - split_span(W) : 3; }
 
 struct Genome {
     int device = 0;
@@ -423,6 +428,7 @@ uint32_t* sort_bucket_counts(Search* s);          // the bucket count array (zer
 uint32_t* sort_bucket_offsets(Search* s);         // nb + 1 offsets
 uint32_t* sort_bucket_cursors(Search* s);
 unsigned long long* sort_region_counts(Search* s);  // the run's hit-region counts (finish_fold)
+uint32_t* sort_crowded(Search* s);                 // [0] count, then the crowded buckets of a mode-1 run
 int alloc_sort_slots(Search* s, const SortPlan& P);  // mode 0's slot array for plan P
 
 // Raw hits arrive in runs of one bucket (a survivor's tries, a wave's batch of nearby
@@ -521,7 +527,7 @@ constexpr int kSchedBase = kPairQBase + 8 * kStatStride;
 constexpr int kHitBase = kSchedBase + 8 * kStatStride;
 constexpr int kHitRegions = 8;
 //   kSchedSplit     two more sets of 8 chunk counters: the gapped and the rest scans of a split
-//                   run (kSplitSpan) -- every scan of a run claims from counters zeroed by the
+//                   run (kSplitSeed) -- every scan of a run claims from counters zeroed by the
 //                   previous run's finish
 constexpr int kSchedSplit = kHitBase + kHitRegions * kStatStride;
 constexpr size_t kCounterBytes = (size_t)(kSchedSplit + 2 * 8 * kStatStride) * 8;

@@ -37,9 +37,11 @@ __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restric
                                                        uint32_t* __restrict__ off, uint32_t* __restrict__ cursor,
                                                        unsigned long long* __restrict__ counters, uint32_t n_words,
                                                        unsigned long long* __restrict__ h_out,
-                                                       unsigned long long* __restrict__ rcount) {
+                                                       unsigned long long* __restrict__ rcount,
+                                                       uint32_t* __restrict__ crowded) {
     __shared__ uint4 s_v4[kOffTile / 4];
     __shared__ uint32_t s_w[16];
+    if (threadIdx.x == 0) crowded[0] = 0;  // the previous run's crowded sort is complete (stream order)
     if (h_out) finish_fold(counters, n_words, h_out, rcount);
     bucket_offsets_block(cnt, nb, off, cursor, s_v4, s_w);
 }
@@ -101,21 +103,28 @@ __device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits
 // kBucketsPerBlock buckets per 256-thread workgroup.  A bucket of at most 64 keys (the common
 // case: ~32 per bucket at capacity) is ranked by its own wave, counting the smaller keys
 // (unique: one hit per (k, record, try)) over shuffles.  The workgroup then takes the larger
-// ones one after another: rank by counting through LDS up to 256 keys, bitonic sort in LDS up
-// to kSortCap.  (One workgroup per bucket left c4's 65,536
-// workgroups of ~24 keys dispatch-bound: 94 us.)
+// ones up to 256 keys one after another, ranking by counting through LDS.  Buckets over 256
+// (c4: IUPAC primers over N runs pile up to 2,048 hits on a position) go to the crowded list
+// for crowded_sort_decode, one 1024-thread workgroup each: a 256-thread workgroup sorting
+// them one after another (bitonic, 66 barrier stages for 2,048 keys) made the longest
+// workgroup of this kernel the order stage's critical path.  (One workgroup per bucket left
+// c4's 65,536 workgroups of ~24 keys dispatch-bound: 94 us.)
 constexpr uint32_t kBucketsPerBlock = 4;
+constexpr uint32_t kRankCap = 256;
 __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
                                                           uint32_t nb, unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
                                                           const uint64_t* __restrict__ seq_len, uint32_t n_seq,
                                                           const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
-                                                          mp_hit* __restrict__ out, unsigned long long* __restrict__ h_out) {
-    __shared__ uint64_t s_k[kSortCap];
+                                                          mp_hit* __restrict__ out, unsigned long long* __restrict__ h_out,
+                                                          uint32_t* __restrict__ crowded) {
+    __shared__ uint64_t s_k[kRankCap];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t b0 = blockIdx.x * kBucketsPerBlock;
     {
         const bool in = b0 + wave < nb;  // nb < kBucketsPerBlock under a forced sort_bucket_bits
         const uint32_t start = in ? off[b0 + wave] : 0u, m = in ? off[b0 + wave + 1] - start : 0u;
+        if (m > kSortCap && lane == 0) flag_overflow(h_out);
+        if (m > kRankCap && m <= kSortCap && lane == 0) crowded[1 + atomicAdd(&crowded[0], 1u)] = b0 + wave;
         if (m > 0 && m <= 64) {  // wave-uniform; no barrier inside
             const uint64_t key = lane < m ? keys[start + lane] : ~0ull;
             uint32_t r = 0;
@@ -125,48 +134,56 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
             }
             if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
         }
-        if (!__syncthreads_or(m > 64)) return;  // every wave reaches this barrier
+        if (!__syncthreads_or(m > 64 && m <= kRankCap)) return;  // every wave reaches this barrier
     }
     for (uint32_t q = 0; q < kBucketsPerBlock && b0 + q < nb; ++q) {  // block-uniform loop
         const uint32_t start = off[b0 + q], m = off[b0 + q + 1] - start;
-        if (m <= 64) continue;  // done by its wave above
-        if (m > kSortCap) {
-            if (threadIdx.x == 0) flag_overflow(h_out);
-            continue;
-        }
+        if (m <= 64 || m > kRankCap) continue;  // done by its wave above / crowded_sort_decode
         for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
-        const bool small = m <= 256;  // rank by counting; larger buckets: bitonic sort in LDS
-        if (!small) {
-            uint32_t P = 512;
-            while (P < m) P <<= 1;
-            for (uint32_t i = m + threadIdx.x; i < P; i += blockDim.x) s_k[i] = ~0ull;
-            __syncthreads();
-            for (uint32_t k = 2; k <= P; k <<= 1) {
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-                        const uint32_t ij = i ^ j;
-                        if (ij > i) {
-                            const uint64_t x = s_k[i], y = s_k[ij];
-                            if ((x > y) == ((i & k) == 0)) {
-                                s_k[i] = y;
-                                s_k[ij] = x;
-                            }
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-        }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
             const uint64_t key = s_k[i];
-            uint32_t r = i;
-            if (small) {
-                r = 0;
-                for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
-            }
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
             decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
         }
+        __syncthreads();  // s_k is refilled by the next bucket
+    }
+}
+
+// The crowded buckets (kRankCap < keys <= kSortCap) of a mode-1 run, one per 1024-thread
+// workgroup (persistent over the list): bitonic sort of the bucket padded to a power of two
+// in LDS, one compare-exchange pair per thread and stage, then the decoded records in order.
+__global__ __launch_bounds__(1024) void crowded_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
+                                                            unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
+                                                            const uint64_t* __restrict__ seq_len, uint32_t n_seq,
+                                                            const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
+                                                            mp_hit* __restrict__ out, const uint32_t* __restrict__ crowded) {
+    __shared__ uint64_t s_k[kSortCap];
+    const uint32_t n = crowded[0];
+    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {  // block-uniform
+        const uint32_t b = crowded[1 + c];
+        const uint32_t start = off[b], m = off[b + 1] - start;
+        uint32_t P = 2 * kRankCap;
+        while (P < m) P <<= 1;
+        for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) s_k[i] = i < m ? keys[start + i] : ~0ull;
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t t = threadIdx.x; t < P / 2; t += blockDim.x) {
+                    const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));  // the pair's lower index (bit j clear)
+                    const uint32_t ij = i | j;
+                    const uint64_t x = s_k[i], y = s_k[ij];
+                    if ((x > y) == ((i & k) == 0)) {
+                        s_k[i] = y;
+                        s_k[ij] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
+            decode_hit(s_k[i], start + i, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
         __syncthreads();  // s_k is refilled by the next bucket
     }
 }
@@ -225,7 +242,9 @@ bool sort_hits_device_ok(const Search* s) {
 
 int alloc_sort_buckets(Search* s) {
     // counts, nb + 1 offsets, cursors, then the hit-region counts (16-B aligned)
-    if (!s->bucket) MP_HIP_CHECK(hipMalloc(&s->bucket, (3ull << kMaxBucketBits) * 4 + 16 + kHitRegions * 8));
+    // + the crowded list: its count and up to 2^kMaxBucketBits bucket indices
+    if (!s->bucket) MP_HIP_CHECK(hipMalloc(&s->bucket, (3ull << kMaxBucketBits) * 4 + 16 + kHitRegions * 8 +
+                                                           4 * ((1ull << kMaxBucketBits) + 1)));
     return MP_OK;
 }
 
@@ -252,6 +271,7 @@ uint32_t* sort_bucket_cursors(Search* s) { return s->bucket + 2 * (1u << kMaxBuc
 unsigned long long* sort_region_counts(Search* s) {
     return reinterpret_cast<unsigned long long*>(s->bucket + 3 * (1u << kMaxBucketBits) + 4);
 }
+uint32_t* sort_crowded(Search* s) { return s->bucket + 3 * (1u << kMaxBucketBits) + 4 + 2 * kHitRegions; }
 
 int alloc_sort_slots(Search* s, const SortPlan& P) {
     const size_t need = (size_t)P.nb * P.slot_cap * sizeof(uint64_t);
@@ -275,7 +295,8 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     // kernel needs an agent-scope release per block (buffer_wbl2 of the XCD's L2, several
     // us each across the persistent grid), measured +65 us on a 1/8 c3 step.
     hipLaunchKernelGGL(bucket_offsets, dim3(1), dim3(1024), 0, st, sort_bucket_counts(s), P.nb, off, cursor,
-                       s->counters, (uint32_t)(counter_bytes() / 8), finish ? s->d_hcnt : nullptr, sort_region_counts(s));
+                       s->counters, (uint32_t)(counter_bytes() / 8), finish ? s->d_hcnt : nullptr, sort_region_counts(s),
+                       sort_crowded(s));
     MP_HIP_CHECK(hipGetLastError());
     if (mode == 0) {
         hipLaunchKernelGGL(sort_decode_slots, dim3((P.nb + kSlotWaves - 1) / kSlotWaves), dim3(64 * kSlotWaves), 0, st,
@@ -290,7 +311,11 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     MP_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
                        s->tmp_hi, off, P.nb, P.try_bits, P.low_bits,
-                       g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->d_hcnt);
+                       g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->d_hcnt, sort_crowded(s));
+    MP_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(crowded_sort_decode, dim3((uint32_t)s->n_cu), dim3(1024), 0, st, s->tmp_hi, off, P.try_bits,
+                       P.low_bits, g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out,
+                       sort_crowded(s));
     MP_HIP_CHECK(hipGetLastError());
     return MP_OK;
 }

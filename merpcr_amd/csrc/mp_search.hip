@@ -99,9 +99,10 @@ struct ScanArgs {
     uint32_t sort_nb, sort_shift, sort_try_bits, sort_low_bits;
     uint64_t* sort_slots;   // order mode 0: keys straight into their bucket slot (null: mode 1)
     uint32_t slot_cap;
-    // gapped seed (split tables, kSplitSpan): key = bases [0, gap_at) ++ the W - gap_at bases
-    // after the gap_len-base gap; gap_len 0: contiguous
-    uint32_t gap_at, gap_len;
+    // gapped seed (split tables, kSplitSeed): key = bases [0, gap_at) ++ the W - gap_at bases
+    // after the gap_len-base gap; gap_len 0: contiguous.  Its key-group fields hold the gap's
+    // bases and the gap_post bases after the seed's span.
+    uint32_t gap_at, gap_len, gap_post;
     uint32_t tail_ctr;      // counters[] slot of this scan's bucket-tail list (4; 5 for the gapped scan)
     uint32_t sched_base;    // counters[] index of this scan's 8 chunk counters (kSchedBase, kSchedSplit...)
 };
@@ -1319,9 +1320,10 @@ __device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, 
 // first W + F is one of A/C/G/T/U (under I = 1 a genome IUPAC base may match anything, and
 // it reads as 'A' in the 2-bit plane); bit 31 of pk marks a window where that fails, which
 // then passes on presence alone.
-// Gapped seed (kGap, split tables): the field holds the record's gap bases; a window passes
-// when they differ in 1..N positions, or when it has an invalid base in its gap (bit 31 of
-// pk) -- with none of either, the contiguous seed of the split finds the window.
+// Gapped seed (kGap, split tables): the field holds the record's gap bases, then its gap_post
+// bases after the seed's span (the low 2 gap_post bits); a window passes when its gap differs
+// in 1..N positions, or has an invalid base (bit 31 of pk) -- with neither, the contiguous seed
+// of the split finds the window -- and gap and post bases together differ in at most N.
 template <bool kGap = false>
 __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
     const uint32_t bit = pk & 15u;
@@ -1332,8 +1334,8 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
         if (!(field & kKgrpFlag)) return true;
         const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
-        const uint32_t mm = (uint32_t)__popc((x | (x >> 1)) & 0x55555555u);
-        return mm <= (uint32_t)a.N && (mm != 0u || (pk >> 31) != 0u);
+        const uint32_t m = (x | (x >> 1)) & 0x55555555u;
+        return (uint32_t)__popc(m) <= (uint32_t)a.N && ((m >> (2u * a.gap_post)) != 0u || (pk >> 31) != 0u);
     }
     if (a.kgrp_wild) {
         if (pk >> 31) return true;
@@ -1590,9 +1592,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                             const uint32_t i = po[q] & 31u;
                             const uint32_t key = (kGap ? gap_key(funnel3(A, B, C, i), a.gap_at, a.gap_len)
                                                        : funnel3(A, B, C, i)) >> shw;
-                            // the field's bases: after the key, or a gapped seed's gap
-                            pk[q] = ((funnel3(A, B, C, i + (kGap ? a.gap_at : W)) >> (32u - 2u * a.kgrp_F)) << 4) |
-                                    (key & 15u) | ((qe >> 15) << 31);
+                            // the field's bases: after the key, or a gapped seed's gap and the
+                            // bases after its span (2 gap_len bases after the gap's start)
+                            uint32_t fb;
+                            if constexpr (kGap) {
+                                const uint32_t f = funnel3(A, B, C, i + a.gap_at);
+                                fb = ((f >> (32u - 2u * a.gap_len)) << (2u * a.gap_post)) |
+                                     (a.gap_post ? (f << (4u * a.gap_len)) >> (32u - 2u * a.gap_post) : 0u);
+                            } else {
+                                fb = funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F);
+                            }
+                            pk[q] = (fb << 4) | (key & 15u) | ((qe >> 15) << 31);
                             rw[q] = a.kgrp[v ? (key >> 4) : 0u];
                         } else {
                             pk[q] = v ? L.rq.r[e] : 0u;
@@ -2441,6 +2451,7 @@ static void scan_fields(ScanArgs& a, const Table* t, const Search* s) {
     a.W = t->prm.wordsize;
     a.gap_at = t->gap_at;
     a.gap_len = t->gap_len;
+    a.gap_post = t->gap_post;
 }
 
 // The scan kernel of table t (dense_kernel, or scan_kernel in the form the table and the
@@ -2510,7 +2521,7 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
     return MP_OK;
 }
 
-// Split seeds in use for this handle (kSplitSpan): the table has them and the options leave
+// Split seeds in use for this handle (kSplitSeed): the table has them and the options leave
 // the dense path alone (no_dense or no_split keep the unsplit table's scan).
 static bool use_split(const Search* s) {
     return s->table->split_a && !s->opt.no_dense && !s->opt.no_split;

@@ -98,21 +98,24 @@ MP_EXPORT int mp_device_count(int32_t* n) {
     return MP_OK;
 }
 
-// Builds one table.  rec_map (sub-tables of a split, see kSplitSpan): record r of these
+// Builds one table.  rec_map (sub-tables of a split, see kSplitSeed): record r of these
 // arrays is record rec_map[r] of the parent, which Entry::rec names.  gap_len > 0: the keys
 // are gapped seeds (bases [0, gap_at) ++ [gap_at + gap_len, gap_at + gap_len + W - gap_at)):
 // no compact heads (they restate a primer from a contiguous key), and the key groups hold
-// the gap's bases for the gapped scan's one-mismatch test (kgrp_pass).
+// the gap's bases and the gap_post bases after the seed's span for the gapped scan's
+// one-mismatch test (kgrp_pass).
 static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const uint32_t* key,
                        const uint32_t* hash_off, const uint64_t* pcr_size, const uint8_t* primer1,
                        const uint64_t* p1_off, const uint8_t* primer2, const uint64_t* p2_off,
-                       const uint32_t* rec_map, uint32_t gap_at, uint32_t gap_len, Table** table_out) {
+                       const uint32_t* rec_map, uint32_t gap_at, uint32_t gap_len, uint32_t gap_post,
+                       Table** table_out) {
     Table* t = new Table();
     t->prm = p;
     t->device = device;
     t->n_rec = n_rec;
     t->gap_at = gap_at;
     t->gap_len = gap_len;
+    t->gap_post = gap_post;
     const bool gapped = gap_len != 0;
     int rc = MP_OK;
     do {
@@ -457,14 +460,17 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
             // F <= 17 - W, and a field holds <= 7 bases
             if (gapped && W >= 11 && W <= 13) {
                 // gapped seed: a field per single-record key holding the record's gap bases
-                // [gap_at, gap_at + gap_len); the gapped scan keeps a window only when they
-                // differ from the window's in 1..N positions, or its gap holds an invalid base
-                // (no mismatch there: the contiguous seed finds the window)
-                const uint32_t F = gap_len;
+                // [gap_at, gap_at + gap_len) and then the gap_post bases after the seed's span
+                // (bases [gap_at + 2 gap_len, + gap_post)); the gapped scan keeps a window only
+                // when its gap differs in 1..N positions (or holds an invalid base: no mismatch
+                // there, the contiguous seed finds the window) and gap + post differ in <= N
+                const uint32_t F = gap_len + gap_post;
+                const uint32_t post_at = gap_at + 2 * gap_len;
                 t->kgrp_F = F;
                 const uint64_t nkeys = 1ull << (2 * W);
                 kgrp.assign(nkeys / kKgrpKeys, 0ull);
-                const uint64_t gm = sp_lt((int)(gap_at + F)) & ~sp_lt((int)gap_at);  // the gap's plain bits
+                const uint64_t gm = (sp_lt((int)(gap_at + gap_len)) & ~sp_lt((int)gap_at)) |
+                                    (sp_lt((int)(post_at + gap_post)) & ~sp_lt((int)post_at));  // plain bits needed
                 for (uint64_t g = 0; g < kgrp.size(); ++g) {
                     const uint32_t pres = (uint32_t)((filt[g >> 1] >> ((g & 1) * 16)) & 0xFFFFu);
                     uint64_t w = pres;
@@ -474,8 +480,12 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                         const uint32_t k = (uint32_t)(g * kKgrpKeys + bit);
                         const uint32_t b = rank_bucket[rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u))];
                         const Entry& e = ents[boff[b]];
-                        if (bcount[b] == 1 && e.hash_off == 0 && (e.pmask & gm) == gm && ((e.pmask >> 1) & gm) == 0)
-                            w |= (uint64_t)(kKgrpFlag | (uint32_t)((e.code << (2 * gap_at)) >> (64 - 2 * F))) << (16u + 16u * j);
+                        if (bcount[b] == 1 && e.hash_off == 0 && e.l1 >= post_at + gap_post && (e.pmask & gm) == gm &&
+                            ((e.pmask >> 1) & gm) == 0) {
+                            const uint32_t gb = (uint32_t)((e.code << (2 * gap_at)) >> (64 - 2 * gap_len));
+                            const uint32_t pb = gap_post ? (uint32_t)((e.code << (2 * post_at)) >> (64 - 2 * gap_post)) : 0u;
+                            w |= (uint64_t)(kKgrpFlag | (gb << (2 * gap_post)) | pb) << (16u + 16u * j);
+                        }
                         ++j;
                     }
                     kgrp[g] = w;
@@ -617,10 +627,11 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
     return MP_OK;
 }
 
-// Split seeds (kSplitSpan): the sub-tables of a W 7..9, I = 0, N <= 1 table.  A record takes
+// Split seeds (kSplitSeed): the sub-tables of a W 7..9, I = 0, N <= 1 table.  A record takes
 // the seeds when it is seeded at its primer start and its primer 1 is plain over the bases
-// the seeds and the pigeonhole cut need (N = 1: [0, kSplitSpan); N = 0: [0, W + 4)); the rest
-// stay in a dense table of their own.  Not split when under half the records qualify.
+// the seeds, the pigeonhole cut and the gapped key groups need (N = 1: [0, S + post), S =
+// split_span(W); N = 0: [0, kSplitSeed)); the rest stay in a dense table of their own.  Not
+// split when under half the records qualify.
 static int build_split(Table* t, uint32_t n_rec, const uint32_t* key, const uint32_t* hash_off,
                        const uint64_t* pcr_size, const uint8_t* primer1, const uint64_t* p1_off,
                        const uint8_t* primer2, const uint64_t* p2_off) {
@@ -628,7 +639,8 @@ static int build_split(Table* t, uint32_t n_rec, const uint32_t* key, const uint
     const uint32_t W = (uint32_t)p.wordsize;
     if (W < 7 || W > 9 || p.iupac_mode != 0 || p.mismatches > 1 || n_rec == 0) return MP_OK;
     if (const char* e = std::getenv("MP_NO_SPLIT"); e && std::atoi(e)) return MP_OK;
-    const uint32_t need = p.mismatches ? kSplitSpan : W + kSplitA;
+    const uint32_t S = split_span(W), A = kSplitSeed - W;  // span of the cut stretch, bases of A (= of B)
+    const uint32_t need = p.mismatches ? S + split_post(W) : kSplitSeed;
     auto code = [](uint8_t c) -> int {
         switch (upcase(c)) { case 'A': return 0; case 'C': return 1; case 'G': return 2; case 'T': return 3; default: return -1; }
     };
@@ -652,11 +664,11 @@ static int build_split(Table* t, uint32_t n_rec, const uint32_t* key, const uint
         for (uint32_t r : recs) {
             const uint8_t* q = primer1 + p1_off[r];
             uint32_t k = 0;
-            if (form == 0) {  // A: [0, W + 4)
-                for (uint32_t i = 0; i < W + kSplitA; ++i) k = (k << 2) | (uint32_t)code(q[i]);
-            } else if (form == 1) {  // B: [0, W) ++ [W + 4, kSplitSpan)
+            if (form == 0) {  // A: [0, W + a)
+                for (uint32_t i = 0; i < kSplitSeed; ++i) k = (k << 2) | (uint32_t)code(q[i]);
+            } else if (form == 1) {  // B: [0, W) ++ [W + a, S)
                 for (uint32_t i = 0; i < W; ++i) k = (k << 2) | (uint32_t)code(q[i]);
-                for (uint32_t i = W + kSplitA; i < kSplitSpan; ++i) k = (k << 2) | (uint32_t)code(q[i]);
+                for (uint32_t i = W + A; i < S; ++i) k = (k << 2) | (uint32_t)code(q[i]);
             } else {
                 k = key[r];
             }
@@ -671,24 +683,25 @@ static int build_split(Table* t, uint32_t n_rec, const uint32_t* key, const uint
         }
         return s;
     };
-    auto make = [&](const Sub& s, uint32_t w, uint32_t gap_at, uint32_t gap_len, Table** out) {
+    auto make = [&](const Sub& s, uint32_t w, uint32_t gap_at, uint32_t gap_len, uint32_t gap_post, Table** out) {
         mp_params q = p;
         q.wordsize = (int32_t)w;
         return build_table(q, t->device, (uint32_t)s.key.size(), s.key.data(), s.hoff.data(), s.size.data(),
-                           s.b1.data(), s.o1.data(), s.b2.data(), s.o2.data(), s.map.data(), gap_at, gap_len, out);
+                           s.b1.data(), s.o1.data(), s.b2.data(), s.o2.data(), s.map.data(), gap_at, gap_len,
+                           gap_post, out);
     };
     int rc = MP_OK;
     {
         const Sub a = subset(yes, 0);
-        rc = make(a, W + kSplitA, 0, 0, &t->split_a);
+        rc = make(a, kSplitSeed, 0, 0, 0, &t->split_a);
     }
     if (!rc && p.mismatches) {
         const Sub b = subset(yes, 1);
-        rc = make(b, W + (kSplitSpan - W - kSplitA), W, kSplitA, &t->split_b);
+        rc = make(b, kSplitSeed, W, A, split_post(W), &t->split_b);
     }
     if (!rc && !rest.empty()) {
         const Sub r = subset(rest, 2);
-        rc = make(r, W, 0, 0, &t->split_rest);
+        rc = make(r, W, 0, 0, 0, &t->split_rest);
     }
     if (rc) {
         free_table(t->split_a); free_table(t->split_b); free_table(t->split_rest);
@@ -715,7 +728,7 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
     if (n_rec && (!key || !hash_off || !pcr_size || !primer1 || !p1_off || !primer2 || !p2_off))
         return fail(MP_E_ARG, "mp_table_create: null record array");
     Table* t = nullptr;
-    int rc = build_table(p, device, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off, nullptr, 0, 0, &t);
+    int rc = build_table(p, device, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off, nullptr, 0, 0, 0, &t);
     if (rc) return rc;
     rc = build_split(t, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off);
     if (rc) {
