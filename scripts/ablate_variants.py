@@ -17,6 +17,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       with mp_debug_pair_counts (a function only this variant exports)
   54  pair_kernel without the primer-1 compare (every fingerprint survivor kept)
   55  pair_kernel's lane-parallel tries computed but never staged (no hits written)
+  60  scan_kernel's genome-plane loads non-temporal (the stream kept out of L2's working set:
+      the c4 level-2 tables, rank words + 16-B heads, are ~4.1 MB against a 4 MB L2)
 """
 import os
 import shutil
@@ -37,6 +39,12 @@ _T_ENTRY = "    zero_sort_counts(a);\n    // stage the seed prefilter in LDS (on
 _T_STAGED = "    const int lane = threadIdx.x & 63;\n    const int w = threadIdx.x >> 6;\n    const uint64_t stride = (uint64_t)gridDim.x * kWaves;"
 _T_END = "    close_chunked(a.surv, a.surv_cap, lane, C);\n    close_chunked<2>(a.tails, a.tails_cap, lane, TC);"
 _T_TAIL = "MP_EXPORT int mp_search_set_stage_timing(void* search, int32_t on) {"
+_WORDS = ("        w0 = a.g2[j >> 5];\n        w1 = a.g2[(j >> 5) + 1];\n        const uint64_t v0 = a.ginv[j >> 6];\n"
+          "        const uint64_t v1 = a.ginv[(j >> 6) + 1];\n        const uint32_t sh = (uint32_t)(j & 32);  // branch-free")
+_WORDS_NT = ("        w0 = __builtin_nontemporal_load(&a.g2[j >> 5]);\n        w1 = __builtin_nontemporal_load(&a.g2[(j >> 5) + 1]);\n"
+             "        const uint64_t v0 = __builtin_nontemporal_load(&a.ginv[j >> 6]);\n"
+             "        const uint64_t v1 = __builtin_nontemporal_load(&a.ginv[(j >> 6) + 1]);\n"
+             "        const uint32_t sh = (uint32_t)(j & 32);  // branch-free")
 _T_GLOBAL = ("}  // namespace mp\n\nusing namespace mp;\n\nMP_EXPORT int mp_search_set_stage_timing")
 
 VARIANTS = {
@@ -78,6 +86,7 @@ VARIANTS = {
          (_T_TAIL, "MP_EXPORT int mp_debug_pair_counts(unsigned long long* out) {  // ablation 52\n"
                    "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_counts), 8 * 8) == hipSuccess ? 0 : -1;\n}\n\n")],
     54: [(_P1, "    if (true) {} else  // ablation 54\n")],
+    60: [(_WORDS, _WORDS_NT, "replace")],
     55: [(_LPHIT, "            if (hit && t < -1000000) // ablation 55\n")],
 }
 
@@ -93,9 +102,10 @@ def make_source_dir(variant: int, csrc: str, root: str) -> str:
     shutil.copytree(os.path.join(os.path.dirname(os.path.dirname(csrc)), "include"), os.path.join(root, "include"))
     p = os.path.join(dst, "mp_search.hip")
     s = open(p).read()
-    for anchor, ins in VARIANTS[variant]:
+    for edit in VARIANTS[variant]:
+        anchor, ins = edit[0], edit[1]
         if s.count(anchor) != 1:
             raise RuntimeError(f"ablation {variant}: anchor not unique in mp_search.hip: {anchor[:60]!r}")
-        s = s.replace(anchor, ins + anchor)
+        s = s.replace(anchor, ins if len(edit) > 2 and edit[2] == "replace" else ins + anchor)
     open(p, "w").write(s)
     return dst
