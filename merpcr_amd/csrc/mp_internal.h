@@ -133,6 +133,8 @@ struct Table {
     uint2* dents8 = nullptr;      // W <= 13: 8-B heads {primer-1 bases W..W+15, rec | (l1-W)<<26 | full<<31}
     uint4* dents16 = nullptr;     // h16: 16-B heads {bases W..W+15, plain bits, never bits, as dents8.y}
     int h16 = 0;                  // many heads need plain/never masks (IUPAC primers): 16-B heads
+    uint2* dents12 = nullptr;     // h12: the IUPAC heads in 8 B (kHead12RecBits), in place of dents16
+    int h12 = 0;                  // h16 tables whose heads fit the 8-B IUPAC form (c4)
     uint64_t* kgrp = nullptr;     // W 11..13: key groups, one u64 per 16 keys (see kKgrpKeys)
     uint32_t kgrp_F = 0;          // primer-1 bases W..W+F-1 a key-group field holds (0: no key groups)
     int kgrp_wild = 0;            // I = 1 field form: two 24-bit fields with the non-plain bases marked
@@ -326,6 +328,15 @@ constexpr uint32_t kHead8RecBits = 26;
 // top).  The ranked drain hands such a bucket to tail_kernel only when some record's F
 // bases are within N mismatches of the genome (a lower bound on primer-1 mismatches).
 constexpr uint32_t kHead8Filt = 0x40000000u;
+// 8-B IUPAC head (Table::h12, round 3): the 16-B head's information for bases W..W+11 only --
+// .x = their 2-bit codes (bits 31..8, base W on top) | l1 - W (bits 4..0, <= 31); .y = record
+// (bits 0..17) | their plain bits (bit 29 = base W ... bit 18 = base W+11); a record with a
+// "never" base there, a longer primer or more records is a full head (as dents8's).  Bases
+// past W+11 are not tested in the drain, so a survivor of a primer longer than W+12 is not
+// exact (pair_kernel compares it whole).  c4's 195k heads take 1.6 MB instead of 3.1 MB,
+// and with the 1 MB rank words they stay in an XCD's 4 MB L2.
+constexpr uint32_t kHead12RecBits = 18;
+constexpr uint32_t kHead12Bases = 12;
 __host__ __device__ __forceinline__ uint32_t head8_filt_bases(uint32_t records) { return 14u / records; }
 // Tables with W <= 9 run dense_kernel: the rank bitmap (4^W / 4 bytes <= 64 KiB) lives in
 // LDS and each lane walks its own seeds' buckets.

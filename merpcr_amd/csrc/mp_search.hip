@@ -62,6 +62,7 @@ struct ScanArgs {
     const Entry* dents;     // W <= 13: bucket heads by rank
     const uint2* dents8;    // W <= 13: 8-B heads
     const uint4* dents16;   // W <= 13, Table::h16: 16-B heads (primers with IUPAC bases after the seed)
+    const uint2* dents12;   // Table::h12: the same heads in the 8-B IUPAC form (kHead12RecBits)
     const uint2* binfo;     // W <= kDenseMaxW: bucket {first padded entry, records} by key rank
     const uint16_t* dfilt;  // W <= kDenseMaxW: filter word per padded entry
     const uint2* dgrp;      // W <= kDenseMaxW: per-32-key bucket index
@@ -910,6 +911,32 @@ __device__ __forceinline__ Entry head16_entry(const uint4 c, uint32_t h, uint32_
     return e;
 }
 
+// The plain bits of an 8-B IUPAC head (bits 29..18 of .y, base W first) spread to the
+// low bits of their 2-bit slots in a window of bases W..W+15 (base W at bit 30).
+__device__ __forceinline__ uint32_t head12_plain(uint32_t y) {
+    uint32_t v = (y >> kHead12RecBits) & 0xFFFu;
+    v = (v | (v << 8)) & 0x00FF00FFu;
+    v = (v | (v << 4)) & 0x0F0F0F0Fu;
+    v = (v | (v << 2)) & 0x33333333u;
+    v = (v | (v << 1)) & 0x55555555u;
+    return v << 8;
+}
+
+// Entry of an 8-B IUPAC head (kHead8Full clear): the seed key h supplies bases [0, W), the
+// head bases W..W+11 and their plain bits; later bases are neither plain nor never (skipped
+// by fp_reject, which then reports the survivor not exact).
+__device__ __forceinline__ Entry head12_entry(const uint2 c, uint32_t h, uint32_t W) {
+    Entry e;
+    e.code = ((uint64_t)h << (64 - 2 * W)) | ((uint64_t)(c.x & 0xFFFFFF00u) << (32 - 2 * W));
+    e.rec = c.y & ((1u << kHead12RecBits) - 1u);
+    e.hash_off = 0;
+    e.l1 = (uint16_t)(W + (c.x & 31u));
+    e.pmask = sp_lt((int)W) | ((uint64_t)head12_plain(c.y) << (32 - 2 * W));
+    e.xstart = 0;
+    e.count = 1;
+    return e;
+}
+
 // Bucket head of seed key h (W <= 13: rank of h in the exact bitmap; above: slot).
 template <int kMode>
 __device__ __forceinline__ bool bucket_head(const ScanArgs& a, uint32_t h, Entry& e0) {
@@ -1036,17 +1063,18 @@ __device__ __forceinline__ void drain_seeds(const ScanArgs& a, const SuperRegs& 
 // full head sends its whole bucket to tail_kernel (its first entry is in the head's low
 // word), so the drain never reads a 32-B Entry.  Compact heads whose primer span holds a
 // genome exception base take the general candidate test (rare: all lanes must call).
-// kH16: 16-B heads (Table::h16) -- .x bases W..W+15, .y plain bits, .z never bits, .w the
+// kH16 1: 16-B heads (Table::h16) -- .x bases W..W+15, .y plain bits, .z never bits, .w the
 // 8-B head's second word; a position that is neither (an IUPAC base under I=1) is skipped,
-// so the count is a lower bound and the survivor is not exact.
-template <bool kH16>
+// so the count is a lower bound and the survivor is not exact.  kH16 2: the 8-B IUPAC form
+// (Table::h12: .x and .w as kHead12RecBits describes) -- bases W..W+11 only.
+template <int kH16>
 __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
                                               bool l, uint32_t p, const uint4 c4, uint64_t G, uint32_t x, int lane,
                                               uint32_t& ncand, SurvChunk& C, SurvChunk& TC) {
     const uint32_t W = (uint32_t)a.W;
     const uint2 c = make_uint2(c4.x, c4.w);  // the 8-B head's words
     const bool full = l && (c.y & kHead8Full);
-    const uint32_t L = (c.y >> kHead8RecBits) & 31u;  // l1 - W
+    const uint32_t L = kH16 == 2 ? (c.x & 31u) : (c.y >> kHead8RecBits) & 31u;  // l1 - W
     const uint32_t l1 = W + L;
     const uint32_t exl = l1 >= 32u ? x : x & ~(0xFFFFFFFFu >> l1);
     const bool compact = l && !full;
@@ -1054,11 +1082,16 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
     bool act = compact && !general && (uint64_t)p + l1 <= n;
     if (!R.owned) act = act && sbase + p >= a.g_lo && sbase + p < a.g_hi;
     const uint32_t g = (uint32_t)((G << (2u * W)) >> 32);
-    const uint32_t xx = g ^ c.x;
-    const uint32_t inm = L >= 16u ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (2u * L));
+    const uint32_t xx = g ^ (kH16 == 2 ? (c.x & 0xFFFFFF00u) : c.x);
+    const uint32_t Lc = kH16 == 2 ? min(L, kHead12Bases) : L;  // bases the head covers
+    const uint32_t inm = Lc >= 16u ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (2u * Lc));
     uint32_t d;
     bool exact = true;
-    if constexpr (kH16) {
+    if constexpr (kH16 == 2) {
+        const uint32_t pl = head12_plain(c.y);
+        d = (xx | (xx >> 1)) & pl & inm;
+        exact = L <= kHead12Bases && (pl & inm) == (0x55555555u & inm);
+    } else if constexpr (kH16 == 1) {
         d = (((xx | (xx >> 1)) & c4.y) | c4.z) & 0x55555555u & inm;
         exact = ((c4.y | c4.z) & 0x55555555u & inm) == (0x55555555u & inm);
     } else {
@@ -1071,7 +1104,8 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
     if (__any(general)) {
         const uint32_t hk = (uint32_t)(G >> (64u - 2u * W));
         Entry e;
-        if constexpr (kH16) e = head16_entry(c4, hk, W);
+        if constexpr (kH16 == 2) e = head12_entry(c, hk, W);
+        else if constexpr (kH16 == 1) e = head16_entry(c4, hk, W);
         else e = head8_entry(c, hk, W);
         uint32_t k2 = 0;
         bool ex2 = false;
@@ -1081,7 +1115,7 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
             exact = ex2;
         }
     }
-    flush_survivors(a, R, sbase, surv, p, c.y & ((1u << kHead8RecBits) - 1u), exact, lane, C);
+    flush_survivors(a, R, sbase, surv, p, c.y & ((1u << (kH16 == 2 ? kHead12RecBits : kHead8RecBits)) - 1u), exact, lane, C);
     bool defer = full;
     if (full && (c.y & kHead8Filt)) {
         // bucket prefilter (kHead8Filt): every record's bases W..W+F-1 against the genome;
@@ -1106,7 +1140,7 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
 
 // drain_seeds for the ranked queue (kMode 1, 1): the head comes straight from the
 // queued key rank -- one dependent load (the 8-B head) per seed instead of two.
-template <bool kInline, bool kDefer, bool kH16 = false>
+template <bool kInline, bool kDefer, int kH16 = 0>
 __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs& R, uint64_t sbase, uint32_t n,
                                              uint32_t qn, int lane, uint32_t& ncand, WaveLds& L,
                                              SurvChunk& C, SurvChunk& TC) {
@@ -1117,15 +1151,26 @@ __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs&
         const uint32_t pa = R.base + (la ? (uint32_t)L.rq.q[ea] : 0u);
         const uint32_t pb = R.base + (lb ? (uint32_t)L.rq.q[eb] : 0u);
         const uint32_t qa = la ? L.rq.r[ea] : 0u, qb = lb ? L.rq.r[eb] : 0u;
-        if constexpr (kH16) {  // deferring drain over 16-B heads
+        if constexpr (kH16 == 2) {  // deferring drain over 8-B IUPAC heads
+            const uint2 ca = a.dents12[qa];
+            const uint2 cb = a.dents12[qb];
+            uint64_t Ga, Gb;
+            uint32_t xa, xb;
+            window_from_regs(a, R, sbase, pa, true, Ga, xa);
+            window_from_regs(a, R, sbase, pb, true, Gb, xb);
+            drain_compact<2>(a, R, sbase, n, la, pa, make_uint4(ca.x, 0u, 0u, ca.y), Ga, xa, lane, ncand, C, TC);
+            if (b + 64 < qn) drain_compact<2>(a, R, sbase, n, lb, pb, make_uint4(cb.x, 0u, 0u, cb.y), Gb, xb, lane, ncand, C, TC);
+            continue;
+        }
+        if constexpr (kH16 == 1) {  // deferring drain over 16-B heads
             const uint4 ca = a.dents16[qa];
             const uint4 cb = a.dents16[qb];
             uint64_t Ga, Gb;
             uint32_t xa, xb;
             window_from_regs(a, R, sbase, pa, true, Ga, xa);
             window_from_regs(a, R, sbase, pb, true, Gb, xb);
-            drain_compact<true>(a, R, sbase, n, la, pa, ca, Ga, xa, lane, ncand, C, TC);
-            if (b + 64 < qn) drain_compact<true>(a, R, sbase, n, lb, pb, cb, Gb, xb, lane, ncand, C, TC);
+            drain_compact<1>(a, R, sbase, n, la, pa, ca, Ga, xa, lane, ncand, C, TC);
+            if (b + 64 < qn) drain_compact<1>(a, R, sbase, n, lb, pb, cb, Gb, xb, lane, ncand, C, TC);
             continue;
         }
         const uint2 ca = a.dents8[qa];
@@ -1135,9 +1180,9 @@ __device__ __forceinline__ void drain_ranked(const ScanArgs& a, const SuperRegs&
         window_from_regs(a, R, sbase, pa, true, Ga, xa);
         window_from_regs(a, R, sbase, pb, true, Gb, xb);
         if constexpr (kDefer) {  // compact heads tested here, full-head buckets to tail_kernel
-            drain_compact<false>(a, R, sbase, n, la, pa, make_uint4(ca.x, 0u, 0u, ca.y), Ga, xa, lane, ncand, C, TC);
+            drain_compact<0>(a, R, sbase, n, la, pa, make_uint4(ca.x, 0u, 0u, ca.y), Ga, xa, lane, ncand, C, TC);
             if (b + 64 < qn)
-                drain_compact<false>(a, R, sbase, n, lb, pb, make_uint4(cb.x, 0u, 0u, cb.y), Gb, xb, lane, ncand, C, TC);
+                drain_compact<0>(a, R, sbase, n, lb, pb, make_uint4(cb.x, 0u, 0u, cb.y), Gb, xb, lane, ncand, C, TC);
             continue;
         }
         const uint32_t ha = (uint32_t)(Ga >> shw), hb = (uint32_t)(Gb >> shw);
@@ -1447,7 +1492,7 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
     }
 };
 
-template <int kMode, bool kInline, int kK = 1, bool kDefer = false, bool kH16 = false, bool kRkf = false,
+template <int kMode, bool kInline, int kK = 1, bool kDefer = false, int kH16 = 0, bool kRkf = false,
           bool kGap = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     static_assert(!kGap || (kMode == 1 && kRkf), "gapped seeds take the key-group path");
@@ -2445,7 +2490,7 @@ static void scan_fields(ScanArgs& a, const Table* t, const Search* s) {
     a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
     a.defer_full = t->defer_full && (!s->opt.no_defer || t->gap_len);
     a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F; a.kgrp_wild = t->kgrp_wild;
-    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.lfilt = t->lfilt;
+    a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.dents12 = t->dents12; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents;
     a.W = t->prm.wordsize;
@@ -2500,16 +2545,22 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 3 && a.defer_full && rkf)  // MP_LDS_K=3 (A/B)
             hipLaunchKernelGGL((scan_kernel<1, false, 3, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 3 && a.defer_full && t->h12)
+            hipLaunchKernelGGL((scan_kernel<1, false, 3, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 3 && a.defer_full && t->h16)
-            hipLaunchKernelGGL((scan_kernel<1, false, 3, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+            hipLaunchKernelGGL((scan_kernel<1, false, 3, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h12)
+            hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full && t->h16)
-            hipLaunchKernelGGL((scan_kernel<1, false, 2, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+            hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 1 && a.defer_full && rkf)
             hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && a.defer_full && t->h12)
+            hipLaunchKernelGGL((scan_kernel<1, false, 1, true, 2>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && a.defer_full && t->h16)
-            hipLaunchKernelGGL((scan_kernel<1, false, 1, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+            hipLaunchKernelGGL((scan_kernel<1, false, 1, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && a.defer_full)
             hipLaunchKernelGGL((scan_kernel<1, false, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);

@@ -51,6 +51,7 @@ static int upload(T** dst, const T* src, size_t n, uint64_t* bytes) {
 static void free_table(Table* t) {
     if (!t) return;
     free_table(t->split_a); free_table(t->split_b); free_table(t->split_rest);
+    hipFree(t->dents12);
     hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->kgrp); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
     hipFree(t->pchars);
@@ -122,6 +123,7 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         if (hipSetDevice(device) != hipSuccess) { rc = fail(MP_E_HIP, "hipSetDevice failed"); break; }
         const uint32_t W = (uint32_t)p.wordsize;
         const uint64_t key_limit = (W == 16) ? (1ull << 32) : (1ull << (2 * W));
+        uint64_t dev_bytes_pre = 0;  // uploads made before the final batch (the 8-B IUPAC heads)
 
         // ---- buckets in first-appearance order, records in insertion order
         std::unordered_map<uint32_t, uint32_t> bucket_of;
@@ -415,16 +417,37 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                                   (uint32_t)((((e.pmask >> 1) & kEven) << (2 * W)) >> 32),
                                   e.rec | ((uint32_t)(e.l1 - W) << kHead8RecBits));
             };
-            uint64_t n_full8 = 0, n_full16 = 0;
+            // 8-B IUPAC form (kHead12RecBits): bases W..W+11, their plain bits, l1 - W
+            auto entry12 = [&](const Entry& e) {
+                const uint64_t seed = sp_lt((int)W);
+                const int cov = (int)std::min<uint32_t>(e.l1 > W ? e.l1 - W : 0u, kHead12Bases);
+                const uint64_t covm = sp_lt((int)W + cov) & ~seed;  // the covered primer bases
+                const bool fits = !gapped && e.count == 1 && e.hash_off == 0 && e.l1 >= W && e.l1 - W <= 31 &&
+                                  e.rec < (1u << kHead12RecBits) && (e.pmask & seed) == seed &&
+                                  ((e.pmask >> 1) & seed) == 0 && ((e.pmask >> 1) & covm) == 0;
+                if (!fits) return make_uint2(0u, kHead8Full);
+                uint32_t plain = 0;
+                for (uint32_t j = 0; j < kHead12Bases; ++j)
+                    if ((e.pmask >> (62 - 2 * (W + j))) & 1ull) plain |= 1u << (kHead12Bases - 1 - j);
+                return make_uint2((uint32_t)(((e.code << (2 * W)) >> 40) << 8) | (uint32_t)(e.l1 - W),
+                                  e.rec | (plain << kHead12RecBits));
+            };
+            uint64_t n_full8 = 0, n_full16 = 0, n_full12 = 0;
             for (uint32_t b = 0; b < nb; ++b) {
                 const Entry& e = ents[boff[b]];
                 n_full8 += (e.count != 1 || (entry8(e).y & kHead8Full)) ? 1u : 0u;
                 n_full16 += (entry16(e).w & kHead8Full) ? 1u : 0u;
+                n_full12 += (entry12(e).y & kHead8Full) ? 1u : 0u;
             }
             // 16-B heads when they make the deferring drain possible (full heads under 5%) and
-            // the 8-B heads do not (c4: 10% IUPAC primer bases)
+            // the 8-B heads do not (c4: 10% IUPAC primer bases); held in the 8-B IUPAC form when
+            // that keeps full heads under 5% too (MP_NO_H12=1: the 16-B form, for A/B runs)
             t->h16 = W >= 10 && n_full16 * 20 < (uint64_t)nb && n_full8 * 20 >= (uint64_t)nb;
-            if (t->h16) dents16.resize(std::max<uint32_t>(nb, 1));
+            t->h12 = t->h16 && n_full12 * 20 < (uint64_t)nb;
+            if (const char* e = std::getenv("MP_NO_H12"); e && std::atoi(e)) t->h12 = 0;
+            if (t->h16 && !t->h12) dents16.resize(std::max<uint32_t>(nb, 1));
+            std::vector<uint2> dents12;
+            if (t->h12) dents12.resize(std::max<uint32_t>(nb, 1));
             uint64_t n_full = 0;
             std::vector<uint32_t> rank_bucket(std::max<uint32_t>(nb, 1));
             for (uint32_t b = 0; b < nb; ++b) {
@@ -441,7 +464,13 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                     dents8[rank].y = kHead8Full | head8_filter(b);
                     if (!t->h16) ++n_full;
                 }
-                if (t->h16) {
+                if (t->h12) {
+                    dents12[rank] = entry12(e);
+                    if (dents12[rank].y & kHead8Full) {
+                        dents12[rank] = make_uint2(boff[b], kHead8Full | head8_filter(b));
+                        ++n_full;
+                    }
+                } else if (t->h16) {
                     dents16[rank] = entry16(e);
                     if (dents16[rank].w & kHead8Full) {
                         dents16[rank] = make_uint4(boff[b], 0u, 0u, kHead8Full | head8_filter(b));
@@ -569,6 +598,7 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                 }
             }
             filt.assign(1, 0);
+            if ((rc = upload(&t->dents12, dents12.data(), dents12.size(), &dev_bytes_pre))) break;
         } else {
             uint32_t lg = 6;
             while ((1ull << lg) < 2ull * nb) ++lg;
@@ -617,7 +647,7 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         t->planes_words = planes.size();
         pchars.resize(pchars.size() + 40, 0);  // chunk_ok reads 36 bytes from a 4-aligned offset
         if ((rc = upload(&t->pchars, pchars.data(), pchars.size(), &bytes))) break;
-        t->dev_bytes = bytes;
+        t->dev_bytes = bytes + dev_bytes_pre;
     } while (0);
     if (rc) {
         free_table(t);
