@@ -151,40 +151,81 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
     }
 }
 
+// One in-wave bitonic compare-exchange stage (j <= 32) on a lane's two keys: e0 at index
+// i0 = base + lane, e1 at i0 + 64; partners by shuffle, direction from bit k of the index.
+__device__ __forceinline__ uint64_t cx_lane(uint64_t e, uint32_t i, uint32_t j, uint32_t k) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)e, (int)j, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(e >> 32), (int)j, 64);
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    const bool up = (i & k) == 0, lower = (i & j) == 0;
+    return (lower == up) ? (e < o ? e : o) : (e > o ? e : o);
+}
+
 // The crowded buckets (kRankCap < keys <= kSortCap) of a mode-1 run, one per 1024-thread
-// workgroup (persistent over the list): bitonic sort of the bucket padded to a power of two
-// in LDS, one compare-exchange pair per thread and stage, then the decoded records in order.
+// workgroup (persistent over the list): bitonic sort of the bucket padded to a power of two.
+// Wave w holds keys [128 w, 128 w + 128) in registers, two per lane (i and i + 64): every
+// stage with j <= 64 is a register compare or a shuffle, and only the stages with j >= 128
+// (10 of the 66 for 2,048 keys) go through LDS with a barrier each.  (All 66 through LDS,
+// one barrier each: c4's crowded buckets took 109 us.)
 __global__ __launch_bounds__(1024) void crowded_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
                                                             unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
                                                             const uint64_t* __restrict__ seq_len, uint32_t n_seq,
                                                             const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
                                                             mp_hit* __restrict__ out, const uint32_t* __restrict__ crowded) {
     __shared__ uint64_t s_k[kSortCap];
+    static_assert(kSortCap == 2 * 1024, "two keys per thread of the 1024-thread workgroup");
     const uint32_t n = crowded[0];
+    const uint32_t lane = threadIdx.x & 63u, base = (threadIdx.x >> 6) * 128u;
+    const uint32_t i0 = base + lane, i1 = i0 + 64u;
     for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {  // block-uniform
         const uint32_t b = crowded[1 + c];
         const uint32_t start = off[b], m = off[b + 1] - start;
         uint32_t P = 2 * kRankCap;
         while (P < m) P <<= 1;
-        for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) s_k[i] = i < m ? keys[start + i] : ~0ull;
-        __syncthreads();
+        const bool on = base < P;  // wave-uniform: this wave holds keys of the padded bucket
+        uint64_t e0 = i0 < m ? keys[start + i0] : ~0ull, e1 = i1 < m ? keys[start + i1] : ~0ull;
         for (uint32_t k = 2; k <= P; k <<= 1) {
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t t = threadIdx.x; t < P / 2; t += blockDim.x) {
-                    const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));  // the pair's lower index (bit j clear)
-                    const uint32_t ij = i | j;
-                    const uint64_t x = s_k[i], y = s_k[ij];
-                    if ((x > y) == ((i & k) == 0)) {
-                        s_k[i] = y;
-                        s_k[ij] = x;
-                    }
+            if (k > 128u) {  // stages j >= 128 across waves, through LDS
+                if (on) {
+                    s_k[i0] = e0;
+                    s_k[i1] = e1;
                 }
                 __syncthreads();
+                for (uint32_t j = k >> 1; j >= 128u; j >>= 1) {
+                    for (uint32_t t = threadIdx.x; t < P / 2; t += blockDim.x) {
+                        const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));  // the pair's lower index
+                        const uint32_t ij = i | j;
+                        const uint64_t x = s_k[i], y = s_k[ij];
+                        if ((x > y) == ((i & k) == 0)) {
+                            s_k[i] = y;
+                            s_k[ij] = x;
+                        }
+                    }
+                    __syncthreads();
+                }
+                if (on) {
+                    e0 = s_k[i0];
+                    e1 = s_k[i1];
+                }
+                __syncthreads();  // every wave has read before the next k writes
+            }
+            if (on) {
+                if (k >= 128u) {  // j = 64: the lane's own two keys (i0 is the lower index)
+                    const bool up = (i0 & k) == 0;
+                    const uint64_t lo = e0 < e1 ? e0 : e1, hi = e0 < e1 ? e1 : e0;
+                    e0 = up ? lo : hi;
+                    e1 = up ? hi : lo;
+                }
+                for (uint32_t j = (k >> 1) < 32u ? (k >> 1) : 32u; j > 0; j >>= 1) {
+                    e0 = cx_lane(e0, i0, j, k);
+                    e1 = cx_lane(e1, i1, j, k);
+                }
             }
         }
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-            decode_hit(s_k[i], start + i, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
-        __syncthreads();  // s_k is refilled by the next bucket
+        if (on) {
+            if (i0 < m) decode_hit(e0, start + i0, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+            if (i1 < m) decode_hit(e1, start + i1, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+        }
     }
 }
 
