@@ -105,6 +105,9 @@ def test_split_seeds_vs_c_oracle(W, N):
         hits = eng.find_hits([FASTARecord(defline=">chrS", sequence=seq)])
         assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes(), split
         stats[split] = dict(eng.last_search_stats)
+        sp = eng.device_table().split()
+        assert sp["seed_tables"] == (2 if N else 1), sp
+        assert 0 < sp["rest_records"] < len(eng.sts_records) // 2, sp  # kinds 3-5 stay dense
     # the split scans count other candidates than the dense scan: the two paths really differ
     assert stats[True]["candidates"] != stats[False]["candidates"], stats
 
@@ -132,3 +135,16 @@ def test_split_sharded_ranges():
     parts = [s.fetch(s.run((a, b, ka, kb))) for (a, ka), (b, kb) in zip(cuts[:-1], cuts[1:])]
     assert len(whole) > 100
     assert np.array_equal(np.concatenate(parts), whole)
+
+
+@pytest.mark.parametrize("W,N,I", [(6, 1, 0), (8, 2, 0), (8, 1, 1), (10, 1, 0)])
+def test_no_split_outside_its_domain(W, N, I):
+    """W 7..9, I = 0, N <= 1 only: other tables keep their own scan (and say so)."""
+    sts_text, _ = _case(8, 1, 3)
+    eng = MerPCR(wordsize=W, mismatches=N, iupac_mode=I, margin=50)
+    with tempfile.TemporaryDirectory() as td:
+        p = f"{td}/x.sts"
+        with open(p, "w") as fh:
+            fh.write(sts_text)
+        assert eng.load_sts_file(p)
+    assert eng.device_table().split()["seed_tables"] == 0
