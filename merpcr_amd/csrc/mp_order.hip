@@ -354,7 +354,12 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
                        s->tmp_hi, off, P.nb, P.try_bits, P.low_bits,
                        g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->d_hcnt, sort_crowded(s));
     MP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(crowded_sort_decode, dim3((uint32_t)s->n_cu), dim3(1024), 0, st, s->tmp_hi, off, P.try_bits,
+    // crowded buckets: MP_CROWD_GRID workgroups (tuning; default one per CU)
+    static const uint32_t crowd_grid = [] {
+        const char* e = std::getenv("MP_CROWD_GRID");
+        return e ? (uint32_t)std::max(1, std::atoi(e)) : 0u;
+    }();
+    hipLaunchKernelGGL(crowded_sort_decode, dim3(crowd_grid ? crowd_grid : (uint32_t)s->n_cu), dim3(1024), 0, st, s->tmp_hi, off, P.try_bits,
                        P.low_bits, g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out,
                        sort_crowded(s));
     MP_HIP_CHECK(hipGetLastError());
