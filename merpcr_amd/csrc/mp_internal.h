@@ -402,6 +402,11 @@ __host__ __device__ __forceinline__ uint32_t lds_block_mask(uint32_t x, uint32_t
 constexpr uint32_t kKgrpKeys = 16;
 constexpr uint32_t kKgrpFields = 3;
 constexpr uint32_t kKgrpFlag = 0x8000u;
+// A field of a key with exactly two records, both seeded at their primer start and plain over
+// bases W..W+2 (round 3): kKgrpPair, then each record's bases W..W+2 (record 0 in bits 11..6).
+// The window passes when either record is within N of them.  Without it every seed of such a
+// key went to tail_kernel: c3's ~5k two-record keys gave most of its 3.4M bucket-tail references.
+constexpr uint32_t kKgrpPair = 0x4000u;
 constexpr uint32_t kKgrpWildFields = 2;  // I = 1 key groups: two 24-bit fields {codes, wild bases}
 
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {

@@ -1394,7 +1394,13 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
     const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
     if (j >= kKgrpFields) return true;
     const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
-    if (!(field & kKgrpFlag)) return true;
+    if (!(field & kKgrpFlag)) {
+        if (!(field & kKgrpPair)) return true;
+        // two records: the window's bases W..W+2 (the top 3 of its F) against each record's
+        const uint32_t g3 = (pk >> (4u + 2u * (a.kgrp_F - 3u))) & 63u;
+        const uint32_t x0 = g3 ^ ((field >> 6) & 63u), x1 = g3 ^ (field & 63u);
+        return __popc((x0 | (x0 >> 1)) & 0x15u) <= a.N || __popc((x1 | (x1 >> 1)) & 0x15u) <= a.N;
+    }
     const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
     return __popc((x | (x >> 1)) & 0x55555555u) <= a.N;
 }

@@ -590,8 +590,20 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                         const uint2 h = dents8[rank];
                         // compact head (single record, seeded at its primer start, plain, <= W + 16
                         // bases) carrying at least F bases after the seed
-                        if (!(h.y & kHead8Full) && ((h.y >> kHead8RecBits) & 31u) >= F)
+                        if (!(h.y & kHead8Full) && ((h.y >> kHead8RecBits) & 31u) >= F) {
                             w |= (uint64_t)(kKgrpFlag | (h.x >> (32u - 2u * F))) << (16u + 16u * j);
+                        } else if (F >= 3 && bcount[rank_bucket[rank]] == 2) {  // kKgrpPair
+                            const uint32_t b = rank_bucket[rank];
+                            const uint64_t m3 = sp_lt((int)W + 3) & ~sp_lt((int)W);
+                            uint32_t f = kKgrpPair;
+                            bool ok = true;
+                            for (uint32_t r = 0; r < 2; ++r) {
+                                const Entry& e = ents[boff[b] + r];
+                                ok = ok && e.hash_off == 0 && e.l1 >= W + 3 && (e.pmask & m3) == m3 && ((e.pmask >> 1) & m3) == 0;
+                                f |= (uint32_t)((e.code << (2 * W)) >> 58) << (6 * (1 - r));
+                            }
+                            if (ok) w |= (uint64_t)f << (16u + 16u * j);
+                        }
                         ++j;
                     }
                     kgrp[g] = w;
