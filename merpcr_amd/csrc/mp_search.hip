@@ -1377,7 +1377,17 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
         if (j >= kKgrpFields) return true;
         const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
-        if (!(field & kKgrpFlag)) return true;
+        if (!(field & kKgrpFlag)) {
+            if (!(field & kKgrpPair)) return true;
+            // two records (gap_len <= 3): either record's gap differs in 1..N positions, or the
+            // window's gap holds an invalid base
+            if (pk >> 31) return true;
+            const uint32_t gm = (1u << (2u * a.gap_len)) - 1u;
+            const uint32_t g = (pk >> (4u + 2u * a.gap_post)) & gm;
+            const uint32_t x0 = g ^ ((field >> 6) & gm), x1 = g ^ (field & gm);
+            const uint32_t m0 = (uint32_t)__popc((x0 | (x0 >> 1)) & 0x555u), m1 = (uint32_t)__popc((x1 | (x1 >> 1)) & 0x555u);
+            return (m0 >= 1u && m0 <= (uint32_t)a.N) || (m1 >= 1u && m1 <= (uint32_t)a.N);
+        }
         const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
         const uint32_t m = (x | (x >> 1)) & 0x55555555u;
         return (uint32_t)__popc(m) <= (uint32_t)a.N && ((m >> (2u * a.gap_post)) != 0u || (pk >> 31) != 0u);

@@ -514,6 +514,16 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                             const uint32_t gb = (uint32_t)((e.code << (2 * gap_at)) >> (64 - 2 * gap_len));
                             const uint32_t pb = gap_post ? (uint32_t)((e.code << (2 * post_at)) >> (64 - 2 * gap_post)) : 0u;
                             w |= (uint64_t)(kKgrpFlag | (gb << (2 * gap_post)) | pb) << (16u + 16u * j);
+                        } else if (bcount[b] == 2 && gap_len <= 3) {  // kKgrpPair: each record's gap bases
+                            const uint64_t am = sp_lt((int)(gap_at + gap_len)) & ~sp_lt((int)gap_at);
+                            uint32_t f = kKgrpPair;
+                            bool ok = true;
+                            for (uint32_t r = 0; r < 2; ++r) {
+                                const Entry& er = ents[boff[b] + r];
+                                ok = ok && er.hash_off == 0 && (er.pmask & am) == am && ((er.pmask >> 1) & am) == 0;
+                                f |= (uint32_t)((er.code << (2 * gap_at)) >> (64 - 2 * gap_len)) << (6 * (1 - r));
+                            }
+                            if (ok) w |= (uint64_t)f << (16u + 16u * j);
                         }
                         ++j;
                     }
