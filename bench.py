@@ -476,6 +476,20 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     timed_scan_ms = list(scan_ms)
+    # single-search latency beside the pipelined step: handle 0 alone, each run enqueued only
+    # after the previous one completed (host turnaround included, no events), median of 5
+    single_ms = None
+    if world == 1:
+        torch.cuda.synchronize()
+        search.set_scan_timing(False)
+        search.set_stage_timing(False)
+        lat = []
+        for _ in range(5):
+            t1 = time.perf_counter()
+            search.enqueue(rng, stream)
+            search.complete()
+            lat.append(time.perf_counter() - t1)
+        single_ms = float(np.median(lat)) * 1e3
     # untimed: three more steps of handle 0 alone (the scan time when the timed steps carried
     # no events), the last with every stage timed (the stage breakdown)
     torch.cuda.synchronize()
@@ -549,6 +563,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(t_step * 1e3, 3),
+        "single_run_ms": round(single_ms, 3) if single_ms is not None else None,
         "higher_is_better": True,
         "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
@@ -577,6 +592,8 @@ def main():
                      "alg_bytes_per_launch": int(alg_bytes),
                      "issue": (dict(issue_bound(pmc), source=f"profiles/{pmc_tag}_pmc.json") if pmc else None)},
         "setup_s": round(setup_s, 2),
+        "single_run_note": "one isolated search (enqueue -> complete, host turnaround included) on one handle, "
+                           "median of 5 after the timed steps; ms_per_step is the pipelined throughput",
         "pipeline": (f"{nbuf} search handles on {'one stream' if args.one_stream else f'{nbuf} streams'}: step i+1 "
                      "enqueued before the host waits for step i (mp_search_enqueue/complete)"
                      if nbuf > 1 else "none: each step waits for the previous"),

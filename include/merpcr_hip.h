@@ -181,6 +181,9 @@ int mp_search_last_stats(void* search, float* scan_ms, uint64_t* n_windows, uint
 /* List regrowths (a run whose survivor, tail or hit list overflowed and was rerun)
  * over the handle's life. */
 int mp_search_regrowths(void* search, uint64_t* n_regrowths);
+/* Device bytes the handle holds: hit, survivor and tail lists, sort buffers and the
+ * order-mode-0 bucket slots (which grow with the hit capacity's bucket plan). */
+int mp_search_dev_bytes(void* search, uint64_t* dev_bytes);
 /* Seeds whose primer-1 fingerprint could not reject them (pair-checked). */
 int mp_search_survivors(void* search, uint64_t* n_survivors);
 /* Last run's stage times (HIP events on the run's stream): seed scan kernel alone,

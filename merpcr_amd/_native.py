@@ -33,7 +33,7 @@ EXPORTS = (
     "mp_genome_stats", "mp_genome_download", "mp_genome_reset", "mp_genome_destroy",
     "mp_search_create", "mp_search_set_options", "mp_search_set_stage_timing", "mp_search_set_scan_timing", "mp_search_run",
     "mp_search_enqueue", "mp_search_complete", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
-    "mp_search_last_stats", "mp_search_regrowths", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
+    "mp_search_last_stats", "mp_search_regrowths", "mp_search_dev_bytes", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
     "mp_multi_create", "mp_multi_genome", "mp_multi_put", "mp_multi_seal", "mp_multi_run", "mp_multi_fetch",
     "mp_multi_device_search", "mp_multi_destroy",
     "mp_comm_unique_id", "mp_comm_create", "mp_comm_gather_hits", "mp_comm_destroy",
@@ -105,6 +105,7 @@ def _sig(lib):
     lib.mp_search_enqueue.argtypes = [P, POINTER(MPRange), P]
     lib.mp_search_complete.argtypes = [P, u64p]
     lib.mp_search_regrowths.argtypes = [P, u64p]
+    lib.mp_search_dev_bytes.argtypes = [P, u64p]
     lib.mp_search_fetch.argtypes = [P, P, c_uint64, P]
     lib.mp_search_fetch_device.argtypes = [P, P, c_uint64, P]
     lib.mp_search_device_hits.argtypes = [P, POINTER(c_void_p)]
@@ -340,6 +341,12 @@ class Search:
     def regrowths(self) -> int:
         n = c_uint64()
         check(lib().mp_search_regrowths(self._h, ctypes.byref(n)))
+        return n.value
+
+    def dev_bytes(self) -> int:
+        """Device bytes of the handle's lists, sort buffers and order slots."""
+        n = c_uint64()
+        check(lib().mp_search_dev_bytes(self._h, ctypes.byref(n)))
         return n.value
 
     def run(self, rng=None, stream=None) -> int:

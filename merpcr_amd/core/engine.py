@@ -188,6 +188,34 @@ class _NativeRecords:
 class MerPCR:
     """Electronic-PCR STS search (reference: core/engine.py:44)."""
 
+    # sts_records / sts_table: the reference's public containers (engine.py:62-63).  A
+    # natively parsed file keeps them lazy (_LazyRecords / _LazyTable) only for the engine's
+    # own paths, which read the parser's arrays; a caller that reaches either container gets
+    # it fully built, so C-level readers (json, numpy, str.join, PyDict_Next) see every item.
+    # From then on the records may be edited in place, and the engine rebuilds its arrays
+    # from the record objects (_native_current() is False).
+    @property
+    def sts_records(self) -> List[STSRecord]:
+        recs = self._recs
+        if isinstance(recs, _LazyRecords):
+            recs._ready()
+        return recs
+
+    @sts_records.setter
+    def sts_records(self, v):
+        self._recs = v
+
+    @property
+    def sts_table(self) -> Dict[int, List[STSRecord]]:
+        tab = self._table
+        if isinstance(tab, _LazyTable):
+            tab._ready()
+        return tab
+
+    @sts_table.setter
+    def sts_table(self, v):
+        self._table = v
+
     def __init__(self, wordsize: int = DEFAULT_WORDSIZE, margin: int = DEFAULT_MARGIN,
                  mismatches: int = DEFAULT_MISMATCHES,
                  three_prime_match: int = DEFAULT_THREE_PRIME_MATCH,
@@ -220,6 +248,7 @@ class MerPCR:
         self.max_pcr_size = 0
         self.total_hits = 0
         self._sts_keys: List[int] = []
+        self._sts_keys_p1: List[str] = []
         self._dev_table = None
         self._dev_table_sig = None
         self._codes = CharCodes()
@@ -276,6 +305,7 @@ class MerPCR:
         self.sts_records = []
         self.sts_table = {}
         self._sts_keys = []
+        self._sts_keys_p1 = []
         self.max_pcr_size = 0
         self._dev_table = None
         self._native_arrays = None
@@ -296,12 +326,12 @@ class MerPCR:
         # the record objects are built lazily (_LazyRecords): the search path reads the arrays
         src = _NativeRecords(r)
         src._blob = (r["rec_text"], r["rec_text_off"])
-        src.recs = self.sts_records = _LazyRecords(src, n)
-        src.table = self.sts_table = _LazyTable(src)
+        src.recs = self._recs = _LazyRecords(src, n)
+        src.table = self._table = _LazyTable(src)
         self._sts_src = src
         self._sts_keys = r["key"].tolist()
         self.max_pcr_size = r["max_pcr_size"]
-        self._native_arrays = (self.sts_records, n, (r["key"], r["hash_off"], r["pcr_size"], r["p1"], r["p1_off"],
+        self._native_arrays = (self._recs, n, (r["key"], r["hash_off"], r["pcr_size"], r["p1"], r["p1_off"],
                                                      r["p2"], r["p2_off"]))
         if r["status"] == _native.MP_STS_BAD_LINE:
             logger.error(f"Bad STS file format at line {r['bad_line']}. Expected at least 4 fields.")
@@ -389,6 +419,7 @@ class MerPCR:
         self.sts_table.setdefault(hash_value, []).append(sts)
         self.sts_records.append(sts)
         self._sts_keys.append(hash_value)
+        self._sts_keys_p1.append(sts.primer1)
 
     def _hash_value(self, primer: str) -> Tuple[int, int]:
         """(offset, value) of the first all-ACGTU W-mer (engine.py:331-355).
@@ -463,25 +494,37 @@ class MerPCR:
 
     def _n_records(self) -> int:
         """len(sts_records), without building a lazy list's records."""
-        recs = self.sts_records
+        recs = self._recs
         n = recs.native_len() if isinstance(recs, _LazyRecords) else None
         return len(recs) if n is None else n
 
     def _native_current(self) -> bool:
-        """sts_records is still exactly what the native parser produced."""
+        """sts_records is the native parser's and has never been handed out: no caller can
+        have edited it (nor a record in it), so the parser's arrays and texts are current."""
         na = getattr(self, "_native_arrays", None)
-        recs = self.sts_records
-        return (na is not None and na[0] is recs and isinstance(recs, _LazyRecords) and not recs._mutated
+        recs = self._recs
+        return (na is not None and na[0] is recs and isinstance(recs, _LazyRecords) and recs._src is not None
                 and recs.native_len() == na[1])
+
+    def _records_sig(self):
+        """What the device table and the formatter's record column depend on: the parser's
+        arrays while they are current, else the records' content (edits in place included)."""
+        if self._native_current():
+            return ("native", id(self._recs))
+        return ("objects", hash(tuple((r.id, r.alias, r.direct, r.primer1, r.primer2, r.pcr_size, r.hash_offset)
+                                      for r in self._recs)))
 
     def _table_arrays(self):
         """Record arrays for mp_table_create in sts_records order."""
-        recs = self.sts_records
+        recs = self._recs
         na = getattr(self, "_native_arrays", None)
         if self._native_current():
             return na[2]
-        if len(self._sts_keys) != len(recs):
-            self._sts_keys = [self._hash_value(r.primer1)[1] for r in recs]
+        p1s = [r.primer1 for r in recs]
+        if getattr(self, "_sts_keys_p1", None) != p1s or len(self._sts_keys) != len(recs):
+            # the loader's keys, unless a primer was edited since (or records were added)
+            self._sts_keys = [self._hash_value(p)[1] for p in p1s]
+        self._sts_keys_p1 = p1s
         key = np.asarray(self._sts_keys, dtype=np.uint32)
         hash_off = np.fromiter((r.hash_offset for r in recs), dtype=np.uint32, count=len(recs))
         size = np.fromiter((r.pcr_size for r in recs), dtype=np.uint64, count=len(recs))
@@ -498,7 +541,7 @@ class MerPCR:
     def device_table(self):
         """The seed table resident on this engine's GPU (rebuilt when stale)."""
         from .. import _native
-        sig = (id(self.sts_records), self._n_records(), self._native_current(), self.wordsize, self.margin,
+        sig = (self._records_sig(), self._n_records(), self.wordsize, self.margin,
                self.mismatches, self.three_prime_match, self.iupac_mode, self.device)
         if self._dev_table is None or self._dev_table_sig != sig:
             self._dev_table = _native.Table(self._params(), self.device, *self._table_arrays())
@@ -684,18 +727,13 @@ class MerPCR:
 
     def _record_texts(self):
         """The formatter's record column (UTF-8 "id\talias\t(direct)" per record, and
-        offsets), cached until sts_records changes: from the parser's bytes while the records
-        are the native parser's, else from the record objects."""
+        offsets): from the parser's bytes while the records are the native parser's and
+        unseen by callers, else from the record objects."""
         if self._native_current():
             return self._sts_src.record_texts()
-        recs = self.sts_records
-        key = (id(recs), len(recs))
-        cache = getattr(self, "_rec_text_cache", None)
-        if cache is None or cache[0] != key or cache[1] is not recs:
-            from .._native import _csr
-            cache = (key, recs, _csr([f"{r.id}\t{r.alias}\t({r.direct})" for r in recs]))
-            self._rec_text_cache = cache
-        return cache[2]
+        from .._native import _csr
+        # rebuilt on every call from the current record objects, as engine.py:437-443 reads them
+        return _csr([f"{r.id}\t{r.alias}\t({r.direct})" for r in self._recs])
 
     def format_hits(self, fasta_records: Sequence[FASTARecord], hits: np.ndarray) -> List[str]:
         """Output lines exactly as engine.py:437-443 prints them."""

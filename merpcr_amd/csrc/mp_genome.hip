@@ -341,6 +341,7 @@ MP_EXPORT int mp_genome_create(int32_t device, uint32_t n_seq, const uint64_t* s
 MP_EXPORT int mp_genome_reset(void* genome, uint32_t n_seq, const uint64_t* seq_len) {
     Genome* g = (Genome*)genome;
     if (!g || (n_seq && !seq_len)) return fail(MP_E_ARG, "mp_genome_reset: null pointer");
+    if (g->n_pending) return fail(MP_E_STATE, "mp_genome_reset: a search run over this genome is enqueued");
     MP_HIP_CHECK(hipSetDevice(g->device));
     int rc = layout(g, n_seq, seq_len);
     if (!rc) rc = place(g);
@@ -351,6 +352,7 @@ MP_EXPORT int mp_genome_put_device(void* genome, uint32_t seq, uint64_t offset, 
                                    uint64_t nbytes, void* stream) {
     Genome* g = (Genome*)genome;
     if (!g || (nbytes && !dev_bytes)) return fail(MP_E_ARG, "mp_genome_put_device: null pointer");
+    if (g->n_pending) return fail(MP_E_STATE, "mp_genome_put_device: a search run over this genome is enqueued");
     MP_HIP_CHECK(hipSetDevice(g->device));
     return put_device_bytes(g, seq, offset, dev_bytes, nbytes, (hipStream_t)stream);
 }
@@ -359,6 +361,7 @@ MP_EXPORT int mp_genome_put(void* genome, uint32_t seq, uint64_t offset, const u
                             uint64_t nbytes, void* stream) {
     Genome* g = (Genome*)genome;
     if (!g || (nbytes && !host_bytes)) return fail(MP_E_ARG, "mp_genome_put: null pointer");
+    if (g->n_pending) return fail(MP_E_STATE, "mp_genome_put: a search run over this genome is enqueued");
     MP_HIP_CHECK(hipSetDevice(g->device));
     hipStream_t st = (hipStream_t)stream;
     const uint64_t piece = 256ull << 20;  // staging granularity (multiple of 64)
@@ -379,6 +382,7 @@ MP_EXPORT int mp_genome_put(void* genome, uint32_t seq, uint64_t offset, const u
 MP_EXPORT int mp_genome_seal(void* genome, void* stream) {
     Genome* g = (Genome*)genome;
     if (!g) return fail(MP_E_ARG, "mp_genome_seal: null genome");
+    if (g->n_pending) return fail(MP_E_STATE, "mp_genome_seal: a search run over this genome is enqueued");
     MP_HIP_CHECK(hipSetDevice(g->device));
     hipStream_t st = (hipStream_t)stream;
     int rc = sort_runs(g, st);

@@ -207,6 +207,7 @@ struct Genome {
     uint64_t dev_bytes = 0;
     uint64_t plane_cap = 0;   // padded bases the planes hold
     uint32_t seq_cap = 0;     // sequences d_base / d_len hold
+    uint32_t n_pending = 0;   // search runs enqueued over this genome and not yet completed
 };
 
 struct Search {

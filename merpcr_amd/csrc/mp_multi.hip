@@ -368,7 +368,9 @@ MP_EXPORT int mp_comm_gather_hits(void* comm, void* search, uint32_t seq_shift, 
     // pinned staging and a polled event: the counts exchange is on every step's critical path
     uint64_t* mine = c->h_meta;
     const uint64_t* meta = c->h_meta + 3;
-    mine[0] = s->n_hits;
+    // a rank whose run is still enqueued (hit list being written) sends the marker ~0: every
+    // rank then leaves with MP_E_STATE after the counts exchange, so no rank waits on it
+    mine[0] = s->pending ? ~0ull : s->n_hits;
     mine[1] = seq_shift;
     mine[2] = cap;
     MP_HIP_CHECK(hipMemcpyAsync(c->d_meta + (size_t)c->rank * 3, mine, 3 * sizeof(uint64_t), hipMemcpyHostToDevice, st));
@@ -383,6 +385,9 @@ MP_EXPORT int mp_comm_gather_hits(void* comm, void* search, uint32_t seq_shift, 
         MP_HIP_CHECK(e);
     }
     uint64_t total = 0;
+    for (int r = 0; r < c->nranks; ++r)
+        if (meta[(size_t)r * 3] == ~0ull)
+            return fail(MP_E_STATE, "mp_comm_gather_hits: a rank's search run is enqueued (mp_search_complete first)");
     for (int r = 0; r < c->nranks; ++r) total += meta[(size_t)r * 3];
     *n_total = total;
     if (total > meta[2]) return fail(MP_E_CAP, "mp_comm_gather_hits: rank 0 buffer too small");

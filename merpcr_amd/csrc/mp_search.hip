@@ -1224,6 +1224,13 @@ __device__ __forceinline__ uint32_t bit_range(int lo, int hi) {
     return a & ~b;
 }
 
+// Windows pb .. pb + 31 of a lane that lie in the span's [p_lo, p_hi).  Both differences in
+// 64 bits, clamped before the narrowing: a lane deep in a record (pb >= 2^31) of a span that
+// starts at 0 gave (int)p_lo - (int)pb > 0 in 32-bit arithmetic and masked every window.
+__device__ __forceinline__ uint32_t span_bits(const SeqSpan& sp, uint32_t pb) {
+    return bit_range((int)smax64((int64_t)sp.p_lo - (int64_t)pb, -1), (int)smin64((int64_t)sp.p_hi - (int64_t)pb, 32));
+}
+
 // W-mer at window i of a lane: top 2W bits of the 32-bit big-endian funnel at bit 2i of
 // (d0, d1, d2), the lane's 48 bases; i is a compile-time constant after unrolling.
 template <int I>
@@ -1592,7 +1599,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint32_t okm = (kGap ? window_ok_mask(R.iv, a.gap_at) &
                                          window_ok_mask(R.iv << (a.gap_at + a.gap_len), W - a.gap_at)
                                    : window_ok_mask(R.iv, W)) &
-                             bit_range((int)sp.p_lo - (int)pb, (int)smin64((int64_t)sp.p_hi - pb, 32));
+                             span_bits(sp, pb);
         const uint64_t nx = sch.next(ss, n_supers, lane);
         (void)stride;
         if constexpr (kMode == 1) {
@@ -1951,7 +1958,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         const uint32_t pb = base + (uint32_t)lane * kLanePos;
         const uint32_t d0 = (uint32_t)(w0 >> 32), d1 = (uint32_t)w0, d2 = (uint32_t)(w1 >> 32);
         const uint32_t okm = window_ok_mask(iv, W) &
-                             bit_range((int)sp.p_lo - (int)pb, (int)smin64((int64_t)sp.p_hi - pb, 32));
+                             span_bits(sp, pb);
         // I=1: a window with a non-A/C/G/T/U base among its first 16 sends all its records
         // to the full test (a genome IUPAC base may match where the 2-bit compare says
         // otherwise; under I=0 such a base reads as 'A' and can only hide a mismatch, and U
@@ -2314,6 +2321,11 @@ __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* _
 
 static void free_search(Search* s) {
     if (!s) return;
+    if (s->pending) {  // a run still owns the buffers: let it drain before they are freed
+        if (!s->pend_empty && s->evd) (void)hipEventSynchronize(s->evd);
+        s->pending = false;
+        if (s->genome && s->genome->n_pending) --s->genome->n_pending;
+    }
     hipFree(s->keys); hipFree(s->tmp_hi); hipFree(s->tmp_lo); hipFree(s->out); hipFree(s->sort_tmp);
     hipFree(s->counters); hipFree(s->spans); hipFree(s->bucket);
     hipFree(s->surv);
@@ -2662,6 +2674,20 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     return MP_OK;
 }
 
+// The order mode of the next run: keys over 64 bits (or a forced rocPRIM sort) take 2; the
+// handle's sticky mode otherwise, except that mode 0's bucket slots (kSlotCap keys per
+// bucket) are skipped once the planned mean bucket at the hit capacity is past kSlotCap / 4:
+// such runs would overflow a slot and redo their order in mode 1 anyway.
+static int run_order_mode(const Search* s) {
+    if (!sort_hits_device_ok(s)) return 2;
+    int m = s->order_mode;
+    if (m == 0) {
+        const SortPlan P = sort_plan(s);
+        if (s->cap / P.nb > kSlotCap / 4) m = 1;
+    }
+    return m;
+}
+
 // Wait for the enqueued run and read its counters (written by finish_kernel).
 static int wait_counts(Search* s, unsigned long long* cnt) {
     MP_HIP_CHECK(poll_event(s->evd));
@@ -2671,11 +2697,14 @@ static int wait_counts(Search* s, unsigned long long* cnt) {
 
 // The run's order again, synchronously, one mode up (a bucket overflowed in `from`); raises
 // the handle's sticky mode.  The linear keys (tmp_lo; hi/lo for rocPRIM) are intact.
-static int redo_order(Search* s, hipStream_t st, int from, uint64_t nh) {
+// The sticky mode rises only when a device order overflowed (raise): a run that took mode 2
+// because its key was wider than 64 bits leaves the handle's mode alone, so a later genome
+// whose key fits goes back to the device order.
+static int redo_order(Search* s, hipStream_t st, int from, uint64_t nh, bool raise) {
     Genome* g = s->genome;
     Table* t = s->table;
     for (int mode = from + 1; mode <= 2; ++mode) {
-        s->order_mode = std::max(s->order_mode, mode);
+        if (raise) s->order_mode = std::max(s->order_mode, mode);
         if (mode == 1) {
             // the bucket counts and keys are intact; the offsets again (no finish: the host
             // words hold this run's counters), then scatter and sort; an overflow shows in
@@ -2728,7 +2757,7 @@ static int search_complete(Search* s, uint64_t* n_hits) {
             const uint64_t mx = cnt[kHitMaxRegion];
             rc = alloc_hits(s, kHitRegions * (mx + mx / 4 + 1024));
         }
-        mode = sort_hits_device_ok(s) ? s->order_mode : 2;
+        mode = run_order_mode(s);
         if (!rc) rc = set_lists(s, a, mode);
         if (!rc) rc = enqueue_kernels(s, a, s->pend_tiles, st, mode);
         if (!rc) rc = wait_counts(s, cnt);
@@ -2743,7 +2772,7 @@ static int search_complete(Search* s, uint64_t* n_hits) {
     s->n_survivors = cnt[3];
     const uint64_t nh = cnt[0];
     if (mode == 2 || cnt[kSortOverflow]) {  // the device order did not hold this run's keys
-        rc = redo_order(s, st, mode == 2 ? 1 : mode, nh);
+        rc = redo_order(s, st, mode == 2 ? 1 : mode, nh, cnt[kSortOverflow] != 0);
         if (rc) return rc;
     }
     if (!s->stage_timing) s->tail_ms = s->pair_ms = s->order_ms = -1.f;  // not measured
@@ -2814,6 +2843,7 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
     s->pend_tiles = tiles;
     s->pend_empty = tiles == 0;
     s->pending = true;
+    ++g->n_pending;
     if (!tiles) return MP_OK;
     const uint32_t n_real_spans = (uint32_t)spans.size();
     {
@@ -2863,13 +2893,14 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         a.g_lo = g_lo; a.g_hi = g_hi;
         a.sched_short = s->sched_short;
         // keys over 64 bits, or a forced rocPRIM sort: mode 2
-        const int mode = sort_hits_device_ok(s) ? s->order_mode : 2;
+        const int mode = run_order_mode(s);
         s->pend_mode = mode;
         rc = set_lists(s, a, mode);
         if (!rc) rc = enqueue_kernels(s, a, tiles, st, mode);
     } while (0);
     if (rc) {
         s->pending = false;
+        --g->n_pending;
         s->dirty = true;
     }
     return rc;
@@ -2882,6 +2913,7 @@ MP_EXPORT int mp_search_complete(void* search, uint64_t* n_hits) {
     MP_HIP_CHECK(hipSetDevice(s->genome->device));
     if (n_hits) *n_hits = 0;
     s->pending = false;
+    if (s->genome->n_pending) --s->genome->n_pending;
     if (s->pend_empty) return MP_OK;
     const int rc = search_complete(s, n_hits);
     if (rc) s->dirty = true;
@@ -2897,6 +2929,7 @@ MP_EXPORT int mp_search_run(void* search, const mp_range* range, void* stream, u
 MP_EXPORT int mp_search_fetch(void* search, mp_hit* out, uint64_t cap, void* stream) {
     Search* s = (Search*)search;
     if (!s || (s->n_hits && !out)) return fail(MP_E_ARG, "mp_search_fetch: null pointer");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_fetch: a run is enqueued (mp_search_complete first)");
     if (cap < s->n_hits) return fail(MP_E_CAP, "mp_search_fetch: output buffer too small");
     if (!s->n_hits) return MP_OK;
     MP_HIP_CHECK(hipSetDevice(s->genome->device));
@@ -2909,6 +2942,7 @@ MP_EXPORT int mp_search_fetch(void* search, mp_hit* out, uint64_t cap, void* str
 MP_EXPORT int mp_search_fetch_device(void* search, mp_hit* dev_out, uint64_t cap, void* stream) {
     Search* s = (Search*)search;
     if (!s || (s->n_hits && !dev_out)) return fail(MP_E_ARG, "mp_search_fetch_device: null pointer");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_fetch_device: a run is enqueued (mp_search_complete first)");
     if (cap < s->n_hits) return fail(MP_E_CAP, "mp_search_fetch_device: output buffer too small");
     if (!s->n_hits) return MP_OK;
     MP_HIP_CHECK(hipSetDevice(s->genome->device));
@@ -2920,6 +2954,7 @@ MP_EXPORT int mp_search_fetch_device(void* search, mp_hit* dev_out, uint64_t cap
 MP_EXPORT int mp_search_device_hits(void* search, const mp_hit** dev_hits) {
     Search* s = (Search*)search;
     if (!s || !dev_hits) return fail(MP_E_ARG, "mp_search_device_hits: null pointer");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_device_hits: a run is enqueued (mp_search_complete first)");
     *dev_hits = s->out;
     return MP_OK;
 }
@@ -2927,9 +2962,18 @@ MP_EXPORT int mp_search_device_hits(void* search, const mp_hit** dev_hits) {
 MP_EXPORT int mp_search_last_stats(void* search, float* scan_ms, uint64_t* n_windows, uint64_t* n_candidates) {
     Search* s = (Search*)search;
     if (!s) return fail(MP_E_ARG, "mp_search_last_stats: null search");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_last_stats: a run is enqueued (mp_search_complete first)");
     if (scan_ms) *scan_ms = s->scan_ms;
     if (n_windows) *n_windows = s->n_windows;
     if (n_candidates) *n_candidates = s->n_candidates;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_search_dev_bytes(void* search, uint64_t* dev_bytes) {
+    Search* s = (Search*)search;
+    if (!s || !dev_bytes) return fail(MP_E_ARG, "mp_search_dev_bytes: null pointer");
+    *dev_bytes = s->cap * (16 + 8 + 8 + sizeof(mp_hit)) + s->surv_cap * sizeof(uint4) + s->tails_cap * 2 * sizeof(uint4) +
+                 s->spans_cap * sizeof(SeqSpan) + s->slots_bytes + s->sort_tmp_bytes + kCounterBytes;
     return MP_OK;
 }
 
@@ -2943,6 +2987,7 @@ MP_EXPORT int mp_search_regrowths(void* search, uint64_t* n_regrowths) {
 MP_EXPORT int mp_search_survivors(void* search, uint64_t* n_survivors) {
     Search* s = (Search*)search;
     if (!s || !n_survivors) return fail(MP_E_ARG, "mp_search_survivors: null pointer");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_survivors: a run is enqueued (mp_search_complete first)");
     *n_survivors = s->n_survivors;
     return MP_OK;
 }
@@ -2950,6 +2995,7 @@ MP_EXPORT int mp_search_survivors(void* search, uint64_t* n_survivors) {
 MP_EXPORT int mp_search_timing(void* search, float* scan_ms, float* tail_ms, float* pair_ms, float* order_ms) {
     Search* s = (Search*)search;
     if (!s) return fail(MP_E_ARG, "mp_search_timing: null search");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_timing: a run is enqueued (mp_search_complete first)");
     if (scan_ms) *scan_ms = s->scan_ms;
     if (tail_ms) *tail_ms = s->tail_ms;
     if (pair_ms) *pair_ms = s->pair_ms;

@@ -146,10 +146,17 @@ def amplicons(sts: STSSet, total: int, seed: int, N: int, M: int, W: int):
 
 
 def build_genome_torch(total: int, records: int, sts: Optional[STSSet], seed: int, N: int, M: int, W: int,
-                       nrun: float, device):
-    """(names, lengths, uint8 device buffer with records at 64-aligned offsets, offsets)."""
+                       nrun: float, device, lens: Optional[List[int]] = None):
+    """(names, lengths, uint8 device buffer with records at 64-aligned offsets, offsets).
+
+    `lens` overrides the human-like layout (record lengths summing to `total`)."""
     import torch
-    names, lens = layout(total, records)
+    if lens is None:
+        names, lens = layout(total, records)
+    else:
+        lens = [int(x) for x in lens]
+        assert sum(lens) == total and len(lens) == records, (lens, total, records)
+        names = [f"rec{i}" for i in range(records)]
     offs = np.zeros(len(lens), dtype=np.int64)
     pos = 0
     for i, n in enumerate(lens):
@@ -220,3 +227,28 @@ def build_genome_torch(total: int, records: int, sts: Optional[STSSet], seed: in
     is_upper = (lower >= 65) & (lower <= 90)
     blk[mask] = torch.where(is_upper, lower + 32, lower)
     return names, lens, buf, offs, planted
+
+
+def plant_at_ends(buf, offs, lens, sts: STSSet, seed: int = 5, per_record: int = 3) -> int:
+    """Overwrite the last bases of every record with `per_record` exact '+' amplicons of
+    random STS: the last one ends on the record's final base, the others a few hundred
+    bases before it.  Returns the number planted (plumbing for the record-end tests)."""
+    import torch
+    rng = np.random.default_rng(seed)
+    n = 0
+    for r, ln in enumerate(lens):
+        end = int(ln)
+        for _ in range(per_record):
+            i = int(rng.integers(0, len(sts.ids)))
+            a, b, size = sts.p1[i], sts.p2[i], int(sts.size[i])
+            a, b = _concrete(rng, a), _concrete(rng, b)
+            fill = _ACGT[rng.integers(0, 4, max(0, size - len(a) - len(b)))].tobytes()
+            amp = a + fill + b
+            start = end - len(amp)
+            if start < 0:
+                break
+            o = int(offs[r]) + start
+            buf[o:o + len(amp)] = torch.from_numpy(np.frombuffer(amp, dtype=np.uint8).copy()).to(buf.device)
+            n += 1
+            end = start - int(rng.integers(1, 200))
+    return n

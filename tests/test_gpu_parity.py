@@ -14,7 +14,7 @@ import tempfile
 import numpy as np
 import pytest
 
-from merpcr_amd import FASTARecord, MerPCR
+from merpcr_amd import FASTARecord, MerPCR, _native
 from oracle import epcr_oracle as O
 from tests.golden_io import data_path, load_golden
 
@@ -437,6 +437,37 @@ def test_forced_regrowth_is_identical():
         assert _device_lines(eng, recs) == exp, opts
         assert eng.last_search_stats["regrowths"] >= 1, opts
     assert len(exp) > 100
+
+
+def test_pending_run_guards():
+    """Between mp_search_enqueue and mp_search_complete the run owns the handle's lists:
+    fetch, stats and the genome's writers fail with MP_E_STATE instead of reading a list
+    being written; complete then returns the same hits; destroying a handle with a run
+    still enqueued waits for it."""
+    sts_text, seq = _synthetic(23, 200, 300_000, 11, 1, 0)
+    eng = MerPCR(wordsize=11, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    g = _native.Genome(0, [len(seq)])
+    g.put(0, seq.encode())
+    g.seal()
+    s = _native.Search(eng.device_table(), g)
+    n = s.run()
+    ref = s.fetch(n)
+    assert n > 10
+    s.enqueue()
+    for fn in (lambda: s.fetch(n), s.last_stats, s.device_hits, lambda: g.reset([len(seq)]),
+               lambda: g.put(0, b"ACGT")):
+        with pytest.raises(_native.NativeError) as ei:
+            fn()
+        assert ei.value.code == _native.MP_E_STATE, ei.value
+    n2 = s.complete()
+    assert n2 == n and s.fetch(n2).tobytes() == ref.tobytes()
+    assert s.dev_bytes() > 0
+    s.enqueue()
+    s.close()  # waits for the enqueued run
+    g.reset([len(seq)])  # no run pending any more
+    g.close()
 
 
 def test_handles_reused_across_searches():

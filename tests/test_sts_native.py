@@ -122,10 +122,10 @@ def test_invalid_utf8_raises(tmp_path):
 
 
 def test_lazy_records_and_record_texts(tmp_path):
-    """A native load builds no STSRecord until sts_records / sts_table are used; the
-    formatter's record column then comes from the parser's bytes and equals the
-    f"{id}\\t{alias}\\t({direct})" text of the built records; any mutation of the list makes
-    the engine rebuild its arrays from the objects."""
+    """A native load builds no STSRecord while only the engine's own paths run (table
+    arrays, formatter column from the parser's bytes); the first caller access to
+    sts_records / sts_table builds both, and the engine then rebuilds its arrays and texts
+    from the record objects, which equal the parser's."""
     import copy
     import pickle
 
@@ -136,23 +136,69 @@ def test_lazy_records_and_record_texts(tmp_path):
                          f"{rng.choice(['al', 'ſ x', ''])}\n" for i in range(300)))
     eng = MerPCR(wordsize=11)
     assert eng.load_sts_file(str(p))
-    assert eng.sts_records._src is not None and eng.sts_table._src is not None
+    assert eng._recs._src is not None and eng._table._src is not None
     n = eng._n_records()
     arrays = eng._table_arrays()
     blob, off = eng._record_texts()
-    assert eng.sts_records._src is not None, "the search path built the records"
+    assert eng._native_current() and eng._table_arrays() is arrays
+    assert eng._recs._src is not None, "the search path built the records"
     assert len(eng.sts_records) == n
-    assert eng.sts_table._src is None  # one build fills both
+    assert eng._table._src is None  # one build fills both
+    assert not eng._native_current()  # handed out: the objects are the truth from now on
     want = _csr([f"{r.id}\t{r.alias}\t({r.direct})" for r in eng.sts_records])
     assert np.array_equal(blob, want[0]) and np.array_equal(off, want[1])
+    rb, ro = eng._record_texts()
+    assert np.array_equal(rb, blob) and np.array_equal(ro, off)
+    arr2 = eng._table_arrays()
+    for x, y in zip(arrays, arr2):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
     assert sum(len(v) for v in eng.sts_table.values()) == n
     ids = {id(r) for v in eng.sts_table.values() for r in v}
     assert ids == {id(r) for r in eng.sts_records}
     assert type(pickle.loads(pickle.dumps(eng.sts_records))) is list
     assert copy.deepcopy(eng.sts_records) == list(eng.sts_records)
-    assert eng._native_current() and eng._table_arrays() is arrays
     eng.sts_records.append(eng.sts_records[0])
-    assert not eng._native_current()
     assert eng._n_records() == n + 1
     blob2, off2 = eng._record_texts()
     assert len(off2) == n + 2
+
+
+def test_lazy_containers_visible_to_c_level_readers():
+    """A caller that reaches sts_records / sts_table gets them built: json, numpy,
+    str.join and dict iteration in C see every item (lazy list subclasses
+    looked empty at the C level)."""
+    import json
+    from merpcr_amd import MerPCR
+    eng = MerPCR(wordsize=11)
+    assert eng.load_sts_file(os.path.join(os.path.dirname(__file__), "golden", "data", "test.sts"))
+    recs = eng.sts_records
+    n = len(recs)
+    assert n > 0
+    assert len(json.loads(json.dumps([r.id for r in recs]))) == n
+    assert "\n".join(r.id for r in eng.sts_records).count("\n") == n - 1
+    assert len(json.loads(json.dumps({str(k): len(v) for k, v in eng.sts_table.items()}))) == len(eng.sts_table)
+    assert sum(len(v) for v in dict(eng.sts_table).values()) == n
+
+
+def test_format_follows_records_edited_in_place():
+    """format_bytes reads the current record objects once they are handed out: an edit of
+    rec.id / rec.alias / rec.direct, or replacing a list element, shows in the next output
+    (engine.py:437-443 formats from the records on every call)."""
+    import numpy as np
+    from merpcr_amd import MerPCR, _native
+    from merpcr_amd.core.models import FASTARecord
+    eng = MerPCR(wordsize=11)
+    assert eng.load_sts_file(os.path.join(os.path.dirname(__file__), "golden", "data", "test.sts"))
+    h = np.zeros(1, dtype=_native.HIT_DTYPE)
+    h["pos1"], h["pos2"], h["seq"], h["rec"] = 10, 200, 0, 0
+    fr = [FASTARecord("seq1 description", "ACGT")]
+    before = eng.format_bytes(fr, h).decode()
+    r0 = eng.sts_records[0]
+    r0.id, r0.alias, r0.direct = "EDITED", "ALIAS2", "-"
+    after = eng.format_bytes(fr, h).decode()
+    assert after != before and "EDITED\tALIAS2\t(-)" in after, (before, after)
+    import copy
+    r1 = copy.copy(r0)
+    r1.id = "REPLACED"
+    eng.sts_records[0] = r1
+    assert "REPLACED" in eng.format_bytes(fr, h).decode()
