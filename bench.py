@@ -323,6 +323,8 @@ def main():
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time only rank 0's owned range of an N-way split on this one GPU "
                          "(no collective); the JSON line is then not the metric")
+    ap.add_argument("--opts", default="",
+                    help="diagnostic A/B: search options for every handle, name=value[,...] (_native.Search.set_options)")
     args = ap.parse_args()
 
     import torch
@@ -390,6 +392,14 @@ def main():
     # handle's next run waits (on the device) for its gather to have sent the hits.
     nbuf = 1 if args.no_pipeline else max(2, args.handles)
     handles = [search] + [_native.Search(table, genome) for _ in range(nbuf - 1)]
+    if args.opts:
+        kw = {}
+        for item in args.opts.split(","):
+            k, val = item.split("=")
+            kw[k] = val if k in ("tails", "sort") else (val.lower() in ("1", "true") if k in (
+                "defer", "dense", "rank_filter", "split", "fuse_tails") else int(val))
+        for h in handles:
+            h.set_options(**kw)
     # one stream per handle (--one-stream: all on the default stream): step i+1's scan may then
     # start on the CUs that step i's latency-bound tail / pair / order kernels leave idle
     streams = [torch.cuda.current_stream()] + [
@@ -602,6 +612,8 @@ def main():
                         "HIP events around the scan kernel on its launch stream in 3 untimed steps after the "
                         "timed ones, run one at a time (in the timed steps kernels of consecutive steps overlap)"),
     }
+    if args.opts:
+        out["search_options"] = args.opts
     if args.shard_of > 1:
         out["diagnostic"] = f"rank 0 of a {args.shard_of}-way owned-range split, alone on one GPU (not the metric)"
     if args.rehearse_one_gpu:

@@ -149,6 +149,8 @@ typedef struct mp_search_options {
                                    filtered rank groups' primer-base filter */
     int32_t no_split;           /* 1: W 7..9 tables keep the dense scan, not the split seeds
                                    (two exact-seed scans, see mp_internal.h kSplitSeed) */
+    int32_t no_fuse_tails;      /* 1: bucket-tail references expanded by their own kernel
+                                   (tail_kernel) instead of inside the pair check */
 } mp_search_options;
 /* Replace the handle's options (reallocating the lists to the given capacities). */
 int mp_search_set_options(void* search, const mp_search_options* opt);
@@ -212,6 +214,10 @@ int mp_multi_fetch(void* multi, mp_hit* out, uint64_t cap);
 /* Device i's search handle (borrowed: stats, timings), its owned range and the last
  * gather's duration on devices[0]'s stream. */
 int mp_multi_device_search(void* multi, uint32_t i, void** search, mp_range* owned, float* gather_ms);
+/* The last mp_multi_run's device span on devices[0] (its start, before the first search is
+ * enqueued, to the gather's end) and the gather alone; wall time minus the span is the host
+ * overhead of the call. */
+int mp_multi_timing(void* multi, float* span_ms, float* gather_ms);
 void mp_multi_destroy(void* multi);
 
 /* One process per GPU (torchrun-style launch): every rank creates a communicator from an

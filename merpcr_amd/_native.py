@@ -13,7 +13,8 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_uint8, c_uint32
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "_lib", "libmerpcr_hip.so")
+# MERPCR_LIB: an A/B variant library built in-tree (scripts/ablate.py, scripts/ab_lib.py)
+LIB_PATH = os.environ.get("MERPCR_LIB") or os.path.join(_PKG, "_lib", "libmerpcr_hip.so")
 
 MP_OK = 0
 MP_E_ARG = -1
@@ -35,7 +36,7 @@ EXPORTS = (
     "mp_search_enqueue", "mp_search_complete", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
     "mp_search_last_stats", "mp_search_regrowths", "mp_search_dev_bytes", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
     "mp_multi_create", "mp_multi_genome", "mp_multi_put", "mp_multi_seal", "mp_multi_run", "mp_multi_fetch",
-    "mp_multi_device_search", "mp_multi_destroy",
+    "mp_multi_device_search", "mp_multi_timing", "mp_multi_destroy",
     "mp_comm_unique_id", "mp_comm_create", "mp_comm_gather_hits", "mp_comm_destroy",
     "mp_fasta_load", "mp_fasta_load_parallel", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record_ascii", "mp_fasta_record", "mp_fasta_destroy",
     "mp_format_hits",
@@ -61,7 +62,7 @@ class MPSearchOptions(ctypes.Structure):
     _fields_ = [("tails", c_int32), ("no_defer", c_int32), ("no_dense", c_int32), ("sort", c_int32),
                 ("sort_bucket_bits", c_int32), ("pair_blocks_per_cu", c_int32),
                 ("hit_cap", c_uint64), ("surv_cap", c_uint64), ("tail_cap", c_uint64),
-                ("no_rank_filter", c_int32), ("no_split", c_int32)]
+                ("no_rank_filter", c_int32), ("no_split", c_int32), ("no_fuse_tails", c_int32)]
 
 
 HIT_DTYPE = np.dtype([("pos1", "<u8"), ("pos2", "<u8"), ("seq", "<u4"), ("rec", "<u4")])
@@ -121,6 +122,7 @@ def _sig(lib):
     lib.mp_multi_run.argtypes = [P, u64p]
     lib.mp_multi_fetch.argtypes = [P, P, c_uint64]
     lib.mp_multi_device_search.argtypes = [P, c_uint32, POINTER(c_void_p), POINTER(MPRange), POINTER(c_float)]
+    lib.mp_multi_timing.argtypes = [P, POINTER(c_float), POINTER(c_float)]
     lib.mp_multi_destroy.argtypes = [P]
     lib.mp_multi_destroy.restype = None
     lib.mp_comm_unique_id.argtypes = [P]
@@ -309,12 +311,13 @@ class Search:
         check(lib().mp_search_create(table._h, genome._h, ctypes.byref(self._h)))
 
     def set_options(self, tails="auto", defer=True, dense=True, sort="auto", sort_bucket_bits=0,
-                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True, split=True):
+                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True, split=True,
+                    fuse_tails=True):
         """Kernel-path selection and initial list capacities (mp_search_set_options);
         the defaults are the library's automatic choices."""
         o = MPSearchOptions(MP_TAILS[tails], 0 if defer else 1, 0 if dense else 1, MP_SORT[sort],
                             sort_bucket_bits, pair_blocks_per_cu, hit_cap, surv_cap, tail_cap,
-                            0 if rank_filter else 1, 0 if split else 1)
+                            0 if rank_filter else 1, 0 if split else 1, 0 if fuse_tails else 1)
         check(lib().mp_search_set_options(self._h, ctypes.byref(o)))
 
     def set_stage_timing(self, on: bool):
@@ -448,6 +451,12 @@ class Multi:
         s, r, g = c_void_p(), MPRange(), c_float()
         check(lib().mp_multi_device_search(self._h, i, ctypes.byref(s), ctypes.byref(r), ctypes.byref(g)))
         return _Borrowed(s), (r.seq_begin, r.seq_end, r.k_begin, r.k_end), g.value
+
+    def timing(self):
+        """(span_ms, gather_ms) of the last run on devices[0]'s stream."""
+        sp, g = c_float(), c_float()
+        check(lib().mp_multi_timing(self._h, ctypes.byref(sp), ctypes.byref(g)))
+        return sp.value, g.value
 
     def close(self):
         if self._h:

@@ -552,20 +552,26 @@ constexpr int kHitMaxRegion = 8;                  // host word 8: the largest re
 constexpr int kHostWords = 16;                    // device-mapped host words per search
 
 // The run's finish, by one workgroup after the last producer (pair_kernel): counters[0..8)
-// to the host words with word 0 = the hit total (the sum of the region counts) and word
+// to the host words with word 0 = the hit total (the sum of the region counts), words 1 and 3
+// = the candidate and survivor statistics (the sums of the add_stats slots), word
 // kHitMaxRegion = the largest region count (capacity check), the region counts to rcount
 // (device copy for the order kernels), then every counter zeroed for the next run.
 __device__ __forceinline__ void finish_fold(unsigned long long* __restrict__ counters, uint32_t n_words,
                                             unsigned long long* __restrict__ h_out,
                                             unsigned long long* __restrict__ rcount) {
-    unsigned long long v = 0, r = 0;
+    unsigned long long v = 0, r = 0, sc = 0, ss = 0;
     if (threadIdx.x < 8) {
         v = counters[threadIdx.x];
         r = counters[kHitBase + threadIdx.x * kStatStride];
     }
+    if (threadIdx.x < kStatSlots) {  // the candidate / survivor statistic slots (add_stats)
+        sc = counters[kStatBase + threadIdx.x * kStatStride];
+        ss = counters[kStatBase + threadIdx.x * kStatStride + 1];
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n_words; i += blockDim.x) counters[i] = 0ull;
-    if (threadIdx.x < 64) {  // wave 0: the region sum and maximum over lanes 0..7
+    if (threadIdx.x < 64) {  // wave 0: the region sum and maximum over lanes 0..7, the statistics' sums
+        static_assert(kStatSlots == 64, "one statistic slot per lane of wave 0");
         unsigned long long sum = r, mx = r;
 #pragma unroll
         for (int o = 1; o < 8; o <<= 1) {
@@ -574,9 +580,14 @@ __device__ __forceinline__ void finish_fold(unsigned long long* __restrict__ cou
             sum += ys;
             mx = ym > mx ? ym : mx;
         }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            sc += (unsigned long long)__shfl_xor((long long)sc, o, 64);
+            ss += (unsigned long long)__shfl_xor((long long)ss, o, 64);
+        }
         if (threadIdx.x < 8) {
             rcount[threadIdx.x] = r;
-            h_out[threadIdx.x] = threadIdx.x == 0 ? sum : v;
+            h_out[threadIdx.x] = threadIdx.x == 0 ? sum : threadIdx.x == 1 ? sc : threadIdx.x == 3 ? ss : v;
             if (threadIdx.x == 0) h_out[kHitMaxRegion] = mx;
             __threadfence_system();  // the host polls the run's event, then reads these
         }

@@ -10,8 +10,9 @@
 // it.
 //
 // Two forms:
-//   * mp_multi_*: one process drives several devices, one host thread per device for the
-//     pack and the search, then one grouped ncclSend/ncclRecv gatherv into devices[0]
+//   * mp_multi_*: one process drives several devices: a host thread per device for the
+//     pack, the searches enqueued and completed from the calling thread (they run
+//     concurrently), then one grouped ncclSend/ncclRecv gatherv into devices[0]
 //     (ncclCommInitAll over distinct devices; a repeated device -- tests on one GPU --
 //     is gathered by device copies instead, as RCCL admits one rank per device).
 //   * mp_comm_*: one process per GPU (torchrun / MPI style): the caller shares the RCCL
@@ -56,6 +57,9 @@ struct Multi {
     mp_hit* all = nullptr;          // gathered hits on dev[0]
     uint64_t all_cap = 0, n_all = 0;
     hipEvent_t e0 = nullptr, e1 = nullptr;  // gather timing on dev[0], made once
+    hipEvent_t es = nullptr;                // the call's start on dev[0] (span: es -> e1)
+    float span_ms = 0.f;
+    std::vector<hipEvent_t> sent;           // per device: its gather send is queued (RCCL form)
     float gather_ms = 0.f;
 };
 
@@ -65,6 +69,7 @@ static void free_multi(Multi* m) {
     for (size_t i = 0; i < m->dev.size(); ++i) {
         hipSetDevice(m->dev[i]);
         if (m->srch[i]) mp_search_destroy(m->srch[i]);
+        if (i < m->sent.size() && m->sent[i]) hipEventDestroy(m->sent[i]);
         if (m->gen[i]) mp_genome_destroy(m->gen[i]);
         if (m->st[i]) hipStreamDestroy(m->st[i]);
     }
@@ -73,6 +78,7 @@ static void free_multi(Multi* m) {
         if (m->all) hipFree(m->all);
         if (m->e0) hipEventDestroy(m->e0);
         if (m->e1) hipEventDestroy(m->e1);
+        if (m->es) hipEventDestroy(m->es);
     }
     delete m;
 }
@@ -171,16 +177,18 @@ MP_EXPORT int mp_multi_create(uint32_t n_dev, const int32_t* devices, void* cons
     m->srch.assign(n_dev, nullptr);
     m->st.assign(n_dev, nullptr);
     m->counts.assign(n_dev, 0);
+    m->sent.assign(n_dev, nullptr);
     int rc = MP_OK;
     for (uint32_t d = 0; d < n_dev && !rc; ++d) {
         m->tab[d] = (Table*)tables[d];
         if (!m->tab[d]) rc = fail(MP_E_ARG, "mp_multi_create: null table");
         else if (m->tab[d]->device != m->dev[d]) rc = fail(MP_E_ARG, "mp_multi_create: table i must live on devices[i]");
-        else if (hipSetDevice(m->dev[d]) != hipSuccess || hipStreamCreateWithFlags(&m->st[d], hipStreamNonBlocking) != hipSuccess)
+        else if (hipSetDevice(m->dev[d]) != hipSuccess || hipStreamCreateWithFlags(&m->st[d], hipStreamNonBlocking) != hipSuccess ||
+                 hipEventCreateWithFlags(&m->sent[d], hipEventDisableTiming) != hipSuccess)
             rc = fail(MP_E_HIP, "mp_multi_create: stream creation failed");
     }
     if (!rc && (hipSetDevice(m->dev[0]) != hipSuccess || hipEventCreate(&m->e0) != hipSuccess ||
-                hipEventCreate(&m->e1) != hipSuccess))
+                hipEventCreate(&m->e1) != hipSuccess || hipEventCreate(&m->es) != hipSuccess))
         rc = fail(MP_E_HIP, "mp_multi_create: event creation failed");
     if (!rc) {
         std::vector<int> sorted(m->dev);
@@ -226,14 +234,37 @@ MP_EXPORT int mp_multi_seal(void* multi) {
     return per_device((uint32_t)m->dev.size(), [&](uint32_t d) { return mp_genome_seal(m->gen[d], m->st[d]); });
 }
 
+// Every device's run is enqueued from the calling thread (mp_search_enqueue returns as soon as
+// its kernels are queued), then completed device by device (each polls its own run's event),
+// so the devices search concurrently with no host thread started per call.  The gather waits
+// on the devices, not the host: device 0's stream takes every sender's event before the
+// gather-end event the host polls.  (Round 3 started a std::thread per device per call and
+// synchronised every device's stream.)
 MP_EXPORT int mp_multi_run(void* multi, uint64_t* n_hits) {
     Multi* m = (Multi*)multi;
     if (!m) return fail(MP_E_ARG, "mp_multi_run: null multi");
     if (!m->gen[0]) return fail(MP_E_STATE, "mp_multi_run: no genome (call mp_multi_genome)");
     const uint32_t nd = (uint32_t)m->dev.size();
     if (n_hits) *n_hits = 0;
-    const int rc = per_device(nd, [&](uint32_t d) { return mp_search_run(m->srch[d], &m->rng[d], m->st[d], &m->counts[d]); });
-    if (rc) return rc;
+    MP_HIP_CHECK(hipSetDevice(m->dev[0]));
+    MP_HIP_CHECK(hipEventRecord(m->es, m->st[0]));
+    for (uint32_t d = 0; d < nd; ++d) {
+        const int rc = mp_search_enqueue(m->srch[d], &m->rng[d], m->st[d]);
+        if (rc) {
+            for (uint32_t e = 0; e < d; ++e) mp_search_complete(m->srch[e], nullptr);  // drain what was queued
+            return rc;
+        }
+    }
+    int rc = MP_OK;
+    std::string msg;
+    for (uint32_t d = 0; d < nd; ++d) {  // complete them all, keeping the first failure
+        const int r = mp_search_complete(m->srch[d], &m->counts[d]);
+        if (r && !rc) {
+            rc = r;
+            msg = mp_last_error();
+        }
+    }
+    if (rc) return fail(rc, msg);
     uint64_t total = 0;
     for (auto c : m->counts) total += c;
     MP_HIP_CHECK(hipSetDevice(m->dev[0]));
@@ -259,11 +290,14 @@ MP_EXPORT int mp_multi_run(void* multi, uint64_t* n_hits) {
             off += m->counts[d];
         }
         MP_NCCL_CHECK(ncclGroupEnd());
+        // device 0's stream waits (on the device) for every sender; a sender's next run is
+        // queued behind its send on its own stream
         for (uint32_t d = 1; d < nd; ++d) {
             MP_HIP_CHECK(hipSetDevice(m->dev[d]));
-            MP_HIP_CHECK(hipStreamSynchronize(m->st[d]));
+            MP_HIP_CHECK(hipEventRecord(m->sent[d], m->st[d]));
         }
         MP_HIP_CHECK(hipSetDevice(m->dev[0]));
+        for (uint32_t d = 1; d < nd; ++d) MP_HIP_CHECK(hipStreamWaitEvent(m->st[0], m->sent[d], 0));
     } else {
         for (uint32_t d = 0; d < nd; ++d) {  // a repeated device: peer / local copies
             const size_t bytes = m->counts[d] * sizeof(mp_hit);
@@ -273,8 +307,9 @@ MP_EXPORT int mp_multi_run(void* multi, uint64_t* n_hits) {
         }
     }
     MP_HIP_CHECK(hipEventRecord(m->e1, m->st[0]));
-    MP_HIP_CHECK(hipStreamSynchronize(m->st[0]));
+    MP_HIP_CHECK(poll_event(m->e1));
     MP_HIP_CHECK(hipEventElapsedTime(&m->gather_ms, m->e0, m->e1));
+    MP_HIP_CHECK(hipEventElapsedTime(&m->span_ms, m->es, m->e1));
     m->n_all = total;
     if (n_hits) *n_hits = total;
     return MP_OK;
@@ -296,6 +331,14 @@ MP_EXPORT int mp_multi_device_search(void* multi, uint32_t i, void** search, mp_
     if (!m || i >= m->dev.size()) return fail(MP_E_ARG, "mp_multi_device_search: bad index");
     if (search) *search = m->srch[i];
     if (owned) *owned = i < m->rng.size() ? m->rng[i] : mp_range{0, 0, 0, 0};
+    if (gather_ms) *gather_ms = m->gather_ms;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_multi_timing(void* multi, float* span_ms, float* gather_ms) {
+    Multi* m = (Multi*)multi;
+    if (!m) return fail(MP_E_ARG, "mp_multi_timing: null multi");
+    if (span_ms) *span_ms = m->span_ms;
     if (gather_ms) *gather_ms = m->gather_ms;
     return MP_OK;
 }

@@ -105,6 +105,7 @@ struct ScanArgs {
     // bases and the gap_post bases after the seed's span.
     uint32_t gap_at, gap_len, gap_post;
     uint32_t tail_ctr;      // counters[] slot of this scan's bucket-tail list (4; 5 for the gapped scan)
+    uint32_t fuse_tails;    // pair_kernel also opens the bucket-tail references (no tail_kernel)
     uint32_t sched_base;    // counters[] index of this scan's 8 chunk counters (kSchedBase, kSchedSplit...)
 };
 
@@ -417,11 +418,11 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int j) {
 // popcount when primer 2 is plain (one base per position) and no exception base is in
 // the windows, else through the accept planes.  The reference's try order 0, -1, +1,
 // ... is restored by the device sort through try_rank(d).
-__device__ void pair_check_batch(const ScanArgs& a, uint64_t base, uint64_t n_surv, uint32_t batch, int lane,
-                                 HitStage& S, uint64_t* __restrict__ pst) {
-    const uint64_t i = base + (uint64_t)lane;
-    uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-    if ((uint32_t)lane < batch && i < n_surv) v = a.surv[i];
+// The lane's survivor v (kEmptySurv: none); batch = the wave's survivors (lanes 0..batch-1),
+// which sets how the lane-parallel tries split over lane groups.
+constexpr uint4 kEmptySurv = {0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u};
+__device__ void pair_check_lanes(const ScanArgs& a, uint4 v, uint32_t batch, int lane, HitStage& S,
+                                 uint64_t* __restrict__ pst) {
     bool keep = !(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu);
     const uint64_t gk = (uint64_t)v.x | ((uint64_t)v.y << 32);
     const uint32_t rec = v.z & 0x7FFFFFFFu;
@@ -1483,6 +1484,7 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         S = min(lo + nw * chunk, hi);
         young = (uint32_t)w >= (uint32_t)kW / 2u;
         const uint32_t st = lo + ((blockIdx.x / g) * (uint32_t)kW + (uint32_t)w) * chunk;
+        lo = x;  // from here on: the group being claimed from (steal)
         end = min(st + chunk, hi);
         hint = st;
         claim(lane);
@@ -1497,13 +1499,21 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         pending = 0;
         if (lane == 0) pending = atomicAdd(ctr, sz);
     }
-    __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane) {
+    template <bool kSteal = true>
+    __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane, int kW) {
         if (stride) return ss + stride;
         if (ss + 1 < end) return ss + 1;
         // lane 0 holds the claimed position; next() runs at the top of the super-step loop
         // with every lane active, so the first active lane is lane 0 and the broadcast is a
         // readfirstlane (the scheduler state then stays in scalar registers)
-        const uint32_t st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);
+        uint32_t st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);
+#ifndef MP_NO_STEAL
+        while (kSteal && st >= hi) {  // this group's range is claimed out: help a group that is behind
+            if (!steal(n_supers, kW, lane)) break;
+            claim(lane);
+            st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);
+        }
+#endif
         if (st >= hi) {
             end = 0;
             return n_supers;
@@ -1512,6 +1522,38 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         hint = st;
         claim(lane);
         return st;
+    }
+    // End-of-scan stealing across XCD groups, in the fields the scheduler already has (a
+    // wider state spilled the scan kernel's SGPRs): lo, unused after first(), names the group
+    // being claimed from; ctr, hi, S and nw are re-pointed at the next group (x + 1, x + 2,
+    // ... around to the home group) whose counter still lies inside its range, read first
+    // with a plain atomic load so that exhausted counters take no read-modify-write.  The
+    // groups' eighths cost 7.7-8.1 us per super-step and wave, differently run to run, and
+    // ended up to 18 us apart without it.  Claims there are of one super-step.
+    __device__ __forceinline__ bool steal(uint64_t n_supers, int kW, int lane) {
+        if (gridDim.x < 8u) return false;  // eight groups (every full-chip grid): shifts, no division
+        const uint32_t home = blockIdx.x & 7u;
+        uint32_t x = lo;
+        for (uint32_t t = 1; t < 8u; ++t) {
+            const uint32_t nx = (x + 1u) & 7u;
+            if (nx == home) return false;
+            ctr += ((int)nx - (int)x) * (int)(2 * kStatStride);  // u32 units
+            x = nx;
+            const uint32_t h = (uint32_t)((n_supers * (x + 1)) >> 3);
+            const uint32_t s0 = min((uint32_t)((n_supers * x) >> 3) + ((gridDim.x - x + 7u) >> 3) * (uint32_t)kW * chunk, h);
+            uint32_t cur = 0;
+            if (lane == 0) cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur);
+            if (s0 + cur < h) {
+                lo = x;
+                hi = h;
+                S = s0;
+                hint = h;  // guided size from a range with nothing left: claims of one
+                young = 0;
+                return true;
+            }
+        }
+        return false;
     }
 };
 
@@ -1600,7 +1642,9 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                                          window_ok_mask(R.iv << (a.gap_at + a.gap_len), W - a.gap_at)
                                    : window_ok_mask(R.iv, W)) &
                              span_bits(sp, pb);
-        const uint64_t nx = sch.next(ss, n_supers, lane);
+        // stealing in the kernels whose registers have room for it (the deferring rank/key-group
+        // scans of c2-c5); the others would spill VGPRs to scratch
+        const uint64_t nx = sch.template next<kMode == 1 && kDefer>(ss, n_supers, lane, kWaves);
         (void)stride;
         if constexpr (kMode == 1) {
             // level 2, wave-compacted: the wave's LDS-positive windows go into the LDS list
@@ -1964,7 +2008,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         // otherwise; under I=0 such a base reads as 'A' and can only hide a mismatch, and U
         // compares as T under I=1)
         const uint32_t slowm = a.I ? ~window_ok_mask(iv, 16u) : 0u;
-        const uint64_t nx = sch.next(ss, n_supers, lane);
+        const uint64_t nx = sch.next(ss, n_supers, lane, kWaves);
         (void)stride;
         if (nx < n_supers) {  // next super-step's words, in flight during this one
             locate(nx);
@@ -2095,6 +2139,91 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
     __syncthreads();
 }
 
+// One bucket-tail reference opened: its bucket (first ents index, record count, the first
+// record's Entry) and what the record tests need from the reference.  A key reference
+// (scan_kernel's key-group path) finds its bucket from the key by rank; a head8 bucket whose
+// filter bases rule out every record is empty (cnt = 0).
+struct TailRef {
+    uint64_t gp, Gs;         // seed position (global) and the 32-base window at it
+    uint32_t ex, rem, seq;   // exception bits of the window, bases from the seed to the end, sequence
+    uint32_t first, cnt;     // the bucket's first ents index and its records
+    Entry e0;                // its first record
+};
+
+template <bool kGap>
+__device__ __forceinline__ void tail_open(const ScanArgs& a, const uint4 v, const uint4 w, TailRef& t) {
+    t.cnt = 0;
+    if (v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu) return;
+    t.gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    t.Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);
+    t.ex = w.z;
+    t.rem = w.w;
+    t.seq = v.w;
+    uint32_t first = v.z;
+    Entry e;
+    if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
+        const uint32_t W = (uint32_t)a.W;
+        const uint32_t h = kGap ? gap_key((uint32_t)(t.Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
+                                : (uint32_t)(t.Gs >> (64u - 2u * W));
+        const uint2 rw = a.rk[h >> 5];
+        const uint2 c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
+        if (c.y & kHead8Full) {
+            first = c.x;  // the bucket's first entry
+            if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
+                const uint32_t cnt = ((c.y >> 28) & 3u) + 1u;
+                const uint32_t F = head8_filt_bases(cnt);
+                const uint32_t fm = (1u << (2u * F)) - 1u;
+                const uint32_t gf = (uint32_t)((t.Gs << (2u * W)) >> (64u - 2u * F));
+                const uint32_t xf = t.ex & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
+                bool any = xf != 0u;
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    const uint32_t xj = gf ^ ((c.y >> (2u * F * j)) & fm);
+                    any = any || __popc((xj | (xj >> 1)) & 0x55555555u) <= a.N;
+                }
+                if (!any) return;
+            }
+            e = a.ents[first];
+        } else {
+            e = head8_entry(c, h, W);
+        }
+    } else {
+        e = a.ents[first];  // its count = tail length
+    }
+    t.first = first;
+    t.cnt = e.count;
+    t.e0 = e;
+}
+
+// Record e of an opened reference: bounds, ownership, the gapped seed's exact-gap rule and
+// the fingerprint test (fp_reject); a survivor in *sv.
+template <bool kGap>
+__device__ __forceinline__ bool tail_test(const ScanArgs& a, const TailRef& t, const Entry& e, uint32_t& ncand,
+                                          uint4& sv) {
+    const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
+    const uint64_t gk = t.gp - e.hash_off;
+    if ((uint32_t)e.l1 > t.rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) return false;  // k + l1 > n / not owned
+    uint64_t G = t.Gs;
+    uint32_t ex = t.ex;
+    if (e.hash_off) {  // seed inside the primer: bounds and window from the genome
+        const uint64_t sbase = a.seq_base[t.seq];
+        if (t.gp - sbase < e.hash_off) return false;  // k < 0
+        G = ext2(a.g2, gk);
+        ex = (uint32_t)(ext1(exc, gk) >> 32);
+    }
+    if constexpr (kGap) {  // a window whose gap matches exactly is the contiguous seed's
+        const uint64_t gm = sp_lt((int)(a.gap_at + a.gap_len)) & ~sp_lt((int)a.gap_at);
+        const uint64_t xg = G ^ e.code;
+        const uint32_t inv = a.has_u ? (uint32_t)(ext1(a.ginv, gk) >> 32) : ex;  // A/C/G/T/U are valid
+        const uint32_t im = (0xFFFFFFFFu >> a.gap_at) & ~(0xFFFFFFFFu >> (a.gap_at + a.gap_len));
+        if (((xg | (xg >> 1)) & gm) == 0 && (inv & im) == 0) return false;
+    }
+    ++ncand;
+    bool exact = false;
+    if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) return false;
+    sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), t.seq);
+    return true;
+}
+
 // kGap: the references of a gapped seed scan (split tables): the key is the gapped one, and a
 // window whose gap matches the record exactly is left to the contiguous seed's scan.
 template <bool kGap = false>
@@ -2106,7 +2235,6 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint64_t n_refs = umin64(a.counters[a.tail_ctr], a.tails_cap);
-    const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
     uint32_t ncand = 0, nsurv = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
     for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride) {  // block-uniform
@@ -2116,73 +2244,20 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
             v = a.tails[2 * i];
             w = a.tails[2 * i + 1];
         }
-        if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
-            const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
-            const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
-            const uint32_t rem = w.w;                                    // bases from the seed to the end
-            uint32_t first = v.z;
-            Entry e;
-            if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
-                const uint32_t W = (uint32_t)a.W;
-                const uint32_t h = kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
-                                        : (uint32_t)(Gs >> (64u - 2u * W));
-                const uint2 rw = a.rk[h >> 5];
-                const uint2 c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
-                if (c.y & kHead8Full) {
-                    first = c.x;  // the bucket's first entry
-                    if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
-                        const uint32_t cnt = ((c.y >> 28) & 3u) + 1u;
-                        const uint32_t F = head8_filt_bases(cnt);
-                        const uint32_t fm = (1u << (2u * F)) - 1u;
-                        const uint32_t gf = (uint32_t)((Gs << (2u * W)) >> (64u - 2u * F));
-                        const uint32_t xf = w.z & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
-                        bool any = xf != 0u;
-                        for (uint32_t j = 0; j < cnt; ++j) {
-                            const uint32_t xj = gf ^ ((c.y >> (2u * F * j)) & fm);
-                            any = any || __popc((xj | (xj >> 1)) & 0x55555555u) <= a.N;
-                        }
-                        if (!any) first = 0xFFFFFFFFu;
-                    }
-                    if (first != 0xFFFFFFFFu) e = a.ents[first];
-                    else e.count = 0;
-                } else {
-                    e = head8_entry(c, h, W);
-                }
-            } else {
-                e = a.ents[first];                                       // its count = tail length
-            }
-            const uint32_t cnt = e.count;
-            for (uint32_t j = 0; j < cnt; ++j) {
-                if (j) e = a.ents[first + j];
-                const uint64_t gk = gp - e.hash_off;
-                if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) continue;  // k + l1 > n / not owned
-                uint64_t G = Gs;
-                uint32_t ex = w.z;
-                if (e.hash_off) {  // seed inside the primer: bounds and window from the genome
-                    const uint64_t sbase = a.seq_base[v.w];
-                    if (gp - sbase < e.hash_off) continue;  // k < 0
-                    G = ext2(a.g2, gk);
-                    ex = (uint32_t)(ext1(exc, gk) >> 32);
-                }
-                if constexpr (kGap) {  // a window whose gap matches exactly is the contiguous seed's
-                    const uint64_t gm = sp_lt((int)(a.gap_at + a.gap_len)) & ~sp_lt((int)a.gap_at);
-                    const uint64_t xg = G ^ e.code;
-                    const uint32_t inv = a.has_u ? (uint32_t)(ext1(a.ginv, gk) >> 32) : ex;  // A/C/G/T/U are valid
-                    const uint32_t im = (0xFFFFFFFFu >> a.gap_at) & ~(0xFFFFFFFFu >> (a.gap_at + a.gap_len));
-                    if (((xg | (xg >> 1)) & gm) == 0 && (inv & im) == 0) continue;
-                }
-                ++ncand;
-                bool exact = false;
-                if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) continue;
-                ++nsurv;
-                const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
-                const uint32_t at = atomicAdd(&s_n, 1u);
-                if (at < kTailBuf) {
-                    s_buf[at] = sv;
-                } else {  // block buffer full (a burst of survivors): straight to the list
-                    const unsigned long long g = atomicAdd(&a.counters[2], 1ull);
-                    if (g < a.surv_cap) a.surv[g] = sv;
-                }
+        TailRef t;
+        tail_open<kGap>(a, v, w, t);
+        Entry e = t.e0;
+        for (uint32_t j = 0; j < t.cnt; ++j) {
+            if (j) e = a.ents[t.first + j];
+            uint4 sv;
+            if (!tail_test<kGap>(a, t, e, ncand, sv)) continue;
+            ++nsurv;
+            const uint32_t at = atomicAdd(&s_n, 1u);
+            if (at < kTailBuf) {
+                s_buf[at] = sv;
+            } else {  // block buffer full (a burst of survivors): straight to the list
+                const unsigned long long g = atomicAdd(&a.counters[2], 1ull);
+                if (g < a.surv_cap) a.surv[g] = sv;
             }
         }
         __syncthreads();
@@ -2202,24 +2277,20 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
 // (256 per launch instead of 1,024 with 4-wave blocks; c4 pair 0.743 -> 0.714 ms).
 constexpr int kPairWaves = 16;
 constexpr int kPairBlock = kPairWaves * 64;
+// Bucket-tail references folded into the pair check (a.fuse_tails; one-table runs): a batch
+// of 64 references, one per lane, is opened and its records tested one step j (the j-th record
+// of every lane's bucket) at a time, as tail_kernel does; a step's survivors are compacted into
+// the wave's LDS queue and pair-checked kFuseQ at a time.  No survivor-list round trip and no
+// kernel boundary between the two stages: tail_kernel was a latency chain of its own (12-21 us
+// per run on 1/8 of c3) that pair_kernel waited out.  One pair-check call site per wave loop
+// keeps the kernel within its 128 VGPRs (two inlined copies spilled to scratch).
+constexpr uint32_t kFuseQ = 63;  // the LDS left beside the stages: 1008 B per wave
 __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
-    if (blockIdx.x == 0 && threadIdx.x < 64) {  // statistics of the scan / tail kernels (add_stats)
-        unsigned long long c = a.counters[kStatBase + threadIdx.x * kStatStride];
-        unsigned long long v = a.counters[kStatBase + threadIdx.x * kStatStride + 1];
-        static_assert(kStatSlots == 64, "one stat slot per lane");
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            c += __shfl_xor(c, o, 64);
-            v += __shfl_xor(v, o, 64);
-        }
-        if (threadIdx.x == 0) {
-            a.counters[1] = c;
-            a.counters[3] = v;
-        }
-    }
+    const uint64_t n_refs = a.fuse_tails ? umin64(a.counters[a.tail_ctr], a.tails_cap) : 0ull;
     __shared__ HitStage s_st[kPairWaves];
     __shared__ uint64_t s_pst[kPairWaves][kPSlots * MP_PBATCH];
+    __shared__ uint4 s_fq[kPairWaves][kFuseQ];
     const int lane = threadIdx.x & 63;
     HitStage& S = s_st[threadIdx.x >> 6];
     if (lane == 0) S.n = 0;
@@ -2227,12 +2298,6 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     // survivors per wave batch: up to MP_PBATCH, fewer when the list is short, so that
     // every resident wave gets work (a batch is checked one survivor at a time)
     const uint64_t waves = (uint64_t)gridDim.x * kPairWaves;
-    // equal rounds for every wave: the fewest rounds of at most MP_PBATCH, then the batch
-    // that spreads n_surv evenly over them (32 per batch would leave 1/3 of the waves
-    // one round short on c3 while the kernel waits for the rest)
-    const uint64_t rounds = umax64(1, (n_surv + waves * MP_PBATCH - 1) / (waves * MP_PBATCH));
-    const uint32_t batch = (uint32_t)umax64(4, umin64(MP_PBATCH, (n_surv + waves * rounds - 1) / (waves * rounds)));
-    const uint64_t stride = waves * batch;
     // Dynamic batches: survivors cost very different amounts (primer-1 failures leave in
     // the prologue), so a static split left the slowest wave ~1.7x the mean.  Each XCD
     // (blocks x, x+8, ...) owns 1/8 of the batches: its waves take one batch each, then
@@ -2245,20 +2310,83 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
         const uint64_t per_wave = (n_surv + waves - 1) / waves;
         const uint32_t db = (uint32_t)umax64(MP_PAIR_MINB, umin64(per_wave < 128 ? 32 : MP_PDYN_BATCH, per_wave));
         const uint64_t nbat = (n_surv + db - 1) / db;
+        const uint64_t nref = (n_refs + 63) / 64;  // reference batches (fused tails)
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
+        // the group's survivor batches [lo_b, hi_b), then its reference batches [lo_r, hi_r):
+        // one local index space li in [0, (hi_b - lo_b) + (hi_r - lo_r))
         const uint64_t lo_b = nbat * x / g, hi_b = nbat * (x + 1) / g;
+        const uint64_t lo_r = nref * x / g, hi_r = nref * (x + 1) / g;
+        const uint64_t ns = hi_b - lo_b, nl = ns + (hi_r - lo_r);
         const uint64_t nw_x = (uint64_t)((gridDim.x - x + g - 1u) / g) * kPairWaves;  // waves of this group
-        uint64_t bi = lo_b + (uint64_t)(blockIdx.x / g) * kPairWaves + (threadIdx.x >> 6);
-        const uint64_t nw_d = nw_x;
-        while (bi < hi_b) {
-            pair_check_batch(a, bi * db, n_surv, db, lane, S, s_pst[threadIdx.x >> 6]);
-            unsigned long long t = 0;
-            if (lane == 0) t = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
-            bi = lo_b + nw_d + (uint64_t)__shfl((long long)t, 0, 64);
+        uint64_t li = (uint64_t)(blockIdx.x / g) * kPairWaves + (threadIdx.x >> 6);
+        uint64_t* pst = s_pst[threadIdx.x >> 6];
+        uint4* Q = s_fq[threadIdx.x >> 6];
+        uint32_t qn = 0, ncand = 0, nsurv = 0;  // queue fill (wave-uniform), statistics
+        // the open reference batch: each lane's reference and the next record step j
+        TailRef t;
+        t.cnt = 0;
+        uint32_t j = 0;
+        bool open = false;  // wave-uniform
+        for (;;) {
+            uint4 v = kEmptySurv;
+            uint32_t batch = 0;  // survivors to check this pass (wave-uniform)
+            if (open) {  // one record step of the open references
+                bool ok = false;
+                uint4 sv = kEmptySurv;
+                if (j < t.cnt) {
+                    const Entry e = j ? a.ents[t.first + j] : t.e0;
+                    ok = tail_test<false>(a, t, e, ncand, sv);
+                }
+                ++j;
+                open = __any(j < t.cnt);
+                const uint64_t bm = __ballot(ok);
+                const uint32_t k = (uint32_t)__popcll(bm);
+                nsurv += ok ? 1u : 0u;
+                if (k > kFuseQ) {  // (nearly) every lane survived: check them in place
+                    v = sv;
+                    batch = 64;
+                } else if (k) {
+                    if (qn + k > kFuseQ) {  // the queue is full: check it, then refill
+                        if ((uint32_t)lane < qn) v = Q[lane];
+                        batch = qn;
+                        qn = 0;
+                        wave_sync();
+                    }
+                    if (ok) Q[qn + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = sv;
+                    qn += k;
+                    wave_sync();
+                }
+            } else if (li < nl) {
+                if (li < ns) {
+                    const uint64_t i = (lo_b + li) * db + (uint64_t)lane;
+                    if ((uint32_t)lane < db && i < n_surv) v = a.surv[i];
+                    batch = db;
+                } else {
+                    const uint64_t i = (lo_r + li - ns) * 64u + (uint64_t)lane;
+                    uint4 rv = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), rw = make_uint4(0u, 0u, 0u, 0u);
+                    if (i < n_refs) {
+                        rv = a.tails[2 * i];
+                        rw = a.tails[2 * i + 1];
+                    }
+                    tail_open<false>(a, rv, rw, t);
+                    j = 0;
+                    open = __any(t.cnt != 0u);
+                }
+                unsigned long long c = 0;
+                if (lane == 0) c = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
+                li = nw_x + (uint64_t)__shfl((long long)c, 0, 64);
+            } else if (qn) {  // the queue's last survivors
+                if ((uint32_t)lane < qn) v = Q[lane];
+                batch = qn;
+                qn = 0;
+            } else {
+                break;
+            }
+            if (batch) pair_check_lanes(a, v, batch, lane, S, pst);
         }
+        if (a.fuse_tails) add_stats(a, ncand, nsurv, lane);
     }
-    (void)stride;
     // the block's stages leave with one returning atomic: one per wave at the end of the
     // kernel would serialise ~4k atomics on the hit counter (~88 per microsecond)
     __syncthreads();
@@ -2621,16 +2749,20 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     }
     const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
     if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
+    // one-table runs open their bucket-tail references inside pair_kernel (fused_ref_batch)
+    bool fuse = !s->opt.no_fuse_tails;
     if (!use_split(s)) {
         bool tail = false;
         const int rc = launch_scan(s, t, a, tiles, st, &tail);
         if (rc) return rc;
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
-        if (tail) {
+        if (tail && !fuse) {
             hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }
+        fuse = fuse && tail;
     } else {
+        fuse = false;
         const Table* sub[3] = {t->split_a, t->split_b, t->split_rest};
         ScanArgs pa[3];
         bool tail[3] = {false, false, false};
@@ -2657,7 +2789,9 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     MID_EVENT(hipEventRecord(s->ev1, st));
     const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
                                                            : s->pair_per_cu;
-    hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, a);
+    ScanArgs pa = a;
+    pa.fuse_tails = fuse ? 1u : 0u;
+    hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, pa);
     MP_HIP_CHECK(hipGetLastError());
     MID_EVENT(hipEventRecord(s->ev2, st));
     if (mode < 2) {  // hit order on the device count: no host round trip before it; its offsets
