@@ -71,7 +71,10 @@ constexpr int kLanePos = 32;                        // consecutive window positi
 constexpr uint32_t kSuper = 64 * kLanePos;          // positions per wave super-step
 constexpr int kBlocksPerCU = 1;                     // persistent grid: resident workgroups per CU
 constexpr int kDirShift = 12;                       // exception-run directory granularity
-constexpr int kLdsFilterLog2 = 20;                  // 128 KiB seed prefilter staged in LDS
+#ifndef MP_LDS_LOG2
+#define MP_LDS_LOG2 20  // A/B builds only (the c5 single-pass question): 19 = 64 KiB
+#endif
+constexpr int kLdsFilterLog2 = MP_LDS_LOG2;         // 128 KiB seed prefilter staged in LDS
 constexpr uint32_t kLdsFilterWords = (1u << kLdsFilterLog2) / 32;
 constexpr int kSub = 8;                             // filter probes in flight per lane
 

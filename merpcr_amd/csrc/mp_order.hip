@@ -73,15 +73,47 @@ __global__ void bucket_scatter(const uint64_t* __restrict__ keys, const unsigned
     }
 }
 
-// The decoded record of one key, written at its sorted slot (as decode_kernel does).
+// The last sequence whose base is <= gk, found by the whole wave (every lane active, gk
+// wave-uniform): a 64-ary search, one parallel load per level -- one level for up to 64
+// sequences (c3-c5: 24), two up to 4,096.
+__device__ inline uint32_t wave_seq_find(const uint64_t* __restrict__ seq_base, uint32_t n_seq, uint64_t gk,
+                                         uint32_t lane) {
+    uint32_t lo = 0, n = n_seq;  // the answer lies in [lo, lo + n); seq_base[lo] <= gk (seq_base[0] = 0)
+    while (n > 64) {
+        const uint32_t step = (n + 63) / 64;
+        const uint32_t idx = lo + lane * step;
+        const bool le = lane * step < n && seq_base[idx] <= gk;
+        const uint32_t c = (uint32_t)__popcll(__ballot(le));  // >= 1: lane 0 holds seq_base[lo]
+        lo += (c - 1) * step;
+        n = min(step, n - (c - 1) * step);
+    }
+    const bool le = lane < n && seq_base[lo + lane] <= gk;
+    return lo + (uint32_t)__popcll(__ballot(le)) - 1u;
+}
+
+// The sequences [lo, hi] that the global positions of bucket b's keys can fall in (keys of
+// bucket b are [b << shift, (b << shift) | (2^shift - 1)], positions are key >> low_bits):
+// the per-hit search is then over that range, usually one sequence, instead of a binary
+// search over seq_base with five dependent loads per hit (c4's order stage: 1.6M hits).
+struct SeqRange {
+    uint32_t lo, hi;
+};
+__device__ inline SeqRange bucket_seqs(uint32_t b, unsigned shift, unsigned low_bits,
+                                       const uint64_t* __restrict__ seq_base, uint32_t n_seq, uint32_t lane) {
+    const uint64_t k0 = (uint64_t)b << shift, k1 = k0 | ((1ull << shift) - 1ull);
+    return SeqRange{wave_seq_find(seq_base, n_seq, k0 >> low_bits, lane), wave_seq_find(seq_base, n_seq, k1 >> low_bits, lane)};
+}
+
+// The decoded record of one key, written at its sorted slot (as decode_kernel does); its
+// sequence is searched within sr (bucket_seqs).
 __device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits, unsigned low_bits,
                                   const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
-                                  uint32_t n_seq, const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
+                                  SeqRange sr, const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
                                   mp_hit* __restrict__ out) {
     const uint64_t gk = key >> low_bits;
     const uint32_t rank = (uint32_t)((key & ((1ull << low_bits) - 1ull)) >> try_bits);
     const uint32_t tr = (uint32_t)(key & ((1ull << try_bits) - 1ull));
-    uint32_t a = 0, b = n_seq;  // last sequence with base <= gk
+    uint32_t a = sr.lo, b = sr.hi + 1u;  // last sequence with base <= gk
     while (b - a > 1) {
         const uint32_t mid = (a + b) >> 1;
         if (seq_base[mid] <= gk) a = mid;
@@ -112,7 +144,8 @@ __device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits
 constexpr uint32_t kBucketsPerBlock = 4;
 constexpr uint32_t kRankCap = 256;
 __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
-                                                          uint32_t nb, unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
+                                                          uint32_t nb, unsigned shift, unsigned try_bits, unsigned low_bits,
+                                                          const uint64_t* __restrict__ seq_base,
                                                           const uint64_t* __restrict__ seq_len, uint32_t n_seq,
                                                           const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
                                                           mp_hit* __restrict__ out, unsigned long long* __restrict__ h_out,
@@ -132,7 +165,8 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
                 const uint64_t kj = __shfl(key, (int)j, 64);
                 r += kj < key || (kj == key && j < lane);  // ties: stable
             }
-            if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+            const SeqRange sr = bucket_seqs(b0 + wave, shift, low_bits, seq_base, n_seq, lane);
+            if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
         }
         if (!__syncthreads_or(m > 64 && m <= kRankCap)) return;  // every wave reaches this barrier
     }
@@ -140,12 +174,13 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
         const uint32_t start = off[b0 + q], m = off[b0 + q + 1] - start;
         if (m <= 64 || m > kRankCap) continue;  // done by its wave above / crowded_sort_decode
         for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
+        const SeqRange sr = bucket_seqs(b0 + q, shift, low_bits, seq_base, n_seq, lane);  // every lane of every wave
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
             const uint64_t key = s_k[i];
             uint32_t r = 0;
             for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
-            decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+            decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
         }
         __syncthreads();  // s_k is refilled by the next bucket
     }
@@ -168,7 +203,8 @@ __device__ __forceinline__ uint64_t cx_lane(uint64_t e, uint32_t i, uint32_t j, 
 // (10 of the 66 for 2,048 keys) go through LDS with a barrier each.  (All 66 through LDS,
 // one barrier each: c4's crowded buckets took 109 us.)
 __global__ __launch_bounds__(1024) void crowded_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
-                                                            unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base,
+                                                            unsigned shift, unsigned try_bits, unsigned low_bits,
+                                                            const uint64_t* __restrict__ seq_base,
                                                             const uint64_t* __restrict__ seq_len, uint32_t n_seq,
                                                             const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
                                                             mp_hit* __restrict__ out, const uint32_t* __restrict__ crowded) {
@@ -223,8 +259,9 @@ __global__ __launch_bounds__(1024) void crowded_sort_decode(const uint64_t* __re
             }
         }
         if (on) {
-            if (i0 < m) decode_hit(e0, start + i0, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
-            if (i1 < m) decode_hit(e1, start + i1, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+            const SeqRange sr = bucket_seqs(b, shift, low_bits, seq_base, n_seq, lane);
+            if (i0 < m) decode_hit(e0, start + i0, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
+            if (i1 < m) decode_hit(e1, start + i1, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
         }
     }
 }
@@ -238,7 +275,7 @@ __global__ __launch_bounds__(1024) void crowded_sort_decode(const uint64_t* __re
 constexpr uint32_t kSlotWaves = 4;
 __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
     const uint64_t* __restrict__ slots, uint32_t slot_cap, const uint32_t* __restrict__ off, uint32_t nb,
-    unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
+    unsigned shift, unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
     uint32_t n_seq, const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs, mp_hit* __restrict__ out,
     unsigned long long* __restrict__ h_out) {
     __shared__ uint64_t s_k[kSlotWaves][kSlotCap];
@@ -252,6 +289,7 @@ __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
         return;
     }
     const uint64_t* src = slots + (uint64_t)b * slot_cap;
+    const SeqRange sr = bucket_seqs(b, shift, low_bits, seq_base, n_seq, lane);
     if (m <= 64) {
         const uint64_t key = lane < m ? src[lane] : ~0ull;
         uint32_t r = 0;
@@ -259,7 +297,7 @@ __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
             const uint64_t kj = __shfl(key, (int)j, 64);
             r += kj < key || (kj == key && j < lane);  // ties: stable (keys are unique anyway)
         }
-        if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+        if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
         return;
     }
     uint64_t* k = s_k[wave];
@@ -271,7 +309,7 @@ __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
         const uint64_t key = k[i];
         uint32_t r = 0;
         for (uint32_t j = 0; j < m; ++j) r += k[j] < key || (k[j] == key && j < i);
-        decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, n_seq, inv_rank, recs, out);
+        decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
     }
 }
 
@@ -341,7 +379,7 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     MP_HIP_CHECK(hipGetLastError());
     if (mode == 0) {
         hipLaunchKernelGGL(sort_decode_slots, dim3((P.nb + kSlotWaves - 1) / kSlotWaves), dim3(64 * kSlotWaves), 0, st,
-                           s->slots, P.slot_cap, off, P.nb, P.try_bits, P.low_bits, g->d_base, g->d_len, g->n_seq,
+                           s->slots, P.slot_cap, off, P.nb, P.shift, P.try_bits, P.low_bits, g->d_base, g->d_len, g->n_seq,
                            s->table->inv_rank, s->table->recs, s->out, s->d_hcnt);
         MP_HIP_CHECK(hipGetLastError());
         return MP_OK;
@@ -351,7 +389,7 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
                        s->cap / kHitRegions, P.shift, cursor, s->tmp_hi);
     MP_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
-                       s->tmp_hi, off, P.nb, P.try_bits, P.low_bits,
+                       s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits,
                        g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->d_hcnt, sort_crowded(s));
     MP_HIP_CHECK(hipGetLastError());
     // crowded buckets: MP_CROWD_GRID workgroups (tuning; default one per CU)
@@ -359,7 +397,7 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
         const char* e = std::getenv("MP_CROWD_GRID");
         return e ? (uint32_t)std::max(1, std::atoi(e)) : 0u;
     }();
-    hipLaunchKernelGGL(crowded_sort_decode, dim3(crowd_grid ? crowd_grid : (uint32_t)s->n_cu), dim3(1024), 0, st, s->tmp_hi, off, P.try_bits,
+    hipLaunchKernelGGL(crowded_sort_decode, dim3(crowd_grid ? crowd_grid : (uint32_t)s->n_cu), dim3(1024), 0, st, s->tmp_hi, off, P.shift, P.try_bits,
                        P.low_bits, g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out,
                        sort_crowded(s));
     MP_HIP_CHECK(hipGetLastError());

@@ -1380,8 +1380,12 @@ __device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, 
 template <bool kGap = false>
 __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
     const uint32_t bit = pk & 15u;
-    if (!((rw.x >> bit) & 1u)) return false;
+    const uint32_t present = (rw.x >> bit) & 1u;
+#ifdef MP_KGRP_BRANCHY
+    if (!present) return false;
+#endif
     if constexpr (kGap) {
+        if (!present) return false;
         const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
         if (j >= kKgrpFields) return true;
         const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
@@ -1401,6 +1405,7 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         return (uint32_t)__popc(m) <= (uint32_t)a.N && ((m >> (2u * a.gap_post)) != 0u || (pk >> 31) != 0u);
     }
     if (a.kgrp_wild) {
+        if (!present) return false;
         if (pk >> 31) return true;
         const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
         if (j >= kKgrpWildFields) return true;
@@ -1409,6 +1414,26 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
         return (uint32_t)__popc((x | (x >> 1)) & 0x555u & ~(field >> 12)) <= (uint32_t)a.N;
     }
+#ifndef MP_KGRP_BRANCHY
+    // Branch-free (round 4): every form is computed and selected, so the probe pass has no
+    // exec-mask branches (the branchy form spent ~45-60 instructions per pass, most of them
+    // SALU exec juggling, ISA of scan_kernel<1,false,2,true,0,true,false>).
+    const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
+    const uint64_t w64 = ((uint64_t)rw.y << 32) | rw.x;
+    const uint32_t field = (uint32_t)(w64 >> (16u + 16u * min(j, kKgrpFields - 1u))) & 0xFFFFu;
+    // one plain record: bases W..W+F-1 within N
+    const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
+    const uint32_t s_ok = (uint32_t)__popc((x | (x >> 1)) & 0x55555555u) <= (uint32_t)a.N;
+    // two records: the window's bases W..W+2 (the top 3 of its F) against each record's
+    const uint32_t g3 = (pk >> (4u + 2u * (a.kgrp_F - 3u))) & 63u;
+    const uint32_t x0 = g3 ^ ((field >> 6) & 63u), x1 = g3 ^ (field & 63u);
+    const uint32_t p_ok = ((uint32_t)__popc((x0 | (x0 >> 1)) & 0x15u) <= (uint32_t)a.N) |
+                          ((uint32_t)__popc((x1 | (x1 >> 1)) & 0x15u) <= (uint32_t)a.N);
+    const uint32_t flag = (field >> 15) & 1u, pair = (field >> 14) & 1u;
+    static_assert(kKgrpFlag == 0x8000u && kKgrpPair == 0x4000u, "field flag bits");
+    const uint32_t ok = (uint32_t)(j >= kKgrpFields) | (flag & s_ok) | ((flag ^ 1u) & ((pair ^ 1u) | p_ok));
+    return (present & ok) != 0u;
+#else
     const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
     if (j >= kKgrpFields) return true;
     const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
@@ -1421,6 +1446,7 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
     }
     const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
     return __popc((x | (x >> 1)) & 0x55555555u) <= a.N;
+#endif
 }
 
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
@@ -1568,13 +1594,14 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     // stage the seed prefilter in LDS (once per persistent workgroup): all eight 16-B loads of
     // a thread in flight before the first LDS store (one L2 round trip, not eight)
     {
-        static_assert(kLdsFilterWords / 4 == 8 * kBlock, "eight uint4 per thread");
+        constexpr int kStage = (int)(kLdsFilterWords / 4 / kBlock);  // eight uint4 per thread (128 KiB)
+        static_assert(kLdsFilterWords / 4 == kStage * kBlock, "whole uint4 rows per thread");
         const uint4* src = reinterpret_cast<const uint4*>(a.lfilt);
-        uint4 v[8];
+        uint4 v[kStage];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = src[threadIdx.x + k * kBlock];
+        for (int k = 0; k < kStage; ++k) v[k] = src[threadIdx.x + k * kBlock];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) reinterpret_cast<uint4*>(s_lf)[threadIdx.x + k * kBlock] = v[k];
+        for (int k = 0; k < kStage; ++k) reinterpret_cast<uint4*>(s_lf)[threadIdx.x + k * kBlock] = v[k];
     }
     __syncthreads();
 

@@ -5,6 +5,8 @@ merpcr_amd/csrc/mp_search.hip: the insertion goes right before the anchor (which
 occur exactly once).  Hit counts of a variant are meaningless; only its scan time is.
 
   1   level 1 alone (genome stream, W-mers, validity smear, LDS prefilter)
+  5   the genome stream, validity smear and scheduler alone (no LDS probe): the part of a
+      scan pass two seed scans could share (the c5 single-pass question)
   2   level 1 and the positives' offset list
   3   level 1, the list and the level-2 loads (consumed, nothing more)
   30  no super-step loop (launch, LDS staging, statistics)
@@ -28,7 +30,8 @@ _L2 = "                constexpr int kP = (kSeedQR + 63) / 64;\n"
 _L3 = "                if constexpr (kRkf) {\n                    // the few seeds that pass the key groups"
 _LOOP = ("    while (ss < n_supers) {\n        const SeqSpan sp = pf;\n        const uint64_t sbase = pf_sbase;\n"
          "        const uint32_t n = pf_n;\n        SuperRegs R;")
-_STAGE = "    {\n        static_assert(kLdsFilterWords / 4 == 8 * kBlock, \"eight uint4 per thread\");\n"
+_STAGE = "    {\n        constexpr int kStage = (int)(kLdsFilterWords / 4 / kBlock);  // eight uint4 per thread (128 KiB)\n"
+_PROBE = "            const uint32_t rem = lds_probe32<kK, kGap>(s_lf, d0, d1, d2, shw, a.gap_at, a.gap_len) & okm;\n"
 
 _LP = "    if (__any(lp)) {\n"
 _TODO = "    uint64_t todo = __ballot(keep && !lp);\n"
@@ -57,6 +60,10 @@ VARIANTS = {
               "                wave_sync();\n                r0 += kSeedQR;\n                continue;\n")],
     3: [(_L3, "                for (int q = 0; q < kP; ++q) ncand += rw[q].x & 1u;  // ablation 3\n"
               "                r0 += kSeedQR;\n                continue;\n")],
+    5: [(_PROBE, "            if constexpr (kMode == 1) {  // ablation 5\n"
+                 "                ncand += (uint32_t)__popc(okm ^ d0 ^ d1 ^ d2);\n"
+                 "                if (nx < n_supers) { locate(nx); words(nx, nw0, nw1, niv); }\n"
+                 "                ss = nx;\n                continue;\n            }\n")],
     30: [(_LOOP, "    ss = n_supers;  // ablation 30\n")],
     31: [(_LOOP, "    ss = n_supers;  // ablation 31\n"), (_STAGE, "    if (false)  // ablation 31\n")],
     40: [(_T_ENTRY, "    const uint64_t wt0 = wall_clock64();  // ablation 40\n"),
