@@ -256,6 +256,20 @@ int mp_fasta_record(void* fasta, uint64_t i, const uint8_t** defline, uint64_t* 
 /* 1 when record i's filtered sequence is ASCII (no U+017F), else 0. */
 int mp_fasta_record_ascii(void* fasta, uint64_t i, int32_t* ascii);
 void mp_fasta_destroy(void* fasta);
+/* Device ingestion of an ASCII FASTA file (the same records as mp_fasta_load): the raw
+ * bytes are uploaded to `device` and the header search, the keep-set filter
+ * (fasta.py:42-66) and the compaction run there; the filtered sequences stay in device
+ * memory, record after record (mp_fasta_device_info's dev_bases), ready for
+ * mp_genome_put_device.  *ascii = 0 and no handle when the file holds a byte >= 0x80 (or
+ * more than 2^20 header lines): read it with mp_fasta_load. */
+int mp_fasta_load_device(const char* path, int32_t device, void* stream, void** fasta_out, int32_t* ascii);
+int mp_fasta_device_info(void* fasta, uint64_t* n_records, uint64_t* total_bases, const uint8_t** dev_bases);
+/* Record i: its stripped defline and its bases' offset and length in dev_bases. */
+int mp_fasta_device_record(void* fasta, uint64_t i, const uint8_t** defline, uint64_t* defline_len,
+                           uint64_t* offset, uint64_t* length);
+/* Bases [offset, offset + n) of dev_bases into host memory. */
+int mp_fasta_device_read(void* fasta, uint64_t offset, uint64_t n, uint8_t* host_dst);
+void mp_fasta_device_destroy(void* fasta);
 
 /* ---- STS file (replaces MerPCR.load_sts_file and helpers, engine.py:193-359) --
  * Parses `path` into the oriented records of the reference's sts_records, in order,

@@ -13,7 +13,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIBDIR, "libmerpcr_hip.so")
 SOURCES = ["mp_table.hip", "mp_genome.hip", "mp_search.hip", "mp_sort.hip", "mp_order.hip", "mp_multi.hip", "mp_fasta.hip",
-           "mp_format.hip", "mp_sts.hip"]
+           "mp_fasta_dev.hip", "mp_format.hip", "mp_sts.hip"]
 HEADERS = ["mp_internal.h", "mp_text.h", os.path.join("..", "..", "include", "merpcr_hip.h")]
 ARCH = os.environ.get("MERPCR_OFFLOAD_ARCH", "gfx950")
 # Per-source flags.  mp_search.hip aggregates its atomics by hand (lane 0 of a wave); the

@@ -39,6 +39,8 @@ EXPORTS = (
     "mp_multi_device_search", "mp_multi_timing", "mp_multi_destroy",
     "mp_comm_unique_id", "mp_comm_create", "mp_comm_gather_hits", "mp_comm_destroy",
     "mp_fasta_load", "mp_fasta_load_parallel", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record_ascii", "mp_fasta_record", "mp_fasta_destroy",
+    "mp_fasta_load_device", "mp_fasta_device_info", "mp_fasta_device_record", "mp_fasta_device_read",
+    "mp_fasta_device_destroy",
     "mp_format_hits",
     "mp_sts_parse", "mp_sts_info", "mp_sts_arrays", "mp_sts_record_texts", "mp_sts_destroy",
 )
@@ -138,6 +140,12 @@ def _sig(lib):
     lib.mp_fasta_record.argtypes = [P, c_uint64, POINTER(c_void_p), u64p, POINTER(c_void_p), u64p]
     lib.mp_fasta_destroy.argtypes = [P]
     lib.mp_fasta_destroy.restype = None
+    lib.mp_fasta_load_device.argtypes = [c_char_p, c_int32, P, POINTER(c_void_p), POINTER(c_int32)]
+    lib.mp_fasta_device_info.argtypes = [P, u64p, u64p, POINTER(c_void_p)]
+    lib.mp_fasta_device_record.argtypes = [P, c_uint64, POINTER(c_void_p), u64p, u64p, u64p]
+    lib.mp_fasta_device_read.argtypes = [P, c_uint64, c_uint64, P]
+    lib.mp_fasta_device_destroy.argtypes = [P]
+    lib.mp_fasta_device_destroy.restype = None
     lib.mp_sts_parse.argtypes = [c_char_p, c_int32, ctypes.c_int64, POINTER(c_void_p)]
     lib.mp_sts_info.argtypes = [P, POINTER(c_int32), u64p]
     lib.mp_sts_arrays.argtypes = [P, POINTER(c_void_p)]
@@ -604,6 +612,79 @@ class _FastaHandle:
                 self._h = None
         except Exception:
             pass
+
+
+class _FastaDeviceHandle:
+    """Owner of a device-ingested FASTA (mp_fasta_load_device): its filtered bases stay in
+    device memory until the last DeviceSpan over them is gone."""
+
+    def __init__(self, h, device: int):
+        self._h = h
+        self.device = device
+
+    def read(self, offset: int, n: int) -> bytes:
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            check(lib().mp_fasta_device_read(self._h, offset, n, ptr(out)))
+        return out.tobytes()
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().mp_fasta_device_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class DeviceSpan:
+    """n bases of a device-ingested FASTA at device address ptr (device `device`): what
+    mp_genome_put_device packs without a host copy.  Slices are spans; host() copies."""
+
+    __slots__ = ("owner", "offset", "n", "base")
+
+    def __init__(self, owner: _FastaDeviceHandle, base: int, offset: int, n: int):
+        self.owner, self.base, self.offset, self.n = owner, base, offset, n
+
+    @property
+    def device(self) -> int:
+        return self.owner.device
+
+    @property
+    def ptr(self) -> int:
+        return self.base + self.offset
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, sl):
+        start, stop, step = sl.indices(self.n)
+        assert step == 1, "contiguous slices only"
+        return DeviceSpan(self.owner, self.base, self.offset + start, max(0, stop - start))
+
+    def host(self) -> bytes:
+        return self.owner.read(self.offset, self.n)
+
+
+def fasta_read_device(path: str, device: int, stream=None):
+    """[(defline, DeviceSpan)] of an ASCII FASTA file ingested on `device`
+    (mp_fasta_load_device), or None when the file needs the host reader (a byte >= 0x80)."""
+    h, asc = c_void_p(), c_int32()
+    check(lib().mp_fasta_load_device(os.fsencode(path), device, c_void_p(stream or 0), ctypes.byref(h),
+                                     ctypes.byref(asc)))
+    if not asc.value:
+        return None
+    if not h.value:  # an empty file or one without a header line: no record
+        return []
+    owner = _FastaDeviceHandle(h, device)
+    n, total, base = c_uint64(), c_uint64(), c_void_p()
+    check(lib().mp_fasta_device_info(h, ctypes.byref(n), ctypes.byref(total), ctypes.byref(base)))
+    out = []
+    dp, dl, off, ln = c_void_p(), c_uint64(), c_uint64(), c_uint64()
+    for i in range(n.value):
+        check(lib().mp_fasta_device_record(h, i, ctypes.byref(dp), ctypes.byref(dl), ctypes.byref(off), ctypes.byref(ln)))
+        out.append((ctypes.string_at(dp, dl.value).decode("ascii"), DeviceSpan(owner, base.value or 0, off.value, ln.value)))
+    return out
 
 
 def _csr(items):

@@ -8,6 +8,7 @@ on success, 1 on any failure (cli.py:217-266).
 import argparse
 import logging
 import sys
+import threading
 from typing import List
 
 from .core.engine import (DEFAULT_IUPAC_MODE, DEFAULT_MARGIN, DEFAULT_MISMATCHES, DEFAULT_PCR_SIZE,
@@ -112,7 +113,20 @@ def main(argv: List[str] = None) -> int:
         if not eng.load_sts_file(args.sts_file):
             logger.error(f"Failed to load STS file: {args.sts_file}")
             return 1
-        records = eng.load_fasta_file(args.fasta_file)
+        # the device tables (and the HIP runtime's start) beside the FASTA read
+        from . import _native
+        prep = None
+        try:
+            _native.lib()  # loaded once, here, before the two threads use it
+            prep = threading.Thread(target=eng.prepare_device, daemon=True)
+            prep.start()
+        except Exception:  # noqa: BLE001 -- no library: search() reports it in its turn
+            prep = None
+        try:
+            records = eng.load_fasta_file(args.fasta_file)
+        finally:
+            if prep is not None:
+                prep.join()
         if not records:
             logger.error(f"Failed to load FASTA file: {args.fasta_file}")
             return 1

@@ -483,8 +483,10 @@ class MerPCR:
         return True
 
     def load_fasta_file(self, filename: str) -> List[FASTARecord]:
-        """FASTA records with the reference's filter (io/fasta.py:18-71)."""
-        return FASTALoader.load_file(filename)
+        """FASTA records with the reference's filter (io/fasta.py:18-71).  A single-device
+        engine ingests large ASCII files on its GPU (the sequences stay there for the
+        search; FASTALoader.load_file's device form)."""
+        return FASTALoader.load_file(filename, device=self.device if len(self.devices) == 1 else None)
 
     # ------------------------------------------------------------------ device
     def _params(self):
@@ -549,6 +551,19 @@ class MerPCR:
             self._extra_tables = {}
         return self._dev_table
 
+    def prepare_device(self):
+        """Build the seed table(s) on the device now -- the HIP runtime starts with them --
+        so that search() finds them ready.  The CLI runs this on a thread beside the FASTA
+        read (both are native calls that release the GIL).  A failure is left for search() to
+        raise at its own point of the run, as without the head start."""
+        try:
+            if len(self.devices) > 1:
+                self.device_tables()
+            else:
+                self.device_table()
+        except Exception:  # noqa: BLE001 -- search() repeats the call and raises it there
+            pass
+
     def device_tables(self) -> list:
         """One seed table per entry of self.devices (a repeated device shares its table)."""
         from .. import _native
@@ -584,6 +599,10 @@ class MerPCR:
         reader hands over its ASCII bytes as they are (no str round trip)."""
         out = []
         for r in fasta_records:
+            span = _device_span(r)
+            if span is not None and span.device == self.device and len(self.devices) == 1:
+                out.append(span)  # packed where it is (mp_genome_put_device)
+                continue
             raw = _raw_ascii(r)
             out.append(np.frombuffer(raw, dtype=np.uint8) if raw is not None else
                        self.encode_sequences([r.sequence])[0])
@@ -697,9 +716,13 @@ class MerPCR:
         if len(self.devices) > 1:
             return self._search_multi(data)
         genome, search = self._device_search([len(d) for d in data])
+        from .._native import DeviceSpan
         for i, d in enumerate(data):
             if len(d):
-                genome.put(i, d)
+                if isinstance(d, DeviceSpan):
+                    genome.put_device(i, d.ptr, len(d))
+                else:
+                    genome.put(i, d)
         genome.seal()
         t0 = time.time()
         n = search.run()
@@ -815,7 +838,15 @@ def _raw_ascii(rec):
     return f() if f is not None else None
 
 
+def _device_span(rec):
+    f = getattr(rec, "device_span", None)
+    return f() if f is not None else None
+
+
 def _seq_len(rec) -> int:
+    span = _device_span(rec)
+    if span is not None:
+        return len(span)
     raw = _raw_ascii(rec)
     return len(raw) if raw is not None else len(rec.sequence)
 

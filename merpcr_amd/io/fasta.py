@@ -90,22 +90,71 @@ class ReaderRecord(FASTARecord):
         return None
 
 
+class DeviceRecord(ReaderRecord):
+    """A FASTARecord whose filtered sequence lives in device memory (mp_fasta_load_device):
+    the search packs it there (mp_genome_put_device), and the str or bytes of the
+    reference's API are copied to the host only when asked for."""
+
+    def __init__(self, defline: str, span):
+        self._span = span
+        super().__init__(defline, None, True)
+
+    def device_span(self):
+        """The sequence's DeviceSpan while it is unmodified, else None."""
+        return self._span if self._str is None else None
+
+    def raw_ascii(self):
+        if self._str is None and self._raw is None and self._span is not None:
+            self._raw = self._span.host()
+        return super().raw_ascii()
+
+    @property
+    def sequence(self) -> str:
+        if self._str is None:
+            self.raw_ascii()
+        return ReaderRecord.sequence.fget(self)
+
+    @sequence.setter
+    def sequence(self, value):
+        if value is not None:
+            self._span = None
+        ReaderRecord.sequence.fset(self, value)
+
+
+# Files of at least this many bytes are ingested on the device when the caller names one
+# (MerPCR's single-device search); smaller ones are read on the host.
+DEVICE_MIN_BYTES = int(os.environ.get("MERPCR_DEVICE_FASTA_MIN", str(16 << 20)))
+
+
 class FASTALoader:
     """Loads FASTA files into FASTARecord lists (reference: io/fasta.py:15-71)."""
 
     @staticmethod
-    def load_file(filename: str, _chunk_bytes: int = 0) -> List[FASTARecord]:
+    def load_file(filename: str, _chunk_bytes: int = 0, device=None) -> List[FASTARecord]:
+        """`device`: ingest an ASCII file of DEVICE_MIN_BYTES or more on that GPU
+        (mp_fasta_load_device, the same records; the sequences stay in device memory)."""
         if not _utf8_locale():
             return FASTALoader.load_file_py(filename)
         from .. import _native
         start = time.time()
-        if os.path.getsize(filename) == 0:
+        size = os.path.getsize(filename)
+        if size == 0:
             logger.error(f"FASTA file '{filename}' is empty")
             return []
         logger.info(f"Reading FASTA file: {filename}")
-        records = []
-        for defline, seq, ascii in _native.fasta_read(filename, _chunk_bytes, with_ascii=True):
-            records.append(ReaderRecord(defline, seq, ascii))
+        records = None
+        if device is not None and not _chunk_bytes and size >= DEVICE_MIN_BYTES:
+            try:
+                got = _native.fasta_read_device(filename, int(device))
+            except _native.NativeError as e:  # no usable device: the host reader
+                logger.debug(f"device FASTA ingestion unavailable ({e}); reading on the host")
+                got = None
+            if got is not None:
+                records = [DeviceRecord(defline, span) for defline, span in got]
+        if records is None:
+            records = []
+            for defline, seq, ascii in _native.fasta_read(filename, _chunk_bytes, with_ascii=True):
+                records.append(ReaderRecord(defline, seq, ascii))
         logger.info(f"Loaded {len(records)} sequences in {time.time() - start:.2f} seconds")
         return records
 
