@@ -149,8 +149,9 @@ typedef struct mp_search_options {
                                    filtered rank groups' primer-base filter */
     int32_t no_split;           /* 1: W 7..9 tables keep the dense scan, not the split seeds
                                    (two exact-seed scans, see mp_internal.h kSplitSeed) */
-    int32_t no_fuse_tails;      /* 1: bucket-tail references expanded by their own kernel
-                                   (tail_kernel) instead of inside the pair check */
+    int32_t fuse_tails;         /* 1: bucket-tail references opened inside the pair check
+                                   instead of by their own kernel (tail_kernel); one-table
+                                   runs only.  Off by default: no gain measured */
 } mp_search_options;
 /* Replace the handle's options (reallocating the lists to the given capacities). */
 int mp_search_set_options(void* search, const mp_search_options* opt);

@@ -64,7 +64,7 @@ class MPSearchOptions(ctypes.Structure):
     _fields_ = [("tails", c_int32), ("no_defer", c_int32), ("no_dense", c_int32), ("sort", c_int32),
                 ("sort_bucket_bits", c_int32), ("pair_blocks_per_cu", c_int32),
                 ("hit_cap", c_uint64), ("surv_cap", c_uint64), ("tail_cap", c_uint64),
-                ("no_rank_filter", c_int32), ("no_split", c_int32), ("no_fuse_tails", c_int32)]
+                ("no_rank_filter", c_int32), ("no_split", c_int32), ("fuse_tails", c_int32)]
 
 
 HIT_DTYPE = np.dtype([("pos1", "<u8"), ("pos2", "<u8"), ("seq", "<u4"), ("rec", "<u4")])
@@ -79,7 +79,24 @@ class NativeError(RuntimeError):
 _lib = None
 
 
+class _Tolerant:
+    """A/B runs against older variant libraries (MERPCR_LIB): a symbol the library lacks
+    takes its signature in a dummy, and calling it fails as a missing symbol would."""
+
+    def __init__(self, lib):
+        self._lib = lib
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._lib, name)
+        except AttributeError:
+            import types
+            return types.SimpleNamespace()
+
+
 def _sig(lib):
+    if os.environ.get("MERPCR_LIB"):
+        lib = _Tolerant(lib)
     P = c_void_p
     u64p = POINTER(c_uint64)
     lib.mp_abi_version.restype = c_int32
@@ -320,12 +337,12 @@ class Search:
 
     def set_options(self, tails="auto", defer=True, dense=True, sort="auto", sort_bucket_bits=0,
                     pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True, split=True,
-                    fuse_tails=True):
+                    fuse_tails=False):
         """Kernel-path selection and initial list capacities (mp_search_set_options);
         the defaults are the library's automatic choices."""
         o = MPSearchOptions(MP_TAILS[tails], 0 if defer else 1, 0 if dense else 1, MP_SORT[sort],
                             sort_bucket_bits, pair_blocks_per_cu, hit_cap, surv_cap, tail_cap,
-                            0 if rank_filter else 1, 0 if split else 1, 0 if fuse_tails else 1)
+                            0 if rank_filter else 1, 0 if split else 1, 1 if fuse_tails else 0)
         check(lib().mp_search_set_options(self._h, ctypes.byref(o)))
 
     def set_stage_timing(self, on: bool):

@@ -1381,7 +1381,7 @@ template <bool kGap = false>
 __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
     const uint32_t bit = pk & 15u;
     const uint32_t present = (rw.x >> bit) & 1u;
-#ifdef MP_KGRP_BRANCHY
+#ifndef MP_KGRP_BRANCHFREE
     if (!present) return false;
 #endif
     if constexpr (kGap) {
@@ -1414,7 +1414,7 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
         return (uint32_t)__popc((x | (x >> 1)) & 0x555u & ~(field >> 12)) <= (uint32_t)a.N;
     }
-#ifndef MP_KGRP_BRANCHY
+#ifdef MP_KGRP_BRANCHFREE
     // Branch-free (round 4): every form is computed and selected, so the probe pass has no
     // exec-mask branches (the branchy form spent ~45-60 instructions per pass, most of them
     // SALU exec juggling, ISA of scan_kernel<1,false,2,true,0,true,false>).
@@ -1481,6 +1481,9 @@ constexpr uint32_t kSChunkShort = 128;
 // super-steps at ~11 us each and waves 0-3 did 60 at ~5 us; with fixed chunks of 4 and one
 // chunk claimed ahead the young waves ended 20 us after the old ones and the last wave 47 us
 // after the first.
+#ifndef MP_STEAL_MIN
+#define MP_STEAL_MIN 1u
+#endif
 struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives beside the scan's registers
     uint32_t lo, hi, nw, end;  // XCD group range, waves of the group, end of the current chunk
     uint32_t S;                // end of the static first chunks: dynamic positions count from here
@@ -1533,7 +1536,7 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         // with every lane active, so the first active lane is lane 0 and the broadcast is a
         // readfirstlane (the scheduler state then stays in scalar registers)
         uint32_t st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);
-#ifndef MP_NO_STEAL
+#ifdef MP_STEAL
         while (kSteal && st >= hi) {  // this group's range is claimed out: help a group that is behind
             if (!steal(n_supers, kW, lane)) break;
             claim(lane);
@@ -1570,7 +1573,11 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
             uint32_t cur = 0;
             if (lane == 0) cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur);
-            if (s0 + cur < h) {
+            // only a group with more than MP_STEAL_MIN super-steps per wave of its own left:
+            // below that its waves finish it as soon, and stealers' atomics on its counter
+            // (same-address atomics serialise, ~88 per us) would only slow its own claims
+            const uint32_t own = ((gridDim.x - x + 7u) >> 3) * (uint32_t)kW;
+            if (s0 + cur + MP_STEAL_MIN * own < h) {
                 lo = x;
                 hi = h;
                 S = s0;
@@ -2312,12 +2319,13 @@ constexpr int kPairBlock = kPairWaves * 64;
 // per run on 1/8 of c3) that pair_kernel waited out.  One pair-check call site per wave loop
 // keeps the kernel within its 128 VGPRs (two inlined copies spilled to scratch).
 constexpr uint32_t kFuseQ = 63;  // the LDS left beside the stages: 1008 B per wave
+template <bool kFuse>
 __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
-    const uint64_t n_refs = a.fuse_tails ? umin64(a.counters[a.tail_ctr], a.tails_cap) : 0ull;
+    const uint64_t n_refs = kFuse ? umin64(a.counters[a.tail_ctr], a.tails_cap) : 0ull;
     __shared__ HitStage s_st[kPairWaves];
     __shared__ uint64_t s_pst[kPairWaves][kPSlots * MP_PBATCH];
-    __shared__ uint4 s_fq[kPairWaves][kFuseQ];
+    __shared__ uint4 s_fq[kPairWaves][kFuse ? kFuseQ : 1];
     const int lane = threadIdx.x & 63;
     HitStage& S = s_st[threadIdx.x >> 6];
     if (lane == 0) S.n = 0;
@@ -2348,6 +2356,17 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
         const uint64_t nw_x = (uint64_t)((gridDim.x - x + g - 1u) / g) * kPairWaves;  // waves of this group
         uint64_t li = (uint64_t)(blockIdx.x / g) * kPairWaves + (threadIdx.x >> 6);
         uint64_t* pst = s_pst[threadIdx.x >> 6];
+        if constexpr (!kFuse) {  // the survivor list alone: check a batch, then claim the next
+            while (li < ns) {
+                const uint64_t i = (lo_b + li) * db + (uint64_t)lane;
+                uint4 v = kEmptySurv;
+                if ((uint32_t)lane < db && i < n_surv) v = a.surv[i];
+                pair_check_lanes(a, v, db, lane, S, pst);
+                unsigned long long c = 0;
+                if (lane == 0) c = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
+                li = nw_x + (uint64_t)__shfl((long long)c, 0, 64);
+            }
+        } else {
         uint4* Q = s_fq[threadIdx.x >> 6];
         uint32_t qn = 0, ncand = 0, nsurv = 0;  // queue fill (wave-uniform), statistics
         // the open reference batch: each lane's reference and the next record step j
@@ -2412,7 +2431,8 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
             }
             if (batch) pair_check_lanes(a, v, batch, lane, S, pst);
         }
-        if (a.fuse_tails) add_stats(a, ncand, nsurv, lane);
+        add_stats(a, ncand, nsurv, lane);
+        }
     }
     // the block's stages leave with one returning atomic: one per wave at the end of the
     // kernel would serialise ~4k atomics on the hit counter (~88 per microsecond)
@@ -2584,7 +2604,7 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
             s->n_cu <= 0)
             s->n_cu = 256;
         int occ = 0;  // persistent pair check: every resident block slot once
-        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel, kPairBlock, 0) == hipSuccess && occ > 0)
+        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel<false>, kPairBlock, 0) == hipSuccess && occ > 0)
                              ? (uint32_t)occ : 1u;
         s->dense_lds = dense_lds_of(t);
         if (t->split_rest) s->dense_lds = std::max(s->dense_lds, dense_lds_of(t->split_rest));
@@ -2777,7 +2797,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
     if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
     // one-table runs open their bucket-tail references inside pair_kernel (fused_ref_batch)
-    bool fuse = !s->opt.no_fuse_tails;
+    bool fuse = s->opt.fuse_tails != 0;
     if (!use_split(s)) {
         bool tail = false;
         const int rc = launch_scan(s, t, a, tiles, st, &tail);
@@ -2818,7 +2838,8 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
                                                            : s->pair_per_cu;
     ScanArgs pa = a;
     pa.fuse_tails = fuse ? 1u : 0u;
-    hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, pa);
+    if (fuse) hipLaunchKernelGGL(pair_kernel<true>, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, pa);
+    else hipLaunchKernelGGL(pair_kernel<false>, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, pa);
     MP_HIP_CHECK(hipGetLastError());
     MID_EVENT(hipEventRecord(s->ev2, st));
     if (mode < 2) {  // hit order on the device count: no host round trip before it; its offsets

@@ -532,7 +532,9 @@ def _multi_case(W, n_sts, seed):
 
 
 @pytest.mark.parametrize("W,n_sts,opts", [(8, 3000, {}), (10, 3000, {}), (11, 6000, {}),
-                                          (11, 6000, dict(tails="inline")), (11, 6000, dict(defer=False))])
+                                          (11, 6000, dict(tails="inline")), (11, 6000, dict(defer=False)),
+                                          # bucket tails opened inside the pair check (fuse_tails)
+                                          (11, 6000, dict(fuse_tails=True)), (12, 6000, dict(fuse_tails=True))])
 def test_sharded_ranges_all_paths(W, n_sts, opts):
     """Owned (seq, k) ranges partition the hit list exactly through every scan path:
     dense_kernel (W=8), the exact-LDS scan (W=10), the ranked drain with full-head deferral
