@@ -110,23 +110,30 @@ def main(argv: List[str] = None) -> int:
                      max_sts_line_length=args.max_sts_line_length, device=args.device,
                      emulate_chunks=args.emulate_chunks,
                      devices=[(args.device or 0) + i for i in range(args.gpus)] if args.gpus > 1 else None)
+        # the HIP runtime starts on a thread beside the STS parse, and the device tables are
+        # built beside the FASTA read (native calls release the GIL)
+        from . import _native
+        warm = None
+        try:
+            _native.lib()  # loaded once, here, before the threads use it
+            warm = threading.Thread(target=_native.device_count, daemon=True)
+            warm.start()
+        except Exception:  # noqa: BLE001 -- no library: search() reports it in its turn
+            warm = None
         if not eng.load_sts_file(args.sts_file):
             logger.error(f"Failed to load STS file: {args.sts_file}")
             return 1
-        # the device tables (and the HIP runtime's start) beside the FASTA read
-        from . import _native
         prep = None
-        try:
-            _native.lib()  # loaded once, here, before the two threads use it
+        if warm is not None:
             prep = threading.Thread(target=eng.prepare_device, daemon=True)
             prep.start()
-        except Exception:  # noqa: BLE001 -- no library: search() reports it in its turn
-            prep = None
         try:
             records = eng.load_fasta_file(args.fasta_file)
         finally:
             if prep is not None:
                 prep.join()
+            if warm is not None:
+                warm.join()
         if not records:
             logger.error(f"Failed to load FASTA file: {args.fasta_file}")
             return 1
