@@ -87,6 +87,19 @@ struct DevRec {            // one oriented STS record, 32 bytes
 };
 static_assert(sizeof(DevRec) == 32, "DevRec layout");
 
+// The pair check's view of one record in one 128-B line (round 4): its DevRec, its tie
+// rank and the accept planes of both primers' first 32 bases.  Three random record-indexed
+// loads per survivor (recs, rank, two plane chunks) become one line; on c4 (2.8M survivors)
+// those loads missed L2 and the pair kernel fetched ~2 GB per launch.
+struct alignas(128) PairRec {
+    DevRec d;
+    uint32_t rank, pad0;
+    uint64_t p1q[4];       // planes of primer-1 bases [0, 32)
+    uint64_t p2q[4];       // planes of primer-2 bases [0, 32)
+    uint64_t pad1[3];
+};
+static_assert(sizeof(PairRec) == 128, "PairRec is one 128-B line");
+
 struct Entry {             // one oriented record, 32 bytes
     uint64_t code;         // 2-bit code of primer-1 bases [0, 32) (big-endian slots)
     uint64_t pmask;        // even bits: base is a single A/C/G/T for the compare rule
@@ -156,6 +169,7 @@ struct Table {
     uint32_t* rank = nullptr;      // rec -> position in (hash_off, rec) order
     uint32_t* inv_rank = nullptr;  // position -> rec
     uint64_t* planes = nullptr;    // 4 u64 per 32-base primer chunk
+    PairRec* prec = nullptr;       // per record: DevRec, rank, both primers' first plane chunks
     uint64_t planes_words = 0;
     uint8_t* pchars = nullptr;
     uint32_t rank_bits = 1;

@@ -80,6 +80,7 @@ struct ScanArgs {
     const DevRec* recs;
     const uint32_t* rank;
     const uint64_t* planes;
+    const PairRec* prec;      // the pair check's per-record lines (Table::prec)
     const uint8_t* pchars;
     int W, M, N, X, I;
     int has_u;              // genome holds U: exception bits come from gexc, not ginv
@@ -272,14 +273,15 @@ __device__ __forceinline__ bool chunk_ok(const ScanArgs& a, uint64_t G, uint32_t
 // one primer: protected positions are i >= L-X on the '+' strand (plus == true)
 // and i < X on the '-' strand; any protected mismatch or more than N fails.
 __device__ __forceinline__ bool primer_ok(const ScanArgs& a, uint64_t gpos, uint32_t L, uint32_t pl, uint32_t ch,
-                                          bool plus) {
+                                          bool plus, const uint64_t* __restrict__ q0 = nullptr) {
     int mm = 0;
     for (uint32_t c = 0; c < L; c += 32) {
         const int len = (int)min(32u, L - c);
         const uint64_t G = ext2(a.g2, gpos + c);
         const uint32_t ex = (uint32_t)(ext1(a.gexc, gpos + c) >> 32);
         const uint32_t wl = a.I && ex ? (uint32_t)(ext1(a.gwild, gpos + c) >> 32) : 0u;
-        const uint64_t* P = a.planes + (uint64_t)(pl + (c >> 5)) * 4;
+        // chunk 0's planes from the record's pair line (q0) when given
+        const uint64_t* P = c == 0 && q0 ? q0 : a.planes + (uint64_t)(pl + (c >> 5)) * 4;
         if (!chunk_ok(a, G, ex, P[0], P[1], P[2], P[3], gpos + c, ch + c, len, c, L, plus, mm, wl)) return false;
     }
     return true;
@@ -430,11 +432,12 @@ __device__ void pair_check_lanes(const ScanArgs& a, uint4 v, uint32_t batch, int
     uint32_t n = 0;
     DevRec r{};
     uint32_t rk = 0;
+    const PairRec* pr = a.prec + rec;  // one 128-B line: the record, its rank, both primers' chunk-0 planes
     if (keep) {
         sbase = a.seq_base[v.w];
         n = (uint32_t)a.seq_len[v.w];
-        r = a.recs[rec];
-        rk = a.rank[rec];
+        r = pr->d;
+        rk = pr->rank;
     }
     const uint32_t k = (uint32_t)(gk - sbase);
     keep = keep && n - k - r.l1 >= r.l2;
@@ -490,13 +493,13 @@ __device__ void pair_check_lanes(const ScanArgs& a, uint4 v, uint32_t batch, int
                     any |= ew[t] & ((~0ull >> s0) & ~(s1 >= 63u ? 0ull : (~0ull >> (s1 + 1u))));
             }
             clean = any == 0;
-            const uint64_t* pp = a.planes + (uint64_t)r.p2_pl * 4;
+            const uint64_t* pp = pr->p2q;  // primer 2 <= 32 bases here: its planes are chunk 0
 #pragma unroll
             for (int t = 0; t < 4; ++t) pst[(kPW + kPE + t) * MP_PBATCH + lane] = pp[t];
         }
     }
     wave_sync_lds();
-    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);
+    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true, pr->p1q);
     // Lane-parallel tries: a survivor whose stretch holds no exception base takes its tries
     // in its own lane -- a 32-base window slid one base per try through the staged words,
     // primer 2 compared by XOR/popcount (plain) or the accept planes -- one wave-wide pass
@@ -3125,7 +3128,7 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         a.tail_ctr = 4;
         a.sched_base = kSchedBase;
         a.recs = t->recs; a.rank = t->rank;
-        a.planes = t->planes; a.pchars = t->pchars;
+        a.planes = t->planes; a.pchars = t->pchars; a.prec = t->prec;
         a.M = t->prm.margin; a.N = t->prm.mismatches;
         a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
         a.g_lo = g_lo; a.g_hi = g_hi;

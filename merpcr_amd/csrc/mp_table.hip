@@ -53,7 +53,7 @@ static void free_table(Table* t) {
     free_table(t->split_a); free_table(t->split_b); free_table(t->split_rest);
     hipFree(t->dents12);
     hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->kgrp); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
-    hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes);
+    hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes); hipFree(t->prec);
     hipFree(t->pchars);
     delete t;
 }
@@ -665,6 +665,20 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         if ((rc = upload(&t->rank, rank.data(), rank.size(), &bytes))) break;
         if ((rc = upload(&t->inv_rank, order.data(), order.size(), &bytes))) break;
         planes.push_back(0); planes.push_back(0); planes.push_back(0); planes.push_back(0);
+        {
+            std::vector<PairRec> prec(n_rec);
+            for (uint32_t r = 0; r < n_rec; ++r) {
+                PairRec& q = prec[r];
+                std::memset(&q, 0, sizeof(q));
+                q.d = recs[r];
+                q.rank = rank[r];
+                for (int k = 0; k < 4; ++k) {
+                    q.p1q[k] = planes[(uint64_t)recs[r].p1_pl * 4 + k];
+                    q.p2q[k] = planes[(uint64_t)recs[r].p2_pl * 4 + k];
+                }
+            }
+            if ((rc = upload(&t->prec, prec.data(), prec.size(), &bytes))) break;
+        }
         if ((rc = upload(&t->planes, planes.data(), planes.size(), &bytes))) break;
         t->planes_words = planes.size();
         pchars.resize(pchars.size() + 40, 0);  // chunk_ok reads 36 bytes from a 4-aligned offset
