@@ -50,8 +50,9 @@ int fail(int code, const std::string& msg);
     do {                                                                       \
         hipError_t _e = (expr);                                                \
         if (_e != hipSuccess)                                                  \
-            return ::mp::fail(MP_E_HIP, std::string(#expr) + ": " +            \
-                                            hipGetErrorString(_e));            \
+            return ::mp::fail(MP_E_HIP, std::string(#expr) + " (" + __FILE__ +   \
+                                            ":" + std::to_string(__LINE__) +   \
+                                            "): " + hipGetErrorString(_e));    \
     } while (0)
 
 // Wait for an event by polling (hipEventQuery) instead of a blocking synchronisation: a
@@ -154,6 +155,7 @@ struct Table {
     uint64_t* kgrp = nullptr;     // W 11..13: key groups, one u64 per 16 keys (see kKgrpKeys)
     uint32_t kgrp_F = 0;          // primer-1 bases W..W+F-1 a key-group field holds (0: no key groups)
     int kgrp_wild = 0;            // I = 1 field form: two 24-bit fields with the non-plain bases marked
+    uint4* kgrp4 = nullptr;       // I = 1, W 11..13: wide key groups, one uint4 per 32 keys (kKgrp4Keys)
     uint2* binfo = nullptr;       // W <= kDenseMaxW: per key rank {first padded entry, records}
     uint16_t* dfilt = nullptr;    // W <= kDenseMaxW: 2-B filter word per padded entry (kDenseAlways...)
     uint2* dgrp = nullptr;        // W <= kDenseMaxW: per 32 keys {inline-bucket bits, first oct | any escape << 31}
@@ -426,6 +428,23 @@ constexpr uint32_t kKgrpFlag = 0x8000u;
 // key went to tail_kernel: c3's ~5k two-record keys gave most of its 3.4M bucket-tail references.
 constexpr uint32_t kKgrpPair = 0x4000u;
 constexpr uint32_t kKgrpWildFields = 2;  // I = 1 key groups: two 24-bit fields {codes, wild bases}
+// Wide I = 1 key groups (kgrp4, round 4; c4: degenerate primers, N = 2): one 16-B word per 32
+// keys of the exact 4^W bitmap, for the ranked drain over 8-B IUPAC heads (Table::h12).
+// .x the 32 presence bits; .y bits 0..17 the rank of the group's first key (the rank word's
+// prefix count); bits 18..95 of (.y, .z, .w) three 26-bit fields, one for each of the group's
+// first three present keys: bits 0..2F-1 the 2-bit codes of primer-1 bases W..W+F-1 (base W
+// on top), bits 16..16+F-1 their plain flags (base W on top).  A key whose bucket is not one
+// record seeded at its primer start has no plain flag set, nor has an IUPAC base or a base
+// past the primer's end.  The probe counts mismatches at the plain bases only, a lower bound
+// on primer-1 mismatches when the window's first W + F genome bases are all A/C/G/T/U (other
+// windows pass on presence), so more than N ends the seed at the probe; the rest go to the
+// drain with their rank, as from a rank word.  One 16-B load per level-1 positive replaces
+// the rank word (8 B), and the drain's head loads drop to the seeds that pass (c4: ~16%).
+constexpr uint32_t kKgrp4Keys = 32;
+constexpr uint32_t kKgrp4Fields = 3;
+constexpr uint32_t kKgrp4F = 8;
+constexpr uint32_t kKgrp4RankBits = 18;
+constexpr uint32_t kKgrp4FieldBits = 26;
 
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {
     return d == 0 ? 0u : (d < 0 ? (uint32_t)(-2 * d - 1) : (uint32_t)(2 * d));

@@ -58,6 +58,7 @@ struct ScanArgs {
     const uint2* kgrp;      // W 11..13: key groups (u64 per 16 keys, see kKgrpKeys)
     uint32_t kgrp_F;
     int kgrp_wild;          // I = 1 field form (kgrp_pass)
+    const uint4* kgrp4;     // I = 1 wide key groups (uint4 per 32 keys, see kKgrp4Keys; kgrp_pass4)
     uint32_t sched_short;   // super-steps per claim in short scans (SuperSched)
     const Entry* dents;     // W <= 13: bucket heads by rank
     const uint2* dents8;    // W <= 13: 8-B heads
@@ -838,22 +839,30 @@ __device__ __forceinline__ bool candidate(const ScanArgs& a, const SuperRegs& R,
 // last chunk are marked empty.
 struct SurvChunk {
     uint64_t base;   // first slot of the current chunk
-    uint32_t used;   // slots of it already written (64 = none left)
+    uint32_t used;   // slots of it already written (kChunkNone: no chunk yet)
     uint32_t total;  // entries of this wave (statistics)
 };
+constexpr uint32_t kChunkNone = 0xFFFFFFFFu;
+// Ranked key references per reservation (the wide key groups: c4 leaves ~20M, where 64-slot
+// reservations, ~94 per microsecond, saturated the list counter; c3's 5.5M keep 64)
+constexpr uint32_t kRefChunk = 256;
 
-template <int kStride = 1>
+// kChunk: slots per reservation (a multiple of 64).  Every reservation is one returning atomic
+// on one address, and same-address atomics serialise at ~88 per microsecond: lists written at
+// more than ~5M entries per millisecond of scan take larger chunks (kRefChunk).
+template <int kStride = 1, uint32_t kChunk = 64>
 __device__ __forceinline__ void append_chunked(unsigned long long* counter, uint4* buf, uint64_t cap, bool on,
                                                const uint4& v, int lane, SurvChunk& C, const uint4& v2 = uint4{}) {
+    static_assert(kChunk % 64u == 0u, "whole waves of slots");
     const uint64_t m = __ballot(on);
     if (!m) return;
     const uint32_t cnt = (uint32_t)__popcll(m);
     C.total += cnt;
-    const uint32_t avail = 64u - C.used;
+    const uint32_t avail = C.used >= kChunk ? 0u : kChunk - C.used;
     uint64_t nbase = C.base;
     if (cnt > avail) {
         unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(counter, 64ull);
+        if (lane == 0) b = atomicAdd(counter, (unsigned long long)kChunk);
         nbase = shfl64((uint64_t)b, 0);
     }
     if (on) {
@@ -879,11 +888,11 @@ __device__ __forceinline__ void flush_survivors(const ScanArgs& a, const SuperRe
                    make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), rec | (exact ? 0x80000000u : 0u), R.seq), lane, C);
 }
 
-template <int kStride = 1>
+template <int kStride = 1, uint32_t kChunk = 64>
 __device__ __forceinline__ void close_chunked(uint4* buf, uint64_t cap, int lane, const SurvChunk& C) {
-    const uint32_t i = C.used + (uint32_t)lane;
-    if (C.used < 64u && i < 64u && C.base + i < cap)
-        buf[(C.base + i) * kStride] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);  // empty slot
+    if (C.used >= kChunk) return;
+    for (uint32_t i = C.used + (uint32_t)lane; i < kChunk; i += 64u)  // the chunk's unused slots: empty
+        if (C.base + i < cap) buf[(C.base + i) * kStride] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
 }
 
 // Entry of an 8-B head (see kHead8Full): the seed key h supplies primer-1 bases [0, W).
@@ -1356,6 +1365,9 @@ __device__ __forceinline__ uint32_t kmer_dyn4(uint32_t d0, uint32_t d1, uint32_t
 // Bucket-tail reference of a seed that passed the key groups (kRkf scan): no bucket field;
 // tail_kernel finds the bucket from the seed window's key.
 constexpr uint32_t kKeyRef = 0x80000000u;
+// ... of a seed that passed the wide key groups (kgrp4): the tag and the key's rank (< 2^30),
+// so tail_kernel reads the key's 8-B IUPAC head (dents12) without the rank word.
+constexpr uint32_t kKeyRank = 0xC0000000u;
 
 // 32-bit funnel of bases p..p+15 of a lane's 48 bases (A, B, C = bases 0-15, 16-31,
 // 32-47), p in [0, 48); bases past 47 read as 0.
@@ -1450,6 +1462,29 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
     const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
     return __popc((x | (x >> 1)) & 0x55555555u) <= a.N;
 #endif
+}
+
+// Level-2 probe of the wide I = 1 key groups (kgrp4, see kKgrp4Keys).  `pk`: the window's
+// bases W..W+F-1 << 5 | the key's low 5 bits, bit 31 set when the window's first W + F bases
+// are not all A/C/G/T/U (it then passes on presence alone).  True = the seed goes on to the
+// drain, with its rank in *rank.
+__device__ __forceinline__ bool kgrp_pass4(const ScanArgs& a, uint4 rw, uint32_t pk, uint32_t& rank) {
+    static_assert(kKgrp4F == 8 && kKgrp4FieldBits == 26 && kKgrp4RankBits == 18, "field layout");
+    const uint32_t bit = pk & 31u;
+    const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
+    rank = (rw.y & ((1u << kKgrp4RankBits) - 1u)) + j;
+    if (!((rw.x >> bit) & 1u)) return false;
+    if ((pk >> 31) || j >= kKgrp4Fields) return true;
+    // field j: bits 18 + 26 j .. of (.y, .z, .w)
+    const uint32_t f = j == 0u ? __builtin_amdgcn_alignbit(rw.z, rw.y, 18u)
+                               : (j == 1u ? __builtin_amdgcn_alignbit(rw.w, rw.z, 12u) : rw.w >> 6);
+    const uint32_t x = ((pk >> 5) ^ f) & 0xFFFFu;
+    // the plain flags (bits 16..23, base W on top) spread to the low bit of each base's slot
+    uint32_t pl = (f >> 16) & 0xFFu;
+    pl = (pl | (pl << 4)) & 0x0F0Fu;
+    pl = (pl | (pl << 2)) & 0x3333u;
+    pl = (pl | (pl << 1)) & 0x5555u;
+    return __popc((x | (x >> 1)) & pl) <= a.N;
 }
 
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
@@ -1593,7 +1628,10 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
     }
 };
 
-template <int kMode, bool kInline, int kK = 1, bool kDefer = false, int kH16 = 0, bool kRkf = false,
+// kRkf: 0 the rank queue and drain; 1 the key groups (kgrp, u64 per 16 keys); 2 the wide I = 1 key
+// groups (kgrp4, uint4 per 32 keys: presence, rank, fields) in place of the rank words, then the
+// ranked drain as for kRkf 0.
+template <int kMode, bool kInline, int kK = 1, bool kDefer = false, int kH16 = 0, int kRkf = 0,
           bool kGap = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     static_assert(!kGap || (kMode == 1 && kRkf), "gapped seeds take the key-group path");
@@ -1623,8 +1661,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     const uint32_t shw = 32u - 2u * W;
     WaveLds& L = s_wl[w];
     uint32_t ncand = 0;
-    SurvChunk C{0, 64u, 0u};
-    SurvChunk TC{0, 64u, 0u};
+    SurvChunk C{0, kChunkNone, 0u};
+    SurvChunk TC{0, kChunkNone, 0u};
 
     SuperSched sch;
     uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kWaves, lane, a.sched_short);
@@ -1692,7 +1730,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // I = 1 key groups: windows whose first W + F bases are not all A/C/G/T/U; gapped
             // seeds: windows with an invalid base in the gap
             const uint32_t fbad = kGap ? ~window_ok_mask(R.iv << a.gap_at, a.gap_len)
-                                       : ((kRkf && a.kgrp_wild) ? ~window_ok_mask(R.iv, W + a.kgrp_F) : 0u);
+                                       : (kRkf == 2 ? ~window_ok_mask(R.iv, W + kKgrp4F)
+                                                    : ((kRkf && a.kgrp_wild) ? ~window_ok_mask(R.iv, W + a.kgrp_F) : 0u));
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
@@ -1720,13 +1759,13 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                 const uint32_t nr = min(tot - r0, kSeedQR);
                 constexpr int kP = (kSeedQR + 63) / 64;
                 uint32_t pk[kP], po[kP];
-                uint2 rw[kP];
+                std::conditional_t<kRkf == 2, uint4, uint2> rw[kP];
 #pragma unroll
                 for (int q = 0; q < kP; ++q) {
                     const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
                     pk[q] = 0;
                     po[q] = 0;
-                    rw[q] = make_uint2(0u, 0u);
+                    rw[q] = {};
                     if ((uint32_t)q * 64u < nr) {
                         const bool v = e < nr;
                         if constexpr (kRkf) {
@@ -1744,15 +1783,25 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                             // the field's bases: after the key, or a gapped seed's gap and the
                             // bases after its span (2 gap_len bases after the gap's start)
                             uint32_t fb;
-                            if constexpr (kGap) {
+                            if constexpr (kRkf == 2) {  // kKgrp4F bases: a fourth shuffle (bases 48..63)
+                                const uint32_t D = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)(uint32_t)R.w1);
+                                const uint32_t p = i + W;
+                                const uint32_t hi = p < 16u ? A : (p < 32u ? B : C), lo = p < 16u ? B : (p < 32u ? C : D);
+                                const uint32_t r = 2u * (p & 15u);
+                                fb = (r ? __builtin_amdgcn_alignbit(hi, lo, 32u - r) : hi) >> (32u - 2u * kKgrp4F);
+                                pk[q] = (fb << 5) | (key & 31u) | ((qe >> 15) << 31);
+                                rw[q] = a.kgrp4[v ? (key >> 5) : 0u];
+                            } else if constexpr (kGap) {
                                 const uint32_t f = funnel3(A, B, C, i + a.gap_at);
                                 fb = ((f >> (32u - 2u * a.gap_len)) << (2u * a.gap_post)) |
                                      (a.gap_post ? (f << (4u * a.gap_len)) >> (32u - 2u * a.gap_post) : 0u);
                             } else {
                                 fb = funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F);
                             }
-                            pk[q] = (fb << 4) | (key & 15u) | ((qe >> 15) << 31);
-                            rw[q] = a.kgrp[v ? (key >> 4) : 0u];
+                            if constexpr (kRkf != 2) {
+                                pk[q] = (fb << 4) | (key & 15u) | ((qe >> 15) << 31);
+                                rw[q] = a.kgrp[v ? (key >> 4) : 0u];
+                            }
                         } else {
                             pk[q] = v ? L.rq.r[e] : 0u;
                             po[q] = v ? (uint32_t)L.rq.q[e] : 0u;
@@ -1768,18 +1817,27 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     }
                 }
                 wave_sync();  // every list entry is in registers before the seeds overwrite it
-                if constexpr (kRkf) {
+                if constexpr (kRkf != 0) {
                     // the few seeds that pass the key groups (c3: 4% of seeds) leave as key
                     // references for tail_kernel, with their window, exception bits and bases
-                    // left: compacted into the list, then one pass of window shuffles per 64
+                    // left: compacted into the list, then one pass of window shuffles per 64.
+                    // The wide key groups (kRkf 2) know the key's rank: their references carry
+                    // it (kKeyRank), and tail_kernel reads the 8-B IUPAC head directly.
                     uint32_t qn = 0;
 #pragma unroll
                     for (int q = 0; q < kP; ++q) {
                         if ((uint32_t)q * 64u < nr) {
                             const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
-                            const bool hit = e < nr && kgrp_pass<kGap>(a, rw[q], pk[q]);
+                            bool hit;
+                            uint32_t rank = 0;
+                            if constexpr (kRkf == 2) hit = kgrp_pass4(a, rw[q], pk[q], rank) && e < nr;
+                            else hit = e < nr && kgrp_pass<kGap>(a, rw[q], pk[q]);
                             const uint64_t hm = __ballot(hit);
-                            if (hit) L.rq.q[qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint16_t)po[q];
+                            const uint32_t at = qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
+                            if (hit) {
+                                L.rq.q[at] = (uint16_t)po[q];
+                                if constexpr (kRkf == 2) L.rq.r[at] = rank;
+                            }
                             qn += (uint32_t)__popcll(hm);
                         }
                     }
@@ -1787,14 +1845,15 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                     for (uint32_t b = 0; b < qn; b += 64) {
                         const uint32_t e = b + (uint32_t)lane;
                         const bool on = e < qn;
-                        const uint32_t p = R.base + (on ? (uint32_t)L.rq.q[e] : 0u);
+                        const uint32_t p = R.base + (on ? ((uint32_t)L.rq.q[e] & 0x7FFu) : 0u);
+                        const uint32_t tag = kRkf == 2 ? (kKeyRank | (on ? L.rq.r[e] : 0u)) : kKeyRef;
                         uint64_t G;
                         uint32_t x;
                         window_from_regs(a, R, sbase, p, true, G, x);
                         const uint64_t gp = sbase + p;
-                        append_chunked<2>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
-                                          make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), kKeyRef, R.seq), lane, TC,
-                                          make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
+                        append_chunked<2, kRkf == 2 ? kRefChunk : 64u>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
+                                                     make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), tag, R.seq), lane, TC,
+                                                     make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
                     }
                     wave_sync();  // the next round rewrites the list
                     r0 += kSeedQR;
@@ -1857,7 +1916,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         ss = nx;
     }
     close_chunked(a.surv, a.surv_cap, lane, C);
-    close_chunked<2>(a.tails, a.tails_cap, lane, TC);
+    close_chunked<2, kRkf == 2 ? kRefChunk : 64u>(a.tails, a.tails_cap, lane, TC);
     // candidate statistics
     add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);
 }
@@ -1994,7 +2053,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     const uint32_t N = (uint32_t)a.N;
     const uint4* __restrict__ octs = reinterpret_cast<const uint4*>(a.dfilt);
     uint32_t ncand = 0;
-    SurvChunk C{0, 64u, 0u};
+    SurvChunk C{0, kChunkNone, 0u};
 
     SuperSched sch;
     uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kDenseWaves, lane, a.sched_short);
@@ -2162,7 +2221,8 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
 // 512 blocks where 2,048 smaller ones spent ~20 us on them at the kernel's end.
 constexpr uint32_t kTailBlock = 1024;
 constexpr uint32_t kTailBuf = 2048;
-static_assert(kKeyRef == 0x80000000u, "key references: bucket field 2^31 (ents indices are below)");
+static_assert(kKeyRef == 0x80000000u && kKeyRank == 0xC0000000u,
+              "key references: bucket field 2^31, with the rank 2^31 | 2^30 | rank (ents indices are below)");
 __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32_t& n_sh,
                                            unsigned long long& base_sh) {
     __syncthreads();
@@ -2198,12 +2258,18 @@ __device__ __forceinline__ void tail_open(const ScanArgs& a, const uint4 v, cons
     t.seq = v.w;
     uint32_t first = v.z;
     Entry e;
-    if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
+    if (v.z >= kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
         const uint32_t W = (uint32_t)a.W;
         const uint32_t h = kGap ? gap_key((uint32_t)(t.Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
                                 : (uint32_t)(t.Gs >> (64u - 2u * W));
-        const uint2 rw = a.rk[h >> 5];
-        const uint2 c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
+        const bool h12 = (v.z & kKeyRank) == kKeyRank;  // the rank came with the reference (kgrp4)
+        uint2 c;
+        if (h12) {
+            c = a.dents12[v.z & ~kKeyRank];
+        } else {
+            const uint2 rw = a.rk[h >> 5];
+            c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
+        }
         if (c.y & kHead8Full) {
             first = c.x;  // the bucket's first entry
             if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
@@ -2221,7 +2287,7 @@ __device__ __forceinline__ void tail_open(const ScanArgs& a, const uint4 v, cons
             }
             e = a.ents[first];
         } else {
-            e = head8_entry(c, h, W);
+            e = h12 ? head12_entry(c, h, W) : head8_entry(c, h, W);
         }
     } else {
         e = a.ents[first];  // its count = tail length
@@ -2265,6 +2331,18 @@ __device__ __forceinline__ bool tail_test(const ScanArgs& a, const TailRef& t, c
 // window whose gap matches the record exactly is left to the contiguous seed's scan.
 // (The same rules as tail_open / tail_test, which the fused pair check uses; written out here
 // in one body: through the helpers c4's tail pass took 0.062 ms against 0.054.)
+// Each thread takes kTailR references per pass, their head loads (the rank word and 8-B head
+// of a key reference, or the 8-B IUPAC head of a ranked one) all in flight together: one
+// reference per thread left a chain of two or three dependent loads per pass exposed (c4's
+// ~20M ranked references, 0.35 ms).
+#ifndef MP_TAIL_R
+#define MP_TAIL_R 2
+#endif
+#ifndef MP_TAIL_BPC
+#define MP_TAIL_BPC 2
+#endif
+constexpr int kTailR = MP_TAIL_R;
+constexpr uint32_t kTailBPC = MP_TAIL_BPC;  // blocks per CU
 template <bool kGap = false>
 __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     __shared__ uint4 s_buf[kTailBuf];
@@ -2275,38 +2353,67 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     const int lane = threadIdx.x & 63;
     const uint64_t n_refs = umin64(a.counters[a.tail_ctr], a.tails_cap);
     const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
+    const uint32_t W = (uint32_t)a.W;
     uint32_t ncand = 0, nsurv = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
-    for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride) {  // block-uniform
-        const uint64_t i = b + threadIdx.x;
-        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
-        if (i < n_refs) {
-            v = a.tails[2 * i];
-            w = a.tails[2 * i + 1];
+    auto key_of = [&](const uint4& w) {  // the seed key from the reference's window
+        const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);
+        return kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
+                    : (uint32_t)(Gs >> (64u - 2u * W));
+    };
+    const uint64_t stride = (uint64_t)gridDim.x * kTailBlock * kTailR;
+    for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock * kTailR; b < n_refs; b += stride) {  // block-uniform
+        uint4 v[kTailR], w[kTailR];
+        uint2 c[kTailR];
+#pragma unroll
+        for (int k = 0; k < kTailR; ++k) {
+            const uint64_t i = b + (uint64_t)k * kTailBlock + threadIdx.x;
+            v[k] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+            w[k] = make_uint4(0u, 0u, 0u, 0u);
+            if (i < n_refs) {
+                v[k] = a.tails[2 * i];
+                w[k] = a.tails[2 * i + 1];
+            }
         }
-        if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
-            const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
-            const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
-            const uint32_t rem = w.w;                                    // bases from the seed to the end
-            uint32_t first = v.z;
+        // key references: kKeyRank (the wide key groups) carries the rank, so its 8-B IUPAC head
+        // is one load; kKeyRef reads the rank word, then the 8-B head
+#pragma unroll
+        for (int k = 0; k < kTailR; ++k) {
+            c[k] = make_uint2(0u, 0u);
+            const bool live = !(v[k].x == 0xFFFFFFFFu && v[k].y == 0xFFFFFFFFu);
+            if (live && (v[k].z & kKeyRank) == kKeyRank) c[k] = a.dents12[v[k].z & ~kKeyRank];
+            else if (live && v[k].z == kKeyRef) c[k] = a.rk[key_of(w[k]) >> 5];
+        }
+#pragma unroll
+        for (int k = 0; k < kTailR; ++k) {
+            const bool live = !(v[k].x == 0xFFFFFFFFu && v[k].y == 0xFFFFFFFFu);
+            if (live && v[k].z == kKeyRef) {
+                const uint32_t h = key_of(w[k]);
+                c[k] = a.dents8[c[k].y + (uint32_t)__popc(c[k].x & ((1u << (h & 31u)) - 1u))];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kTailR; ++k) {
+            if (v[k].x == 0xFFFFFFFFu && v[k].y == 0xFFFFFFFFu) continue;
+            const uint64_t gp = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+            const uint64_t Gs = (uint64_t)w[k].x | ((uint64_t)w[k].y << 32);  // window at the seed
+            const uint32_t rem = w[k].w;                                          // bases from the seed to the end
+            uint32_t first = v[k].z;
             Entry e;
-            if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
-                const uint32_t W = (uint32_t)a.W;
-                const uint32_t h = kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
-                                        : (uint32_t)(Gs >> (64u - 2u * W));
-                const uint2 rw = a.rk[h >> 5];
-                const uint2 c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
-                if (c.y & kHead8Full) {
-                    first = c.x;  // the bucket's first entry
-                    if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
-                        const uint32_t cnt = ((c.y >> 28) & 3u) + 1u;
+            if (v[k].z >= kKeyRef) {  // a seed that passed the key groups: its bucket's head
+                const uint32_t h = key_of(w[k]);
+                const bool h12 = (v[k].z & kKeyRank) == kKeyRank;
+                const uint2 cc = c[k];
+                if (cc.y & kHead8Full) {
+                    first = cc.x;  // the bucket's first entry
+                    if (cc.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
+                        const uint32_t cnt = ((cc.y >> 28) & 3u) + 1u;
                         const uint32_t F = head8_filt_bases(cnt);
                         const uint32_t fm = (1u << (2u * F)) - 1u;
                         const uint32_t gf = (uint32_t)((Gs << (2u * W)) >> (64u - 2u * F));
-                        const uint32_t xf = w.z & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
+                        const uint32_t xf = w[k].z & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
                         bool any = xf != 0u;
                         for (uint32_t j = 0; j < cnt; ++j) {
-                            const uint32_t xj = gf ^ ((c.y >> (2u * F * j)) & fm);
+                            const uint32_t xj = gf ^ ((cc.y >> (2u * F * j)) & fm);
                             any = any || __popc((xj | (xj >> 1)) & 0x55555555u) <= a.N;
                         }
                         if (!any) first = 0xFFFFFFFFu;
@@ -2314,10 +2421,10 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                     if (first != 0xFFFFFFFFu) e = a.ents[first];
                     else e.count = 0;
                 } else {
-                    e = head8_entry(c, h, W);
+                    e = h12 ? head12_entry(cc, h, W) : head8_entry(cc, h, W);
                 }
             } else {
-                e = a.ents[first];                                       // its count = tail length
+                e = a.ents[first];  // its count = tail length
             }
             const uint32_t cnt = e.count;
             for (uint32_t j = 0; j < cnt; ++j) {
@@ -2325,9 +2432,9 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 const uint64_t gk = gp - e.hash_off;
                 if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) continue;  // k + l1 > n / not owned
                 uint64_t G = Gs;
-                uint32_t ex = w.z;
+                uint32_t ex = w[k].z;
                 if (e.hash_off) {  // seed inside the primer: bounds and window from the genome
-                    const uint64_t sbase = a.seq_base[v.w];
+                    const uint64_t sbase = a.seq_base[v[k].w];
                     if (gp - sbase < e.hash_off) continue;  // k < 0
                     G = ext2(a.g2, gk);
                     ex = (uint32_t)(ext1(exc, gk) >> 32);
@@ -2343,7 +2450,7 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 bool exact = false;
                 if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) continue;
                 ++nsurv;
-                const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
+                const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v[k].w);
                 const uint32_t at = atomicAdd(&s_n, 1u);
                 if (at < kTailBuf) {
                     s_buf[at] = sv;
@@ -2752,6 +2859,7 @@ static void scan_fields(ScanArgs& a, const Table* t, const Search* s) {
     a.dsum = t->dsum; a.dsum_mode = t->dsum_mode; a.dense_F = t->dense_F;
     a.defer_full = t->defer_full && (!s->opt.no_defer || t->gap_len);
     a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F; a.kgrp_wild = t->kgrp_wild;
+    a.kgrp4 = t->kgrp4;
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.dents12 = t->dents12; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents;
@@ -2785,6 +2893,9 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
     // (I = 1: the field form with the non-plain bases marked, kgrp_wild)
     const bool rkf = t->kgrp_F >= 2 && (a.I == 0 ? !t->h16 && !t->kgrp_wild : t->kgrp_wild != 0) &&
                      !s->opt.no_rank_filter && t->filt_direct && !t->lds_exact && a.W >= 11 && a.W <= 13;
+    // I = 1 tables whose 8-B fields are too short (c4): the wide key groups
+    const bool rkf4 = t->kgrp4 && a.I == 1 && !s->opt.no_rank_filter && t->filt_direct && !t->lds_exact &&
+                      a.W >= 11 && a.W <= 13 && a.defer_full && t->h12;
     if (dense) {
         const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
                                                             (uint64_t)s->n_cu * (uint64_t)s->dense_per_cu);
@@ -2803,6 +2914,10 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
         else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
     } else {
         if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (rkf4 && t->lds_k == 2)
+            hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (rkf4 && t->lds_k == 1)
+            hipLaunchKernelGGL((scan_kernel<1, false, 1, true, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full && rkf)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 3 && a.defer_full && rkf)  // MP_LDS_K=3 (A/B)
@@ -2863,7 +2978,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         if (rc) return rc;
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
         if (tail && !fuse) {
-            hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, a);
+            hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }
         fuse = fuse && tail;
@@ -2887,8 +3002,8 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
         for (int i = 0; i < 3; ++i) {
             if (!sub[i] || !tail[i]) continue;
-            if (sub[i]->gap_len) hipLaunchKernelGGL(tail_kernel<true>, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, pa[i]);
-            else hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * 2), dim3(kTailBlock), 0, st, pa[i]);
+            if (sub[i]->gap_len) hipLaunchKernelGGL(tail_kernel<true>, dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, pa[i]);
+            else hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, pa[i]);
             MP_HIP_CHECK(hipGetLastError());
         }
     }

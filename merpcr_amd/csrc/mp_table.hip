@@ -52,7 +52,7 @@ static void free_table(Table* t) {
     if (!t) return;
     free_table(t->split_a); free_table(t->split_b); free_table(t->split_rest);
     hipFree(t->dents12);
-    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->kgrp); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
+    hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->kgrp); hipFree(t->kgrp4); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
     hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes); hipFree(t->prec);
     hipFree(t->pchars);
     delete t;
@@ -286,6 +286,7 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         std::vector<uint2> dents8;
         std::vector<uint4> dents16;
         std::vector<uint64_t> kgrp;
+        std::vector<uint4> kgrp4;
         std::vector<Slot> slots;
         if (t->filt_direct) {
             // rank bitmap over the exact 4^W presence bitmap; heads in key order
@@ -584,6 +585,52 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                 // pass ~0.5%); c4's (N = 2, ~30% IUPAC bases after the seed) pass ~30% and stay
                 // on the 16-B heads, which test 16 bases
                 t->kgrp_wild = pass_n && pass_sum / (double)pass_n < 0.08 ? 1 : 0;
+                // wide key groups (kKgrp4Keys) when the 8-B fields are too short to end most
+                // seeds and the ranked drain runs over 8-B IUPAC heads (h12): eight bases per
+                // field; a key without one (several records, a seed inside the primer, the
+                // fourth present key of its group) always passes.  Taken when fewer than a
+                // quarter of a random window's seeds would pass (c4: ~0.16 with the keys
+                // without a field counted, against ~0.30 for the 8-B fields)
+                const char* no4 = std::getenv("MP_NO_KGRP4");
+                if (!t->kgrp_wild && t->h12 && t->defer_full && nb < (1u << kKgrp4RankBits) && !(no4 && std::atoi(no4))) {
+                    const uint32_t F4 = kKgrp4F;
+                    const uint64_t seedm = sp_lt((int)W);
+                    double pass4 = 0.0;
+                    uint64_t n4 = 0;
+                    kgrp4.assign(nkeys / kKgrp4Keys, make_uint4(0u, 0u, 0u, 0u));
+                    for (uint64_t g = 0; g < kgrp4.size(); ++g) {
+                        const uint32_t pres = filt[g];  // the exact bitmap's word: this group's 32 keys
+                        unsigned __int128 fields = 0;
+                        uint32_t j = 0;
+                        for (uint32_t bit = 0; bit < 32; ++bit) {
+                            if (!((pres >> bit) & 1u)) continue;
+                            ++n4;
+                            if (j >= kKgrp4Fields) {
+                                pass4 += 1.0;
+                                continue;
+                            }
+                            const uint32_t rank = rk[g].y + (uint32_t)__builtin_popcount(rk[g].x & ((1u << bit) - 1u));
+                            const uint32_t b = rank_bucket[rank];
+                            const Entry& e = ents[boff[b]];
+                            uint32_t f = 0;
+                            double pr = 1.0;
+                            if (bcount[b] == 1 && e.hash_off == 0 && e.l1 > W && (e.pmask & seedm) == seedm &&
+                                ((e.pmask >> 1) & seedm) == 0) {
+                                uint32_t plain = 0;
+                                for (uint32_t i = 0; i < F4 && W + i < e.l1 && W + i < 32; ++i)
+                                    if ((e.pmask >> (62 - 2 * (W + i))) & 1ull) plain |= 1u << (F4 - 1 - i);
+                                f = (plain << 16) | (uint32_t)((e.code << (2 * W)) >> (64 - 2 * F4));
+                                pr = pass_rate((uint32_t)__builtin_popcount(plain));
+                            }
+                            fields |= (unsigned __int128)f << (kKgrp4FieldBits * j);
+                            pass4 += pr;
+                            ++j;
+                        }
+                        const unsigned __int128 hi = (fields << kKgrp4RankBits) | rk[g].y;  // bits 0..95 of (.y, .z, .w)
+                        kgrp4[g] = make_uint4(pres, (uint32_t)hi, (uint32_t)(hi >> 32), (uint32_t)(hi >> 64));
+                    }
+                    if (!(n4 && pass4 / (double)n4 < 0.25)) kgrp4.clear();
+                }
             } else if (W >= 11 && W <= 13) {
                 const uint32_t F = std::min<uint32_t>(7u, 17u - W);
                 t->kgrp_F = F;
@@ -654,6 +701,7 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         if ((rc = upload(&t->dents8, dents8.data(), dents8.size(), &bytes))) break;
         if ((rc = upload(&t->dents16, dents16.data(), dents16.size(), &bytes))) break;
         if ((rc = upload(&t->kgrp, kgrp.data(), kgrp.size(), &bytes))) break;
+        if (!kgrp4.empty() && (rc = upload(&t->kgrp4, kgrp4.data(), kgrp4.size(), &bytes))) break;
         if ((rc = upload(&t->binfo, binfo.data(), binfo.size(), &bytes))) break;
         if ((rc = upload(&t->dfilt, dfilt.data(), dfilt.size(), &bytes))) break;
         if ((rc = upload(&t->dgrp, dgrp.data(), dgrp.size(), &bytes))) break;

@@ -27,7 +27,7 @@ import shutil
 
 _L1 = "            const uint32_t c = (uint32_t)__popc(rem);\n"
 _L2 = "                constexpr int kP = (kSeedQR + 63) / 64;\n"
-_L3 = "                if constexpr (kRkf) {\n                    // the few seeds that pass the key groups"
+_L3 = "                if constexpr (kRkf == 1) {\n                    // the few seeds that pass the key groups"
 _LOOP = ("    while (ss < n_supers) {\n        const SeqSpan sp = pf;\n        const uint64_t sbase = pf_sbase;\n"
          "        const uint32_t n = pf_n;\n        SuperRegs R;")
 _STAGE = "    {\n        constexpr int kStage = (int)(kLdsFilterWords / 4 / kBlock);  // eight uint4 per thread (128 KiB)\n"

@@ -692,9 +692,10 @@ def test_two_ranks_on_one_gpu():
 
 def test_iupac_wide_key_groups_with_genome_ambiguity():
     """I = 1 tables whose primers carry IUPAC bases right after the seed (c4's shape) take
-    the wide 13-base key groups (kgrp_pass_wide).  Genome IUPAC characters inside those 13
-    bases match under I = 1 although the 2-bit plane reads them as 'A': such windows must
-    pass on presence alone.  Planted amplicons put N/R/Y/K into exactly those positions."""
+    the wide key groups (kgrp4: ten bases per field, kgrp_pass4).  Genome IUPAC characters
+    inside those bases match under I = 1 although the 2-bit plane reads them as 'A': such
+    windows must pass on presence alone.  Planted amplicons put N/R/Y/K into exactly those
+    positions."""
     rng = random.Random(41)
     W, N, M, glen = 11, 2, 50, 250_000
     seq = [rng.choice("ACGT") for _ in range(glen)]
@@ -733,3 +734,38 @@ def test_iupac_wide_key_groups_with_genome_ambiguity():
     exp = O.search_lines([("chrW", seq)], table, O.params(**prm))
     assert len(exp) > 200
     assert got == exp
+
+
+@pytest.mark.parametrize("W,N,iupac", [(11, 2, 0.1), (11, 1, 0.3), (12, 2, 0.1), (13, 2, 0.2)])
+def test_wide_key_groups_vs_rank_heads(W, N, iupac, monkeypatch):
+    """The I = 1 scan through the wide key groups (kgrp4, the default for c4-shaped tables)
+    and through the rank words and 8-B IUPAC heads (MP_NO_KGRP4=1, read when the table is
+    built) give the C oracle's hit list byte for byte: primers with IUPAC bases after the
+    seed, short primers (fields past the primer's end), multi-record keys, groups with more
+    than three present keys, N runs and planted amplicons."""
+    from merpcr_amd import synth
+    from oracle import c_oracle as C
+    n_sts = {11: 30000, 12: 40000, 13: 40000}[W]
+    sts = synth.make_sts(n_sts, seed=11 + W, W=W, iupac=iupac)
+    rng = np.random.default_rng(W)
+    glen = 3_000_000
+    g = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, glen)].copy()
+    for _ in range(20):
+        a = int(rng.integers(0, glen - 3000))
+        g[a:a + int(rng.integers(50, 3000))] = ord("N")
+    amps, starts = synth.amplicons(sts, glen, 5, N, 50, W)
+    for amp, st in list(zip(amps, starts))[::2]:
+        if st + len(amp) <= glen:
+            g[st:st + len(amp)] = np.frombuffer(amp, dtype=np.uint8)
+    seq = g.tobytes().decode("ascii")
+    prm = dict(wordsize=W, mismatches=N, iupac_mode=1, margin=50)
+    table = O.load_sts_lines(sts.text().splitlines(True), W, 240)
+    ref = C.search(table, [g], O.params(**prm), 8)
+    assert len(ref) > 100
+    for no4 in ("0", "1"):
+        monkeypatch.setenv("MP_NO_KGRP4", no4)
+        eng = MerPCR(**prm)
+        with tempfile.TemporaryDirectory() as td:
+            assert _load_sts(eng, sts.text(), td)
+        hits = eng.find_hits([FASTARecord(defline=">chrK", sequence=seq)])
+        assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes(), no4
