@@ -2258,18 +2258,12 @@ __device__ __forceinline__ void tail_open(const ScanArgs& a, const uint4 v, cons
     t.seq = v.w;
     uint32_t first = v.z;
     Entry e;
-    if (v.z >= kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
+    if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
         const uint32_t W = (uint32_t)a.W;
         const uint32_t h = kGap ? gap_key((uint32_t)(t.Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
                                 : (uint32_t)(t.Gs >> (64u - 2u * W));
-        const bool h12 = (v.z & kKeyRank) == kKeyRank;  // the rank came with the reference (kgrp4)
-        uint2 c;
-        if (h12) {
-            c = a.dents12[v.z & ~kKeyRank];
-        } else {
-            const uint2 rw = a.rk[h >> 5];
-            c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
-        }
+        const uint2 rw = a.rk[h >> 5];
+        const uint2 c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
         if (c.y & kHead8Full) {
             first = c.x;  // the bucket's first entry
             if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
@@ -2287,7 +2281,7 @@ __device__ __forceinline__ void tail_open(const ScanArgs& a, const uint4 v, cons
             }
             e = a.ents[first];
         } else {
-            e = h12 ? head12_entry(c, h, W) : head8_entry(c, h, W);
+            e = head8_entry(c, h, W);
         }
     } else {
         e = a.ents[first];  // its count = tail length
@@ -2869,6 +2863,16 @@ static void scan_fields(ScanArgs& a, const Table* t, const Search* s) {
     a.gap_post = t->gap_post;
 }
 
+// The scan of table t takes the wide I = 1 key groups (kgrp4) and leaves ranked key references
+// (kKeyRank) that only tail_kernel opens.
+static bool scan_uses_kgrp4(const Search* s, const Table* t, const ScanArgs& a) {
+    const bool inl = (t->n_rec > t->n_keys + t->n_keys / 4 || s->opt.tails == MP_TAILS_INLINE) &&
+                     s->opt.tails != MP_TAILS_KERNEL;
+    const bool dense = (uint32_t)t->prm.wordsize <= kDenseMaxW && !s->opt.no_dense;
+    return t->kgrp4 && a.I == 1 && !s->opt.no_rank_filter && t->filt_direct && !t->lds_exact && a.W >= 11 &&
+           a.W <= 13 && a.defer_full && t->h12 && !t->gap_len && !inl && !dense;
+}
+
 // The scan kernel of table t (dense_kernel, or scan_kernel in the form the table and the
 // handle's options select).  *tail: the run needs tail_kernel over this scan's references.
 static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t tiles, hipStream_t st, bool* tail) {
@@ -2894,8 +2898,7 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
     const bool rkf = t->kgrp_F >= 2 && (a.I == 0 ? !t->h16 && !t->kgrp_wild : t->kgrp_wild != 0) &&
                      !s->opt.no_rank_filter && t->filt_direct && !t->lds_exact && a.W >= 11 && a.W <= 13;
     // I = 1 tables whose 8-B fields are too short (c4): the wide key groups
-    const bool rkf4 = t->kgrp4 && a.I == 1 && !s->opt.no_rank_filter && t->filt_direct && !t->lds_exact &&
-                      a.W >= 11 && a.W <= 13 && a.defer_full && t->h12;
+    const bool rkf4 = scan_uses_kgrp4(s, t, a);
     if (dense) {
         const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
                                                             (uint64_t)s->n_cu * (uint64_t)s->dense_per_cu);
@@ -2970,8 +2973,9 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     }
     const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
     if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-    // one-table runs open their bucket-tail references inside pair_kernel (fused_ref_batch)
-    bool fuse = s->opt.fuse_tails != 0;
+    // one-table runs open their bucket-tail references inside pair_kernel (fused_ref_batch);
+    // the wide key groups' ranked references keep tail_kernel
+    bool fuse = s->opt.fuse_tails != 0 && !scan_uses_kgrp4(s, t, a);
     if (!use_split(s)) {
         bool tail = false;
         const int rc = launch_scan(s, t, a, tiles, st, &tail);
