@@ -429,22 +429,20 @@ constexpr uint32_t kKgrpFlag = 0x8000u;
 constexpr uint32_t kKgrpPair = 0x4000u;
 constexpr uint32_t kKgrpWildFields = 2;  // I = 1 key groups: two 24-bit fields {codes, wild bases}
 // Wide I = 1 key groups (kgrp4, round 4; c4: degenerate primers, N = 2): one 16-B word per 32
-// keys of the exact 4^W bitmap, for the ranked drain over 8-B IUPAC heads (Table::h12).
-// .x the 32 presence bits; .y bits 0..17 the rank of the group's first key (the rank word's
-// prefix count); bits 18..95 of (.y, .z, .w) three 26-bit fields, one for each of the group's
-// first three present keys: bits 0..2F-1 the 2-bit codes of primer-1 bases W..W+F-1 (base W
-// on top), bits 16..16+F-1 their plain flags (base W on top).  A key whose bucket is not one
-// record seeded at its primer start has no plain flag set, nor has an IUPAC base or a base
-// past the primer's end.  The probe counts mismatches at the plain bases only, a lower bound
-// on primer-1 mismatches when the window's first W + F genome bases are all A/C/G/T/U (other
-// windows pass on presence), so more than N ends the seed at the probe; the rest go to the
-// drain with their rank, as from a rank word.  One 16-B load per level-1 positive replaces
-// the rank word (8 B), and the drain's head loads drop to the seeds that pass (c4: ~16%).
+// keys of the exact 4^W bitmap, for tables whose heads are in the 8-B IUPAC form (Table::h12).
+// .x the 32 presence bits; .y, .z, .w a 32-bit field for each of the group's first three
+// present keys: bits 0..2F-1 the 2-bit codes of primer-1 bases W..W+F-1 (base W on top), bits
+// 2F..3F-1 their plain flags (base W on top).  A key whose bucket is not one record seeded at
+// its primer start has no plain flag set, nor has an IUPAC base or a base past the primer's
+// end.  The probe counts mismatches at the plain bases only, a lower bound on primer-1
+// mismatches when the window's first W + F genome bases are all A/C/G/T/U (other windows pass
+// on presence), so more than N ends the seed at the probe; the rest leave as key references,
+// whose bucket tail_kernel finds by the rank word and the 8-B IUPAC head.  One 16-B load per
+// level-1 positive replaces the rank word, and the drain with its head load per seed is gone
+// (c4: ~12% of seeds pass, against ~30% for the 8-B groups' six bases).  2 MB at W = 11.
 constexpr uint32_t kKgrp4Keys = 32;
 constexpr uint32_t kKgrp4Fields = 3;
-constexpr uint32_t kKgrp4F = 8;
-constexpr uint32_t kKgrp4RankBits = 18;
-constexpr uint32_t kKgrp4FieldBits = 26;
+constexpr uint32_t kKgrp4F = 10;
 
 __host__ __device__ __forceinline__ uint32_t try_rank(int32_t d) {
     return d == 0 ? 0u : (d < 0 ? (uint32_t)(-2 * d - 1) : (uint32_t)(2 * d));

@@ -846,6 +846,10 @@ constexpr uint32_t kChunkNone = 0xFFFFFFFFu;
 // Ranked key references per reservation (the wide key groups: c4 leaves ~20M, where 64-slot
 // reservations, ~94 per microsecond, saturated the list counter; c3's 5.5M keep 64)
 constexpr uint32_t kRefChunk = 256;
+#ifndef MP_REF_CHUNK1
+#define MP_REF_CHUNK1 64
+#endif
+constexpr uint32_t kRefChunk1 = MP_REF_CHUNK1;  // the 8-B key groups' references (c3: 5.5M)
 
 // kChunk: slots per reservation (a multiple of 64).  Every reservation is one returning atomic
 // on one address, and same-address atomics serialise at ~88 per microsecond: lists written at
@@ -1365,9 +1369,6 @@ __device__ __forceinline__ uint32_t kmer_dyn4(uint32_t d0, uint32_t d1, uint32_t
 // Bucket-tail reference of a seed that passed the key groups (kRkf scan): no bucket field;
 // tail_kernel finds the bucket from the seed window's key.
 constexpr uint32_t kKeyRef = 0x80000000u;
-// ... of a seed that passed the wide key groups (kgrp4): the tag and the key's rank (< 2^30),
-// so tail_kernel reads the key's 8-B IUPAC head (dents12) without the rank word.
-constexpr uint32_t kKeyRank = 0xC0000000u;
 
 // 32-bit funnel of bases p..p+15 of a lane's 48 bases (A, B, C = bases 0-15, 16-31,
 // 32-47), p in [0, 48); bases past 47 read as 0.
@@ -1466,24 +1467,22 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
 
 // Level-2 probe of the wide I = 1 key groups (kgrp4, see kKgrp4Keys).  `pk`: the window's
 // bases W..W+F-1 << 5 | the key's low 5 bits, bit 31 set when the window's first W + F bases
-// are not all A/C/G/T/U (it then passes on presence alone).  True = the seed goes on to the
-// drain, with its rank in *rank.
-__device__ __forceinline__ bool kgrp_pass4(const ScanArgs& a, uint4 rw, uint32_t pk, uint32_t& rank) {
-    static_assert(kKgrp4F == 8 && kKgrp4FieldBits == 26 && kKgrp4RankBits == 18, "field layout");
+// are not all A/C/G/T/U (it then passes on presence alone).  True = the seed goes on (as a
+// key reference).
+__device__ __forceinline__ bool kgrp_pass4(const ScanArgs& a, uint4 rw, uint32_t pk) {
+    static_assert(kKgrp4F == 10 && kKgrp4Fields == 3, "field layout: three 32-bit fields");
     const uint32_t bit = pk & 31u;
-    const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
-    rank = (rw.y & ((1u << kKgrp4RankBits) - 1u)) + j;
     if (!((rw.x >> bit) & 1u)) return false;
+    const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
     if ((pk >> 31) || j >= kKgrp4Fields) return true;
-    // field j: bits 18 + 26 j .. of (.y, .z, .w)
-    const uint32_t f = j == 0u ? __builtin_amdgcn_alignbit(rw.z, rw.y, 18u)
-                               : (j == 1u ? __builtin_amdgcn_alignbit(rw.w, rw.z, 12u) : rw.w >> 6);
-    const uint32_t x = ((pk >> 5) ^ f) & 0xFFFFu;
-    // the plain flags (bits 16..23, base W on top) spread to the low bit of each base's slot
-    uint32_t pl = (f >> 16) & 0xFFu;
-    pl = (pl | (pl << 4)) & 0x0F0Fu;
-    pl = (pl | (pl << 2)) & 0x3333u;
-    pl = (pl | (pl << 1)) & 0x5555u;
+    const uint32_t f = j == 0u ? rw.y : (j == 1u ? rw.z : rw.w);
+    const uint32_t x = ((pk >> 5) ^ f) & ((1u << (2u * kKgrp4F)) - 1u);
+    // the plain flags (bits 2F.., base W on top) spread to the low bit of each base's slot
+    uint32_t pl = (f >> (2u * kKgrp4F)) & ((1u << kKgrp4F) - 1u);
+    pl = (pl | (pl << 8)) & 0x00FF00FFu;
+    pl = (pl | (pl << 4)) & 0x0F0F0F0Fu;
+    pl = (pl | (pl << 2)) & 0x33333333u;
+    pl = (pl | (pl << 1)) & 0x55555555u;
     return __popc((x | (x >> 1)) & pl) <= a.N;
 }
 
@@ -1820,24 +1819,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                 if constexpr (kRkf != 0) {
                     // the few seeds that pass the key groups (c3: 4% of seeds) leave as key
                     // references for tail_kernel, with their window, exception bits and bases
-                    // left: compacted into the list, then one pass of window shuffles per 64.
-                    // The wide key groups (kRkf 2) know the key's rank: their references carry
-                    // it (kKeyRank), and tail_kernel reads the 8-B IUPAC head directly.
+                    // left: compacted into the list, then one pass of window shuffles per 64
                     uint32_t qn = 0;
 #pragma unroll
                     for (int q = 0; q < kP; ++q) {
                         if ((uint32_t)q * 64u < nr) {
                             const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
                             bool hit;
-                            uint32_t rank = 0;
-                            if constexpr (kRkf == 2) hit = kgrp_pass4(a, rw[q], pk[q], rank) && e < nr;
+                            if constexpr (kRkf == 2) hit = kgrp_pass4(a, rw[q], pk[q]) && e < nr;
                             else hit = e < nr && kgrp_pass<kGap>(a, rw[q], pk[q]);
                             const uint64_t hm = __ballot(hit);
-                            const uint32_t at = qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));
-                            if (hit) {
-                                L.rq.q[at] = (uint16_t)po[q];
-                                if constexpr (kRkf == 2) L.rq.r[at] = rank;
-                            }
+                            if (hit) L.rq.q[qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint16_t)po[q];
                             qn += (uint32_t)__popcll(hm);
                         }
                     }
@@ -1846,13 +1838,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         const uint32_t e = b + (uint32_t)lane;
                         const bool on = e < qn;
                         const uint32_t p = R.base + (on ? ((uint32_t)L.rq.q[e] & 0x7FFu) : 0u);
-                        const uint32_t tag = kRkf == 2 ? (kKeyRank | (on ? L.rq.r[e] : 0u)) : kKeyRef;
                         uint64_t G;
                         uint32_t x;
                         window_from_regs(a, R, sbase, p, true, G, x);
                         const uint64_t gp = sbase + p;
-                        append_chunked<2, kRkf == 2 ? kRefChunk : 64u>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
-                                                     make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), tag, R.seq), lane, TC,
+                        append_chunked<2, kRkf == 2 ? kRefChunk : kRefChunk1>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
+                                                     make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), kKeyRef, R.seq), lane, TC,
                                                      make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
                     }
                     wave_sync();  // the next round rewrites the list
@@ -1916,7 +1907,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         ss = nx;
     }
     close_chunked(a.surv, a.surv_cap, lane, C);
-    close_chunked<2, kRkf == 2 ? kRefChunk : 64u>(a.tails, a.tails_cap, lane, TC);
+    close_chunked<2, kRkf == 2 ? kRefChunk : (kRkf ? kRefChunk1 : 64u)>(a.tails, a.tails_cap, lane, TC);
     // candidate statistics
     add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);
 }
@@ -2221,8 +2212,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
 // 512 blocks where 2,048 smaller ones spent ~20 us on them at the kernel's end.
 constexpr uint32_t kTailBlock = 1024;
 constexpr uint32_t kTailBuf = 2048;
-static_assert(kKeyRef == 0x80000000u && kKeyRank == 0xC0000000u,
-              "key references: bucket field 2^31, with the rank 2^31 | 2^30 | rank (ents indices are below)");
+static_assert(kKeyRef == 0x80000000u, "key references: bucket field 2^31 (ents indices are below)");
 __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32_t& n_sh,
                                            unsigned long long& base_sh) {
     __syncthreads();
@@ -2325,10 +2315,9 @@ __device__ __forceinline__ bool tail_test(const ScanArgs& a, const TailRef& t, c
 // window whose gap matches the record exactly is left to the contiguous seed's scan.
 // (The same rules as tail_open / tail_test, which the fused pair check uses; written out here
 // in one body: through the helpers c4's tail pass took 0.062 ms against 0.054.)
-// Each thread takes kTailR references per pass, their head loads (the rank word and 8-B head
-// of a key reference, or the 8-B IUPAC head of a ranked one) all in flight together: one
-// reference per thread left a chain of two or three dependent loads per pass exposed (c4's
-// ~20M ranked references, 0.35 ms).
+// Each thread takes kTailR references per pass, the head loads of its key references (rank
+// word, then head) in flight together.  (Measured on c4's ~16-22M key references: one, two
+// or four per thread ran within 4% of each other, 0.35-0.37 ms; kept at two.)
 #ifndef MP_TAIL_R
 #define MP_TAIL_R 2
 #endif
@@ -2368,21 +2357,22 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 w[k] = a.tails[2 * i + 1];
             }
         }
-        // key references: kKeyRank (the wide key groups) carries the rank, so its 8-B IUPAC head
-        // is one load; kKeyRef reads the rank word, then the 8-B head
+        // key references: the rank word, then the 8-B head (the 8-B IUPAC head on a table with
+        // wide key groups, whose scan left them)
 #pragma unroll
         for (int k = 0; k < kTailR; ++k) {
             c[k] = make_uint2(0u, 0u);
             const bool live = !(v[k].x == 0xFFFFFFFFu && v[k].y == 0xFFFFFFFFu);
-            if (live && (v[k].z & kKeyRank) == kKeyRank) c[k] = a.dents12[v[k].z & ~kKeyRank];
-            else if (live && v[k].z == kKeyRef) c[k] = a.rk[key_of(w[k]) >> 5];
+            if (live && v[k].z == kKeyRef) c[k] = a.rk[key_of(w[k]) >> 5];
         }
+        const bool h12 = a.kgrp4 != nullptr;
+        const uint2* kref_heads = h12 ? a.dents12 : a.dents8;
 #pragma unroll
         for (int k = 0; k < kTailR; ++k) {
             const bool live = !(v[k].x == 0xFFFFFFFFu && v[k].y == 0xFFFFFFFFu);
             if (live && v[k].z == kKeyRef) {
                 const uint32_t h = key_of(w[k]);
-                c[k] = a.dents8[c[k].y + (uint32_t)__popc(c[k].x & ((1u << (h & 31u)) - 1u))];
+                c[k] = kref_heads[c[k].y + (uint32_t)__popc(c[k].x & ((1u << (h & 31u)) - 1u))];
             }
         }
 #pragma unroll
@@ -2393,9 +2383,8 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
             const uint32_t rem = w[k].w;                                          // bases from the seed to the end
             uint32_t first = v[k].z;
             Entry e;
-            if (v[k].z >= kKeyRef) {  // a seed that passed the key groups: its bucket's head
+            if (v[k].z == kKeyRef) {  // a seed that passed the key groups: its bucket's head
                 const uint32_t h = key_of(w[k]);
-                const bool h12 = (v[k].z & kKeyRank) == kKeyRank;
                 const uint2 cc = c[k];
                 if (cc.y & kHead8Full) {
                     first = cc.x;  // the bucket's first entry
@@ -2863,8 +2852,8 @@ static void scan_fields(ScanArgs& a, const Table* t, const Search* s) {
     a.gap_post = t->gap_post;
 }
 
-// The scan of table t takes the wide I = 1 key groups (kgrp4) and leaves ranked key references
-// (kKeyRank) that only tail_kernel opens.
+// The scan of table t takes the wide I = 1 key groups (kgrp4); its key references are opened by
+// tail_kernel through the 8-B IUPAC heads.
 static bool scan_uses_kgrp4(const Search* s, const Table* t, const ScanArgs& a) {
     const bool inl = (t->n_rec > t->n_keys + t->n_keys / 4 || s->opt.tails == MP_TAILS_INLINE) &&
                      s->opt.tails != MP_TAILS_KERNEL;
@@ -2974,7 +2963,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
     if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
     // one-table runs open their bucket-tail references inside pair_kernel (fused_ref_batch);
-    // the wide key groups' ranked references keep tail_kernel
+    // the wide key groups' references keep tail_kernel (which reads their 8-B IUPAC heads)
     bool fuse = s->opt.fuse_tails != 0 && !scan_uses_kgrp4(s, t, a);
     if (!use_split(s)) {
         bool tail = false;

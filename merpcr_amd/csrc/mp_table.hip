@@ -586,13 +586,13 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                 // on the 16-B heads, which test 16 bases
                 t->kgrp_wild = pass_n && pass_sum / (double)pass_n < 0.08 ? 1 : 0;
                 // wide key groups (kKgrp4Keys) when the 8-B fields are too short to end most
-                // seeds and the ranked drain runs over 8-B IUPAC heads (h12): eight bases per
-                // field; a key without one (several records, a seed inside the primer, the
-                // fourth present key of its group) always passes.  Taken when fewer than a
-                // quarter of a random window's seeds would pass (c4: ~0.16 with the keys
-                // without a field counted, against ~0.30 for the 8-B fields)
+                // seeds and the heads are in the 8-B IUPAC form (h12): ten bases per field; a
+                // key without one (several records, a seed inside the primer, the fourth
+                // present key of its group) always passes.  Taken when fewer than a quarter of
+                // a random window's seeds would pass (c4: ~0.12 with the keys without a field
+                // counted, against ~0.30 for the 8-B fields)
                 const char* no4 = std::getenv("MP_NO_KGRP4");
-                if (!t->kgrp_wild && t->h12 && t->defer_full && nb < (1u << kKgrp4RankBits) && !(no4 && std::atoi(no4))) {
+                if (!t->kgrp_wild && t->h12 && t->defer_full && !(no4 && std::atoi(no4))) {
                     const uint32_t F4 = kKgrp4F;
                     const uint64_t seedm = sp_lt((int)W);
                     double pass4 = 0.0;
@@ -600,7 +600,7 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                     kgrp4.assign(nkeys / kKgrp4Keys, make_uint4(0u, 0u, 0u, 0u));
                     for (uint64_t g = 0; g < kgrp4.size(); ++g) {
                         const uint32_t pres = filt[g];  // the exact bitmap's word: this group's 32 keys
-                        unsigned __int128 fields = 0;
+                        uint32_t fields[kKgrp4Fields] = {0u, 0u, 0u};
                         uint32_t j = 0;
                         for (uint32_t bit = 0; bit < 32; ++bit) {
                             if (!((pres >> bit) & 1u)) continue;
@@ -619,15 +619,14 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                                 uint32_t plain = 0;
                                 for (uint32_t i = 0; i < F4 && W + i < e.l1 && W + i < 32; ++i)
                                     if ((e.pmask >> (62 - 2 * (W + i))) & 1ull) plain |= 1u << (F4 - 1 - i);
-                                f = (plain << 16) | (uint32_t)((e.code << (2 * W)) >> (64 - 2 * F4));
+                                f = (plain << (2 * F4)) | (uint32_t)((e.code << (2 * W)) >> (64 - 2 * F4));
                                 pr = pass_rate((uint32_t)__builtin_popcount(plain));
                             }
-                            fields |= (unsigned __int128)f << (kKgrp4FieldBits * j);
+                            fields[j] = f;
                             pass4 += pr;
                             ++j;
                         }
-                        const unsigned __int128 hi = (fields << kKgrp4RankBits) | rk[g].y;  // bits 0..95 of (.y, .z, .w)
-                        kgrp4[g] = make_uint4(pres, (uint32_t)hi, (uint32_t)(hi >> 32), (uint32_t)(hi >> 64));
+                        kgrp4[g] = make_uint4(pres, fields[0], fields[1], fields[2]);
                     }
                     if (!(n4 && pass4 / (double)n4 < 0.25)) kgrp4.clear();
                 }
