@@ -440,7 +440,12 @@ constexpr uint32_t kKgrpWildFields = 2;  // I = 1 key groups: two 24-bit fields 
 // whose bucket tail_kernel finds by the rank word and the 8-B IUPAC head.  One 16-B load per
 // level-1 positive replaces the rank word, and the drain with its head load per seed is gone
 // (c4: ~12% of seeds pass, against ~30% for the 8-B groups' six bases).  2 MB at W = 11.
-constexpr uint32_t kKgrp4Keys = 32;
+#ifndef MP_KGRP4_KEYS
+#define MP_KGRP4_KEYS 32
+#endif
+constexpr uint32_t kKgrp4Keys = MP_KGRP4_KEYS;  // 16 or 32
+constexpr uint32_t kKgrp4Log2 = kKgrp4Keys == 16 ? 4 : 5;
+static_assert(kKgrp4Keys == 16 || kKgrp4Keys == 32, "key-group size");
 constexpr uint32_t kKgrp4Fields = 3;
 constexpr uint32_t kKgrp4F = 10;
 

@@ -58,7 +58,7 @@ struct ScanArgs {
     const uint2* kgrp;      // W 11..13: key groups (u64 per 16 keys, see kKgrpKeys)
     uint32_t kgrp_F;
     int kgrp_wild;          // I = 1 field form (kgrp_pass)
-    const uint4* kgrp4;     // I = 1 wide key groups (uint4 per 32 keys, see kKgrp4Keys; kgrp_pass4)
+    const uint4* kgrp4;     // I = 1 wide key groups (uint4 per kKgrp4Keys keys; kgrp_pass4)
     uint32_t sched_short;   // super-steps per claim in short scans (SuperSched)
     const Entry* dents;     // W <= 13: bucket heads by rank
     const uint2* dents8;    // W <= 13: 8-B heads
@@ -1788,8 +1788,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                                 const uint32_t hi = p < 16u ? A : (p < 32u ? B : C), lo = p < 16u ? B : (p < 32u ? C : D);
                                 const uint32_t r = 2u * (p & 15u);
                                 fb = (r ? __builtin_amdgcn_alignbit(hi, lo, 32u - r) : hi) >> (32u - 2u * kKgrp4F);
-                                pk[q] = (fb << 5) | (key & 31u) | ((qe >> 15) << 31);
-                                rw[q] = a.kgrp4[v ? (key >> 5) : 0u];
+                                pk[q] = (fb << 5) | (key & (kKgrp4Keys - 1u)) | ((qe >> 15) << 31);
+                                rw[q] = a.kgrp4[v ? (key >> kKgrp4Log2) : 0u];
                             } else if constexpr (kGap) {
                                 const uint32_t f = funnel3(A, B, C, i + a.gap_at);
                                 fb = ((f >> (32u - 2u * a.gap_len)) << (2u * a.gap_post)) |

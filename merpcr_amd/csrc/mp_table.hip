@@ -599,17 +599,20 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                     uint64_t n4 = 0;
                     kgrp4.assign(nkeys / kKgrp4Keys, make_uint4(0u, 0u, 0u, 0u));
                     for (uint64_t g = 0; g < kgrp4.size(); ++g) {
-                        const uint32_t pres = filt[g];  // the exact bitmap's word: this group's 32 keys
+                        // this group's keys: a word of the exact bitmap, or half of one
+                        const uint64_t g0 = g * kKgrp4Keys;
+                        const uint32_t pres = kKgrp4Keys == 32 ? filt[g] : (filt[g0 >> 5] >> (g0 & 31)) & 0xFFFFu;
                         uint32_t fields[kKgrp4Fields] = {0u, 0u, 0u};
                         uint32_t j = 0;
-                        for (uint32_t bit = 0; bit < 32; ++bit) {
+                        for (uint32_t bit = 0; bit < kKgrp4Keys; ++bit) {
                             if (!((pres >> bit) & 1u)) continue;
                             ++n4;
                             if (j >= kKgrp4Fields) {
                                 pass4 += 1.0;
                                 continue;
                             }
-                            const uint32_t rank = rk[g].y + (uint32_t)__builtin_popcount(rk[g].x & ((1u << bit) - 1u));
+                            const uint32_t k = (uint32_t)(g0 + bit);
+                            const uint32_t rank = rk[k >> 5].y + (uint32_t)__builtin_popcount(rk[k >> 5].x & ((1u << (k & 31)) - 1u));
                             const uint32_t b = rank_bucket[rank];
                             const Entry& e = ents[boff[b]];
                             uint32_t f = 0;
