@@ -2315,16 +2315,12 @@ __device__ __forceinline__ bool tail_test(const ScanArgs& a, const TailRef& t, c
 // window whose gap matches the record exactly is left to the contiguous seed's scan.
 // (The same rules as tail_open / tail_test, which the fused pair check uses; written out here
 // in one body: through the helpers c4's tail pass took 0.062 ms against 0.054.)
-// Each thread takes kTailR references per pass, the head loads of its key references (rank
-// word, then head) in flight together.  (Measured on c4's ~16-22M key references: one, two
-// or four per thread ran within 4% of each other, 0.35-0.37 ms; kept at two.)
-#ifndef MP_TAIL_R
-#define MP_TAIL_R 2
-#endif
+// One reference per thread.  (Round 4 measured two and four per thread with their head loads
+// in flight together: c4's ~16M key references took 0.33-0.37 ms either way, bound by the
+// references' own traffic, and c3's / c5's tails took 17 us longer in that form.)
 #ifndef MP_TAIL_BPC
 #define MP_TAIL_BPC 2
 #endif
-constexpr int kTailR = MP_TAIL_R;
 constexpr uint32_t kTailBPC = MP_TAIL_BPC;  // blocks per CU
 template <bool kGap = false>
 __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
@@ -2336,67 +2332,41 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     const int lane = threadIdx.x & 63;
     const uint64_t n_refs = umin64(a.counters[a.tail_ctr], a.tails_cap);
     const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
-    const uint32_t W = (uint32_t)a.W;
     uint32_t ncand = 0, nsurv = 0;
-    auto key_of = [&](const uint4& w) {  // the seed key from the reference's window
-        const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);
-        return kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
-                    : (uint32_t)(Gs >> (64u - 2u * W));
-    };
-    const uint64_t stride = (uint64_t)gridDim.x * kTailBlock * kTailR;
-    for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock * kTailR; b < n_refs; b += stride) {  // block-uniform
-        uint4 v[kTailR], w[kTailR];
-        uint2 c[kTailR];
-#pragma unroll
-        for (int k = 0; k < kTailR; ++k) {
-            const uint64_t i = b + (uint64_t)k * kTailBlock + threadIdx.x;
-            v[k] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-            w[k] = make_uint4(0u, 0u, 0u, 0u);
-            if (i < n_refs) {
-                v[k] = a.tails[2 * i];
-                w[k] = a.tails[2 * i + 1];
-            }
+    // key references of a table with wide key groups: the 8-B IUPAC heads (kgrp_pass4)
+    const bool h12 = a.kgrp4 != nullptr;
+    const uint2* kref_heads = h12 ? a.dents12 : a.dents8;
+    const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
+    for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride) {  // block-uniform
+        const uint64_t i = b + threadIdx.x;
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
+        if (i < n_refs) {
+            v = a.tails[2 * i];
+            w = a.tails[2 * i + 1];
         }
-        // key references: the rank word, then the 8-B head (the 8-B IUPAC head on a table with
-        // wide key groups, whose scan left them)
-#pragma unroll
-        for (int k = 0; k < kTailR; ++k) {
-            c[k] = make_uint2(0u, 0u);
-            const bool live = !(v[k].x == 0xFFFFFFFFu && v[k].y == 0xFFFFFFFFu);
-            if (live && v[k].z == kKeyRef) c[k] = a.rk[key_of(w[k]) >> 5];
-        }
-        const bool h12 = a.kgrp4 != nullptr;
-        const uint2* kref_heads = h12 ? a.dents12 : a.dents8;
-#pragma unroll
-        for (int k = 0; k < kTailR; ++k) {
-            const bool live = !(v[k].x == 0xFFFFFFFFu && v[k].y == 0xFFFFFFFFu);
-            if (live && v[k].z == kKeyRef) {
-                const uint32_t h = key_of(w[k]);
-                c[k] = kref_heads[c[k].y + (uint32_t)__popc(c[k].x & ((1u << (h & 31u)) - 1u))];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kTailR; ++k) {
-            if (v[k].x == 0xFFFFFFFFu && v[k].y == 0xFFFFFFFFu) continue;
-            const uint64_t gp = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
-            const uint64_t Gs = (uint64_t)w[k].x | ((uint64_t)w[k].y << 32);  // window at the seed
-            const uint32_t rem = w[k].w;                                          // bases from the seed to the end
-            uint32_t first = v[k].z;
+        if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
+            const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
+            const uint32_t rem = w.w;                                    // bases from the seed to the end
+            uint32_t first = v.z;
             Entry e;
-            if (v[k].z == kKeyRef) {  // a seed that passed the key groups: its bucket's head
-                const uint32_t h = key_of(w[k]);
-                const uint2 cc = c[k];
-                if (cc.y & kHead8Full) {
-                    first = cc.x;  // the bucket's first entry
-                    if (cc.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
-                        const uint32_t cnt = ((cc.y >> 28) & 3u) + 1u;
+            if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
+                const uint32_t W = (uint32_t)a.W;
+                const uint32_t h = kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
+                                        : (uint32_t)(Gs >> (64u - 2u * W));
+                const uint2 rw = a.rk[h >> 5];
+                const uint2 c = kref_heads[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
+                if (c.y & kHead8Full) {
+                    first = c.x;  // the bucket's first entry
+                    if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
+                        const uint32_t cnt = ((c.y >> 28) & 3u) + 1u;
                         const uint32_t F = head8_filt_bases(cnt);
                         const uint32_t fm = (1u << (2u * F)) - 1u;
                         const uint32_t gf = (uint32_t)((Gs << (2u * W)) >> (64u - 2u * F));
-                        const uint32_t xf = w[k].z & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
+                        const uint32_t xf = w.z & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
                         bool any = xf != 0u;
                         for (uint32_t j = 0; j < cnt; ++j) {
-                            const uint32_t xj = gf ^ ((cc.y >> (2u * F * j)) & fm);
+                            const uint32_t xj = gf ^ ((c.y >> (2u * F * j)) & fm);
                             any = any || __popc((xj | (xj >> 1)) & 0x55555555u) <= a.N;
                         }
                         if (!any) first = 0xFFFFFFFFu;
@@ -2404,10 +2374,10 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                     if (first != 0xFFFFFFFFu) e = a.ents[first];
                     else e.count = 0;
                 } else {
-                    e = h12 ? head12_entry(cc, h, W) : head8_entry(cc, h, W);
+                    e = h12 ? head12_entry(c, h, W) : head8_entry(c, h, W);
                 }
             } else {
-                e = a.ents[first];  // its count = tail length
+                e = a.ents[first];                                       // its count = tail length
             }
             const uint32_t cnt = e.count;
             for (uint32_t j = 0; j < cnt; ++j) {
@@ -2415,9 +2385,9 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 const uint64_t gk = gp - e.hash_off;
                 if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) continue;  // k + l1 > n / not owned
                 uint64_t G = Gs;
-                uint32_t ex = w[k].z;
+                uint32_t ex = w.z;
                 if (e.hash_off) {  // seed inside the primer: bounds and window from the genome
-                    const uint64_t sbase = a.seq_base[v[k].w];
+                    const uint64_t sbase = a.seq_base[v.w];
                     if (gp - sbase < e.hash_off) continue;  // k < 0
                     G = ext2(a.g2, gk);
                     ex = (uint32_t)(ext1(exc, gk) >> 32);
@@ -2433,7 +2403,7 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 bool exact = false;
                 if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) continue;
                 ++nsurv;
-                const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v[k].w);
+                const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
                 const uint32_t at = atomicAdd(&s_n, 1u);
                 if (at < kTailBuf) {
                     s_buf[at] = sv;

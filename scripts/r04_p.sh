@@ -4,7 +4,7 @@ set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p gpurun_out
 T=${1:-r4p}
-for cfg in c3 c5; do
+for cfg in c3 c4 c5; do
   for lib in "" PRE "" PRE; do
     L=""; [ -n "$lib" ] && L=$PWD/merpcr_amd/_lib/libmerpcr_hip_ablate$lib.so
     MERPCR_LIB=$L timeout -k 10 300 python -u bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-e2e \
