@@ -2322,7 +2322,8 @@ __device__ __forceinline__ bool tail_test(const ScanArgs& a, const TailRef& t, c
 #define MP_TAIL_BPC 2
 #endif
 constexpr uint32_t kTailBPC = MP_TAIL_BPC;  // blocks per CU
-template <bool kGap = false>
+// kH12: the table has wide key groups (kgrp4), whose key references read the 8-B IUPAC heads
+template <bool kGap = false, bool kH12 = false>
 __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     __shared__ uint4 s_buf[kTailBuf];
     __shared__ uint32_t s_n;
@@ -2333,9 +2334,9 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     const uint64_t n_refs = umin64(a.counters[a.tail_ctr], a.tails_cap);
     const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
     uint32_t ncand = 0, nsurv = 0;
-    // key references of a table with wide key groups: the 8-B IUPAC heads (kgrp_pass4)
-    const bool h12 = a.kgrp4 != nullptr;
-    const uint2* kref_heads = h12 ? a.dents12 : a.dents8;
+    // key references of a table with wide key groups: the 8-B IUPAC heads (kgrp_pass4); a run-time
+    // choice here cost c3's tail 17 us
+    const uint2* kref_heads = kH12 ? a.dents12 : a.dents8;
     const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
     for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride) {  // block-uniform
         const uint64_t i = b + threadIdx.x;
@@ -2374,7 +2375,8 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                     if (first != 0xFFFFFFFFu) e = a.ents[first];
                     else e.count = 0;
                 } else {
-                    e = h12 ? head12_entry(c, h, W) : head8_entry(c, h, W);
+                    if constexpr (kH12) e = head12_entry(c, h, W);
+                    else e = head8_entry(c, h, W);
                 }
             } else {
                 e = a.ents[first];                                       // its count = tail length
@@ -2941,7 +2943,8 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         if (rc) return rc;
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
         if (tail && !fuse) {
-            hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, a);
+            if (t->kgrp4) hipLaunchKernelGGL((tail_kernel<false, true>), dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, a);
+            else hipLaunchKernelGGL((tail_kernel<false, false>), dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }
         fuse = fuse && tail;
