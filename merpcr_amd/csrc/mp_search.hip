@@ -843,8 +843,9 @@ struct SurvChunk {
     uint32_t total;  // entries of this wave (statistics)
 };
 constexpr uint32_t kChunkNone = 0xFFFFFFFFu;
-// Ranked key references per reservation (the wide key groups: c4 leaves ~20M, where 64-slot
-// reservations, ~94 per microsecond, saturated the list counter; c3's 5.5M keep 64)
+// Key references per reservation from the wide key groups (c4 leaves ~16M, where 64-slot
+// reservations, ~94 per microsecond, saturated the list counter; c3's 5.5M keep 64: 256 was
+// slower there, more empty slots for tail_kernel)
 constexpr uint32_t kRefChunk = 256;
 #ifndef MP_REF_CHUNK1
 #define MP_REF_CHUNK1 64
@@ -1628,8 +1629,8 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
 };
 
 // kRkf: 0 the rank queue and drain; 1 the key groups (kgrp, u64 per 16 keys); 2 the wide I = 1 key
-// groups (kgrp4, uint4 per 32 keys: presence, rank, fields) in place of the rank words, then the
-// ranked drain as for kRkf 0.
+// groups (kgrp4, uint4 per 32 keys: presence and three ten-base fields).  1 and 2 leave the seeds
+// that pass as key references for tail_kernel.
 template <int kMode, bool kInline, int kK = 1, bool kDefer = false, int kH16 = 0, int kRkf = 0,
           bool kGap = false>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
