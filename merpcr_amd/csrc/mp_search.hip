@@ -846,7 +846,10 @@ constexpr uint32_t kChunkNone = 0xFFFFFFFFu;
 // Key references per reservation from the wide key groups (c4 leaves ~16M, where 64-slot
 // reservations, ~94 per microsecond, saturated the list counter; c3's 5.5M keep 64: 256 was
 // slower there, more empty slots for tail_kernel)
-constexpr uint32_t kRefChunk = 256;
+#ifndef MP_REF_CHUNK
+#define MP_REF_CHUNK 256
+#endif
+constexpr uint32_t kRefChunk = MP_REF_CHUNK;
 #ifndef MP_REF_CHUNK1
 #define MP_REF_CHUNK1 64
 #endif
