@@ -55,10 +55,11 @@ def host_cores() -> int:
     return n
 
 
-def pmc_profile(workload: str):
-    """Newest committed PMC summary of this workload (profiles/<tag>_pmc.json next to the
-    bench line it was collected with; the highest round tag wins -- file times are those of
-    the checkout), or (None, None)."""
+def pmc_profile(workload: str, build: str):
+    """Newest committed PMC summary of this workload taken with THIS build (profiles/<tag>_pmc.json
+    whose "build" is the source digest of the library being benched, next to the bench line it
+    was collected with; the highest tag wins), or (None, None).  A profile of another build is
+    never used: its traffic would describe other kernels."""
     import glob
     best = None
     for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")):
@@ -70,18 +71,105 @@ def pmc_profile(workload: str):
             d = json.load(open(f))
         except (OSError, ValueError, KeyError):
             continue
+        if d.get("build") != build:
+            continue
         if "hbm_traffic_bytes_per_launch" in d and (best is None or tag > best[0]):
             best = (tag, d, tag)
     return (best[1], best[2]) if best else (None, None)
 
 
-def issue_bound(pmc: dict):
+# Live counter passes (MI355X_MICROARCH.md, rocprofv3 section): per pass at most 8 SQ, 4 TCC
+# (FETCH_SIZE takes 3, WRITE_SIZE 2) and 2 GRBM counters, and never a tracing domain beside --pmc.
+PMC_PASSES = [
+    ("fetch", ["FETCH_SIZE", "SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_LDS_IDX_ACTIVE",
+               "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE"]),
+    ("write", ["WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]),
+]
+
+
+def pmc_counters(csv_path: str) -> dict:
+    """Counter totals per search step from one rocprofv3 counter CSV: each dispatch's
+    instances summed, the dispatches of each kernel form averaged (a list that overflowed
+    and was rerun adds dispatches of the same form), and the forms of the step summed (a split
+    W 7..9 table's step is two or three scan launches)."""
+    import collections
+    import csv
+    per = collections.defaultdict(float)
+    names = {}
+    for r in csv.DictReader(open(csv_path)):
+        key = (r["Dispatch_Id"], r["Counter_Name"])
+        per[key] += float(r["Counter_Value"])
+        names[r["Dispatch_Id"]] = r["Kernel_Name"]
+    by_form = collections.defaultdict(list)
+    for (d, c), v in per.items():
+        by_form[(names[d], c)].append(v)
+    out = collections.defaultdict(float)
+    for (_, c), v in by_form.items():
+        out[c] += sum(v) / len(v)
+    return dict(out)
+
+
+def pmc_child_args(argv):
+    """The caller's workload options for a counter pass, without its step counts and extras."""
+    skip = {"--gpus", "--steps", "--warmup", "--cpu-budget", "--cpu-threads", "--handles"}
+    flags = {"--no-cpu-baseline", "--no-e2e", "--no-ref-model", "--e2e-file", "--no-pmc", "--pmc-child"}
+    child, i = [], 0
+    while i < len(argv):
+        a = argv[i]
+        key = a.split("=")[0]
+        if key in skip:
+            i += 1 if "=" in a else 2
+            continue
+        if a not in flags:
+            child.append(a)
+        i += 1
+    return child + ["--pmc-child", "--no-cpu-baseline", "--no-e2e", "--steps", "2", "--warmup", "1"]
+
+
+def live_pmc(argv, kernel_regex: str, timeout_s: float = 150.0):
+    """HBM traffic and issue counters of the scan stage measured in THIS bench invocation:
+    rocprofv3 --pmc child passes of this script (--pmc-child: the same workload, build and
+    options; setup and three searches, nothing else), one pass per counter set.  Returns
+    (counters per step, note) or (None, reason)."""
+    import glob
+    import shutil
+    import subprocess
+    prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if prof is None:
+        return None, "rocprofv3 not found"
+    child = pmc_child_args(argv)
+    ctr = {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        for name, counters in PMC_PASSES:
+            out = os.path.join(td, name)
+            cmd = [prof, "--pmc", *counters, "--kernel-include-regex", kernel_regex, "-d", out, "-o", "run",
+                   "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), *child]
+            try:
+                res = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, cwd=td,
+                                     env=dict(os.environ, TMPDIR=td))
+            except subprocess.TimeoutExpired:
+                return None, f"pass {name}: rocprofv3 timed out after {timeout_s:.0f} s"
+            if res.returncode:
+                return None, f"pass {name}: rocprofv3 exit {res.returncode}: {res.stderr[-300:]}"
+            files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+            if not files:
+                return None, f"pass {name}: no counter CSV"
+            for f in files:
+                ctr.update(pmc_counters(f))
+    missing = [c for _, cs in PMC_PASSES for c in cs if c not in ctr]
+    if missing:
+        return None, f"counters missing from the passes: {missing}"
+    return ctr, (f"live: {len(PMC_PASSES)} rocprofv3 --pmc passes of this bench command (--pmc-child: same build, "
+                 f"workload and options), kernels /{kernel_regex}/, counters per search step")
+
+
+def issue_bound(pmc: dict, dur_ns=None):
     """Issue-side utilisation of the dominant kernel from its committed PMC passes:
     VALU = SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (1024 SIMDs x kernel cycles),
     kernel cycles = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs); LDS = LDS-array cycles
     (SQ_LDS_IDX_ACTIVE) / (256 CUs x kernel cycles); the bank-conflict share of them; and the
     L2 request rate against the ~270G/s line ceiling (34.5 TB/s / 128 B)."""
-    c = pmc.get("counters_mean_per_dispatch", {})
+    c = pmc.get("counters_mean_per_dispatch", pmc)
     out = {}
     cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
     if cyc > 0 and "SQ_INSTS_VALU" in c:
@@ -93,7 +181,7 @@ def issue_bound(pmc: dict):
     if "SQ_WAIT_ANY" in c and c.get("SQ_WAVE_CYCLES"):
         out["wave_wait_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
     req = c.get("TCC_REQ_sum") or (c.get("TCC_HIT_sum", 0.0) + c.get("TCC_MISS_sum", 0.0))
-    dur = pmc.get("avg_duration_ns_trace")
+    dur = dur_ns or pmc.get("avg_duration_ns_trace")
     if req and dur:
         out["l2_req_per_launch"] = int(req)
         out["l2_req_frac"] = round(req / (dur * 1e-9) / L2_REQ_PEAK, 4)
@@ -295,9 +383,43 @@ def end_to_end_file(sts_path, names, lens, buf, offs, cfg, device):
                     "time (interpreter start, FASTA parse, upload + pack, search, format, write); not the metric"}
 
 
+def free_port() -> int:
+    """A TCP port on 127.0.0.1 that nothing listens on right now (the child job's rendezvous)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launcher_command(argv, n: int, port: int):
+    """The one-rank-per-GPU job `bench.py --gpus N` starts for itself when it was not launched
+    by torch.distributed.run: the same arguments, N local ranks, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def resolve_world(gpus, env) -> tuple:
+    """(ranks, launch): how many ranks the job has and whether this process must start them.
+    WORLD_SIZE set (torch.distributed.run): it is the rank count, and an explicit --gpus must
+    agree with it.  Unset: --gpus N > 1 means launch N ranks as a child job; 1 (or no flag) is
+    the single-process N=1 bench."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if gpus is not None and int(ws) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws} (launched with "
+                             f"{ws} ranks); pass the same N to both or drop --gpus")
+        return int(ws), False
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {n}")
+    return n, n > 1
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); N > 1 without torch.distributed.run launches "
+                         "the N-rank job itself (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"])
@@ -323,15 +445,25 @@ def main():
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic: time only rank 0's owned range of an N-way split on this one GPU "
                          "(no collective); the JSON line is then not the metric")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live rocprofv3 counter passes (roofline.traffic / issue)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # live_pmc's passes
     ap.add_argument("--opts", default="",
                     help="diagnostic A/B: search options for every handle, name=value[,...] (_native.Search.set_options)")
     args = ap.parse_args()
+    # N > 1 and no launcher: start the N-rank job as a child before anything touches the GPU
+    # (this process never initialises HIP), and exit with its code
+    world, launch = resolve_world(args.gpus, os.environ)
+    if launch:
+        import subprocess
+        cmd = launcher_command(sys.argv[1:], world, free_port())
+        log("launching: " + " ".join(cmd))
+        sys.exit(subprocess.call(cmd, cwd=ROOT))
 
     import torch
     from merpcr_amd import MerPCR, _native, synth
     from merpcr_amd.dist import HIT_BYTES, native_comm, shard_ranges
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -397,7 +529,7 @@ def main():
         for item in args.opts.split(","):
             k, val = item.split("=")
             kw[k] = val if k in ("tails", "sort") else (val.lower() in ("1", "true") if k in (
-                "defer", "dense", "rank_filter", "split", "fuse_tails") else int(val))
+                "defer", "dense", "rank_filter", "split") else int(val))
         for h in handles:
             h.set_options(**kw)
     # one stream per handle (--one-stream: all on the default stream): step i+1's scan may then
@@ -486,6 +618,11 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     timed_scan_ms = list(scan_ms)
+    if args.pmc_child:  # a counter pass of live_pmc: the counters are all it is for
+        for h in handles:
+            h.close()
+        print(json.dumps({"pmc_child": True, "runs": args.warmup + args.steps}), flush=True)
+        return
     # single-search latency beside the pipelined step: handle 0 alone, each run enqueued only
     # after the previous one completed (host turnaround included, no events), median of 5
     single_ms = None
@@ -563,8 +700,23 @@ def main():
                 f"W={cfg['W']} N={cfg['N']} M={cfg['M']} I={cfg['I']}")
     if world > 1 and weak:
         workload += f" per rank ({world} contig sets, {tot_bases / 1e9:.3f} Gbp in all)"
-    pmc, pmc_tag = pmc_profile(workload) if world == 1 and args.shard_of <= 1 else (None, None)
-    traffic = pmc["hbm_traffic_bytes_per_launch"] if pmc else None
+    from merpcr_amd._build import source_digest
+    build = source_digest()
+    # roofline.traffic / issue: counters measured now, in child passes of this very command;
+    # failing that, a committed profile of this same build; else null with the reason
+    pmc, pmc_src, traffic, why = None, None, None, "not measured for N > 1 or shard runs"
+    if world == 1 and args.shard_of <= 1:
+        regex = "scan_kernel|dense_kernel" if (sp["seed_tables"] or cfg["W"] <= 9) else "scan_kernel"
+        live, why = (None, "--no-pmc") if args.no_pmc else live_pmc(sys.argv[1:], regex)
+        if live is not None:
+            pmc, pmc_src = live, why
+            traffic = 2.0 * live["FETCH_SIZE"] * 1024 + live["WRITE_SIZE"] * 1024
+        else:
+            log(f"live counters unavailable ({why}); looking for a committed profile of build {build}")
+            prof, tag = pmc_profile(workload, build)
+            if prof is not None:
+                pmc, pmc_src = prof, f"profiles/{tag}_pmc.json (committed profile of this build)"
+                traffic = prof["hbm_traffic_bytes_per_launch"]
     out = {
         "metric": METRIC,
         "value": round(tot_bases / max(args.shard_of, 1) / t_step / 1e9, 4),
@@ -596,11 +748,13 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": int(traffic) if traffic else None,
-                     "traffic_source": f"profiles/{pmc_tag}_pmc.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, "
-                                       "gfx950-corrected; includes Infinity-Cache hits)" if traffic else None,
+                     "traffic_source": (pmc_src + "; 2 x FETCH_SIZE KiB (gfx950 half-count) + WRITE_SIZE KiB, "
+                                        "Infinity-Cache hits included") if traffic else None,
+                     "traffic_null_reason": None if traffic else why,
                      "kernel": scan_label,
                      "alg_bytes_per_launch": int(alg_bytes),
-                     "issue": (dict(issue_bound(pmc), source=f"profiles/{pmc_tag}_pmc.json") if pmc else None)},
+                     "issue": (dict(issue_bound(pmc, kern_s * 1e9), source=pmc_src) if pmc else None)},
+        "build": build,
         "setup_s": round(setup_s, 2),
         "single_run_note": "one isolated search (enqueue -> complete, host turnaround included) on one handle, "
                            "median of 5 after the timed steps; ms_per_step is the pipelined throughput",

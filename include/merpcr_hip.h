@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 1
+#define MP_ABI_VERSION 2  /* 2: mp_search_options without fuse_tails; mp_table_layout */
 
 #define MP_OK 0
 #define MP_E_ARG (-1)     /* bad argument (maps to ValueError) */
@@ -91,6 +91,15 @@ int mp_table_stats(void* table, uint64_t* n_keys, uint64_t* max_bucket, uint64_t
  * scans, mp_internal.h kSplitSeed): seed_tables = 0 (not split), 1 (the contiguous seed, N = 0) or 2
  * (contiguous + gapped, N = 1); rest_records = records left to the dense scan. */
 int mp_table_split(void* table, uint32_t* seed_tables, uint32_t* rest_records);
+/* Which seed structures the table holds (what its scans will take), as MP_LAYOUT_* bits. */
+#define MP_LAYOUT_LDS_EXACT 1u /* the LDS prefilter is the exact 4^W bitmap (W <= 10) */
+#define MP_LAYOUT_RANK 2u      /* rank words + bucket heads (W <= 13) */
+#define MP_LAYOUT_KGRP 4u      /* key groups, one u64 per 16 keys (W 11..13) */
+#define MP_LAYOUT_KGRP4 8u     /* wide I = 1 key groups, one 16-B word per 32 keys */
+#define MP_LAYOUT_DENSE 16u    /* dense_kernel structures (W <= 9) */
+#define MP_LAYOUT_SPLIT 32u    /* split seeds (mp_table_split) */
+#define MP_LAYOUT_HASHED 64u   /* hashed presence filter + open-addressed slots (W >= 14) */
+int mp_table_layout(void* table, uint32_t* flags);
 void mp_table_destroy(void* table);
 
 /* ---- genome (replaces the per-record sequence strings that search() walks,
@@ -149,9 +158,6 @@ typedef struct mp_search_options {
                                    filtered rank groups' primer-base filter */
     int32_t no_split;           /* 1: W 7..9 tables keep the dense scan, not the split seeds
                                    (two exact-seed scans, see mp_internal.h kSplitSeed) */
-    int32_t fuse_tails;         /* 1: bucket-tail references opened inside the pair check
-                                   instead of by their own kernel (tail_kernel); one-table
-                                   runs only.  Off by default: no gain measured */
 } mp_search_options;
 /* Replace the handle's options (reallocating the lists to the given capacities). */
 int mp_search_set_options(void* search, const mp_search_options* opt);

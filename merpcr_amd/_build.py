@@ -23,6 +23,17 @@ ARCH = os.environ.get("MERPCR_OFFLOAD_ARCH", "gfx950")
 SOURCE_FLAGS = {"mp_search.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
 
 
+def source_digest(src_dir: str = CSRC) -> str:
+    """16 hex digits of sha256 over the library's sources and headers: the build a bench line
+    or a profile was taken with (profiles/*_pmc.json record it; bench.py matches on it)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        with open(os.path.normpath(os.path.join(src_dir, f)), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and os.path.exists(cand):

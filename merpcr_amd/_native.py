@@ -29,7 +29,7 @@ MP_STS_OK, MP_STS_BAD_LINE, MP_STS_PYTHON = 0, 1, 2
 # every symbol include/merpcr_hip.h declares
 EXPORTS = (
     "mp_abi_version", "mp_last_error", "mp_device_count",
-    "mp_table_create", "mp_table_stats", "mp_table_split", "mp_table_destroy",
+    "mp_table_create", "mp_table_stats", "mp_table_split", "mp_table_layout", "mp_table_destroy",
     "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
     "mp_genome_stats", "mp_genome_download", "mp_genome_reset", "mp_genome_destroy",
     "mp_search_create", "mp_search_set_options", "mp_search_set_stage_timing", "mp_search_set_scan_timing", "mp_search_run",
@@ -64,7 +64,7 @@ class MPSearchOptions(ctypes.Structure):
     _fields_ = [("tails", c_int32), ("no_defer", c_int32), ("no_dense", c_int32), ("sort", c_int32),
                 ("sort_bucket_bits", c_int32), ("pair_blocks_per_cu", c_int32),
                 ("hit_cap", c_uint64), ("surv_cap", c_uint64), ("tail_cap", c_uint64),
-                ("no_rank_filter", c_int32), ("no_split", c_int32), ("fuse_tails", c_int32)]
+                ("no_rank_filter", c_int32), ("no_split", c_int32)]
 
 
 HIT_DTYPE = np.dtype([("pos1", "<u8"), ("pos2", "<u8"), ("seq", "<u4"), ("rec", "<u4")])
@@ -106,6 +106,7 @@ def _sig(lib):
                                     POINTER(c_void_p)]
     lib.mp_table_stats.argtypes = [P, u64p, u64p, u64p]
     lib.mp_table_split.argtypes = [P, POINTER(c_uint32), POINTER(c_uint32)]
+    lib.mp_table_layout.argtypes = [P, POINTER(c_uint32)]
     lib.mp_table_destroy.argtypes = [P]
     lib.mp_table_destroy.restype = None
     lib.mp_genome_create.argtypes = [c_int32, c_uint32, P, POINTER(c_void_p)]
@@ -207,7 +208,7 @@ def lib():
         _share_hip_runtime()
         l = ctypes.CDLL(LIB_PATH)
         _sig(l)
-        if l.mp_abi_version() != 1:
+        if l.mp_abi_version() != 2:
             raise RuntimeError("libmerpcr_hip ABI version mismatch")
         _lib = l
     return _lib
@@ -261,6 +262,14 @@ class Table:
         a, b = c_uint32(), c_uint32()
         check(lib().mp_table_split(self._h, ctypes.byref(a), ctypes.byref(b)))
         return {"seed_tables": a.value, "rest_records": b.value}
+
+    LAYOUT = {"lds_exact": 1, "rank": 2, "kgrp": 4, "kgrp4": 8, "dense": 16, "split": 32, "hashed": 64}
+
+    def layout(self) -> set:
+        """The seed structures the table holds (mp_table_layout), by name."""
+        f = c_uint32()
+        check(lib().mp_table_layout(self._h, ctypes.byref(f)))
+        return {k for k, b in self.LAYOUT.items() if f.value & b}
 
     def close(self):
         if self._h:
@@ -336,13 +345,12 @@ class Search:
         check(lib().mp_search_create(table._h, genome._h, ctypes.byref(self._h)))
 
     def set_options(self, tails="auto", defer=True, dense=True, sort="auto", sort_bucket_bits=0,
-                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True, split=True,
-                    fuse_tails=False):
+                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True, split=True):
         """Kernel-path selection and initial list capacities (mp_search_set_options);
         the defaults are the library's automatic choices."""
         o = MPSearchOptions(MP_TAILS[tails], 0 if defer else 1, 0 if dense else 1, MP_SORT[sort],
                             sort_bucket_bits, pair_blocks_per_cu, hit_cap, surv_cap, tail_cap,
-                            0 if rank_filter else 1, 0 if split else 1, 1 if fuse_tails else 0)
+                            0 if rank_filter else 1, 0 if split else 1)
         check(lib().mp_search_set_options(self._h, ctypes.byref(o)))
 
     def set_stage_timing(self, on: bool):

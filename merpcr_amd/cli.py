@@ -128,7 +128,8 @@ def main(argv: List[str] = None) -> int:
             prep = threading.Thread(target=eng.prepare_device, daemon=True)
             prep.start()
         try:
-            records = eng.load_fasta_file(args.fasta_file)
+            # the CLI searches what it reads: large ASCII files are ingested on the GPU
+            records = eng.load_fasta_file(args.fasta_file, on_device=True)
         finally:
             if prep is not None:
                 prep.join()

@@ -247,8 +247,6 @@ class MerPCR:
         self.sts_table: Dict[int, List[STSRecord]] = {}
         self.max_pcr_size = 0
         self.total_hits = 0
-        self._sts_keys: List[int] = []
-        self._sts_keys_p1: List[str] = []
         self._dev_table = None
         self._dev_table_sig = None
         self._codes = CharCodes()
@@ -304,8 +302,6 @@ class MerPCR:
         logger.info(f"Reading STS file: {filename}")
         self.sts_records = []
         self.sts_table = {}
-        self._sts_keys = []
-        self._sts_keys_p1 = []
         self.max_pcr_size = 0
         self._dev_table = None
         self._native_arrays = None
@@ -329,7 +325,6 @@ class MerPCR:
         src.recs = self._recs = _LazyRecords(src, n)
         src.table = self._table = _LazyTable(src)
         self._sts_src = src
-        self._sts_keys = r["key"].tolist()
         self.max_pcr_size = r["max_pcr_size"]
         self._native_arrays = (self._recs, n, (r["key"], r["hash_off"], r["pcr_size"], r["p1"], r["p1_off"],
                                                      r["p2"], r["p2_off"]))
@@ -418,8 +413,6 @@ class MerPCR:
         """Append to the key's bucket and the flat record list (engine.py:324-329)."""
         self.sts_table.setdefault(hash_value, []).append(sts)
         self.sts_records.append(sts)
-        self._sts_keys.append(hash_value)
-        self._sts_keys_p1.append(sts.primer1)
 
     def _hash_value(self, primer: str) -> Tuple[int, int]:
         """(offset, value) of the first all-ACGTU W-mer (engine.py:331-355).
@@ -482,11 +475,13 @@ class MerPCR:
                     return False
         return True
 
-    def load_fasta_file(self, filename: str) -> List[FASTARecord]:
-        """FASTA records with the reference's filter (io/fasta.py:18-71).  A single-device
-        engine ingests large ASCII files on its GPU (the sequences stay there for the
-        search; FASTALoader.load_file's device form)."""
-        return FASTALoader.load_file(filename, device=self.device if len(self.devices) == 1 else None)
+    def load_fasta_file(self, filename: str, *, on_device: bool = False) -> List[FASTARecord]:
+        """FASTA records with the reference's filter (io/fasta.py:18-71).  With on_device=True
+        (the CLI, which searches what it reads) a single-device engine ingests large ASCII
+        files on its GPU, and the sequences stay there for the search (FASTALoader.load_file's
+        device form); by default the records are host strings, as the reference's are."""
+        dev = self.device if on_device and len(self.devices) == 1 else None
+        return FASTALoader.load_file(filename, device=dev)
 
     # ------------------------------------------------------------------ device
     def _params(self):
@@ -516,18 +511,26 @@ class MerPCR:
         return ("objects", hash(tuple((r.id, r.alias, r.direct, r.primer1, r.primer2, r.pcr_size, r.hash_offset)
                                       for r in self._recs)))
 
+    def _record_keys(self, recs) -> np.ndarray:
+        """Each record's seed key: the one it is filed under in sts_table.  The reference finds a
+        record only through its load-time bucket (engine.py:265-279, 483-486), whatever its
+        primer holds after an edit in place, and takes hash_offset from the record itself.  A
+        record the caller put in sts_records alone is keyed by its primer as the loader would
+        have keyed it."""
+        filed = {}
+        for h, lst in self.sts_table.items():
+            for r in lst:
+                filed.setdefault(id(r), h)
+        return np.fromiter((filed[id(r)] if id(r) in filed else self._hash_value(r.primer1)[1] for r in recs),
+                           dtype=np.uint32, count=len(recs))
+
     def _table_arrays(self):
         """Record arrays for mp_table_create in sts_records order."""
         recs = self._recs
         na = getattr(self, "_native_arrays", None)
         if self._native_current():
             return na[2]
-        p1s = [r.primer1 for r in recs]
-        if getattr(self, "_sts_keys_p1", None) != p1s or len(self._sts_keys) != len(recs):
-            # the loader's keys, unless a primer was edited since (or records were added)
-            self._sts_keys = [self._hash_value(p)[1] for p in p1s]
-        self._sts_keys_p1 = p1s
-        key = np.asarray(self._sts_keys, dtype=np.uint32)
+        key = self._record_keys(recs)
         hash_off = np.fromiter((r.hash_offset for r in recs), dtype=np.uint32, count=len(recs))
         size = np.fromiter((r.pcr_size for r in recs), dtype=np.uint64, count=len(recs))
         p1 = [self._codes.primer_bytes(r.primer1) for r in recs]

@@ -33,7 +33,10 @@ namespace mp {
 
 constexpr uint32_t kFaTile = 65536;          // bytes per compaction tile (one 1024-thread block)
 constexpr uint32_t kFaPerThread = 64;        // bytes per thread of a tile
-constexpr uint32_t kMaxHeaders = 1u << 20;   // header lines the device path takes
+// Header lines the device path takes.  Its per-record cost is a pread of each header line on
+// the host and two 1024-thread blocks of fa_points_kernel per record (each rescans a tile), so
+// a file of many short records (reads, ESTs) is the host reader's: it has no per-record pass.
+constexpr uint32_t kMaxHeaders = 1u << 16;
 static_assert(kFaTile == 1024 * kFaPerThread, "one tile per 1024-thread block");
 
 // Keep set of fasta.py:60 over ASCII: the letters A B C D G H K M N R S T V W X Y, either case.

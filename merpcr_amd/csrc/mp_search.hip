@@ -107,7 +107,6 @@ struct ScanArgs {
     // bases and the gap_post bases after the seed's span.
     uint32_t gap_at, gap_len, gap_post;
     uint32_t tail_ctr;      // counters[] slot of this scan's bucket-tail list (4; 5 for the gapped scan)
-    uint32_t fuse_tails;    // pair_kernel also opens the bucket-tail references (no tail_kernel)
     uint32_t sched_base;    // counters[] index of this scan's 8 chunk counters (kSchedBase, kSchedSplit...)
 };
 
@@ -1400,12 +1399,8 @@ __device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, 
 template <bool kGap = false>
 __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
     const uint32_t bit = pk & 15u;
-    const uint32_t present = (rw.x >> bit) & 1u;
-#ifndef MP_KGRP_BRANCHFREE
-    if (!present) return false;
-#endif
+    if (!((rw.x >> bit) & 1u)) return false;  // the key is absent
     if constexpr (kGap) {
-        if (!present) return false;
         const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
         if (j >= kKgrpFields) return true;
         const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
@@ -1425,7 +1420,6 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         return (uint32_t)__popc(m) <= (uint32_t)a.N && ((m >> (2u * a.gap_post)) != 0u || (pk >> 31) != 0u);
     }
     if (a.kgrp_wild) {
-        if (!present) return false;
         if (pk >> 31) return true;
         const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
         if (j >= kKgrpWildFields) return true;
@@ -1434,26 +1428,6 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
         return (uint32_t)__popc((x | (x >> 1)) & 0x555u & ~(field >> 12)) <= (uint32_t)a.N;
     }
-#ifdef MP_KGRP_BRANCHFREE
-    // Branch-free (round 4): every form is computed and selected, so the probe pass has no
-    // exec-mask branches (the branchy form spent ~45-60 instructions per pass, most of them
-    // SALU exec juggling, ISA of scan_kernel<1,false,2,true,0,true,false>).
-    const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
-    const uint64_t w64 = ((uint64_t)rw.y << 32) | rw.x;
-    const uint32_t field = (uint32_t)(w64 >> (16u + 16u * min(j, kKgrpFields - 1u))) & 0xFFFFu;
-    // one plain record: bases W..W+F-1 within N
-    const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
-    const uint32_t s_ok = (uint32_t)__popc((x | (x >> 1)) & 0x55555555u) <= (uint32_t)a.N;
-    // two records: the window's bases W..W+2 (the top 3 of its F) against each record's
-    const uint32_t g3 = (pk >> (4u + 2u * (a.kgrp_F - 3u))) & 63u;
-    const uint32_t x0 = g3 ^ ((field >> 6) & 63u), x1 = g3 ^ (field & 63u);
-    const uint32_t p_ok = ((uint32_t)__popc((x0 | (x0 >> 1)) & 0x15u) <= (uint32_t)a.N) |
-                          ((uint32_t)__popc((x1 | (x1 >> 1)) & 0x15u) <= (uint32_t)a.N);
-    const uint32_t flag = (field >> 15) & 1u, pair = (field >> 14) & 1u;
-    static_assert(kKgrpFlag == 0x8000u && kKgrpPair == 0x4000u, "field flag bits");
-    const uint32_t ok = (uint32_t)(j >= kKgrpFields) | (flag & s_ok) | ((flag ^ 1u) & ((pair ^ 1u) | p_ok));
-    return (present & ok) != 0u;
-#else
     const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
     if (j >= kKgrpFields) return true;
     const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
@@ -1466,7 +1440,6 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
     }
     const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
     return __popc((x | (x >> 1)) & 0x55555555u) <= a.N;
-#endif
 }
 
 // Level-2 probe of the wide I = 1 key groups (kgrp4, see kKgrp4Keys).  `pk`: the window's
@@ -1522,9 +1495,6 @@ constexpr uint32_t kSChunkShort = 128;
 // super-steps at ~11 us each and waves 0-3 did 60 at ~5 us; with fixed chunks of 4 and one
 // chunk claimed ahead the young waves ended 20 us after the old ones and the last wave 47 us
 // after the first.
-#ifndef MP_STEAL_MIN
-#define MP_STEAL_MIN 1u
-#endif
 struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives beside the scan's registers
     uint32_t lo, hi, nw, end;  // XCD group range, waves of the group, end of the current chunk
     uint32_t S;                // end of the static first chunks: dynamic positions count from here
@@ -1554,7 +1524,6 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         S = min(lo + nw * chunk, hi);
         young = (uint32_t)w >= (uint32_t)kW / 2u;
         const uint32_t st = lo + ((blockIdx.x / g) * (uint32_t)kW + (uint32_t)w) * chunk;
-        lo = x;  // from here on: the group being claimed from (steal)
         end = min(st + chunk, hi);
         hint = st;
         claim(lane);
@@ -1569,21 +1538,13 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         pending = 0;
         if (lane == 0) pending = atomicAdd(ctr, sz);
     }
-    template <bool kSteal = true>
-    __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane, int kW) {
+    __device__ __forceinline__ uint64_t next(uint64_t ss, uint64_t n_supers, int lane) {
         if (stride) return ss + stride;
         if (ss + 1 < end) return ss + 1;
         // lane 0 holds the claimed position; next() runs at the top of the super-step loop
         // with every lane active, so the first active lane is lane 0 and the broadcast is a
         // readfirstlane (the scheduler state then stays in scalar registers)
         uint32_t st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);
-#ifdef MP_STEAL
-        while (kSteal && st >= hi) {  // this group's range is claimed out: help a group that is behind
-            if (!steal(n_supers, kW, lane)) break;
-            claim(lane);
-            st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);
-        }
-#endif
         if (st >= hi) {
             end = 0;
             return n_supers;
@@ -1592,42 +1553,6 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
         hint = st;
         claim(lane);
         return st;
-    }
-    // End-of-scan stealing across XCD groups, in the fields the scheduler already has (a
-    // wider state spilled the scan kernel's SGPRs): lo, unused after first(), names the group
-    // being claimed from; ctr, hi, S and nw are re-pointed at the next group (x + 1, x + 2,
-    // ... around to the home group) whose counter still lies inside its range, read first
-    // with a plain atomic load so that exhausted counters take no read-modify-write.  The
-    // groups' eighths cost 7.7-8.1 us per super-step and wave, differently run to run, and
-    // ended up to 18 us apart without it.  Claims there are of one super-step.
-    __device__ __forceinline__ bool steal(uint64_t n_supers, int kW, int lane) {
-        if (gridDim.x < 8u) return false;  // eight groups (every full-chip grid): shifts, no division
-        const uint32_t home = blockIdx.x & 7u;
-        uint32_t x = lo;
-        for (uint32_t t = 1; t < 8u; ++t) {
-            const uint32_t nx = (x + 1u) & 7u;
-            if (nx == home) return false;
-            ctr += ((int)nx - (int)x) * (int)(2 * kStatStride);  // u32 units
-            x = nx;
-            const uint32_t h = (uint32_t)((n_supers * (x + 1)) >> 3);
-            const uint32_t s0 = min((uint32_t)((n_supers * x) >> 3) + ((gridDim.x - x + 7u) >> 3) * (uint32_t)kW * chunk, h);
-            uint32_t cur = 0;
-            if (lane == 0) cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur);
-            // only a group with more than MP_STEAL_MIN super-steps per wave of its own left:
-            // below that its waves finish it as soon, and stealers' atomics on its counter
-            // (same-address atomics serialise, ~88 per us) would only slow its own claims
-            const uint32_t own = ((gridDim.x - x + 7u) >> 3) * (uint32_t)kW;
-            if (s0 + cur + MP_STEAL_MIN * own < h) {
-                lo = x;
-                hi = h;
-                S = s0;
-                hint = h;  // guided size from a range with nothing left: claims of one
-                young = 0;
-                return true;
-            }
-        }
-        return false;
     }
 };
 
@@ -1720,9 +1645,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                                          window_ok_mask(R.iv << (a.gap_at + a.gap_len), W - a.gap_at)
                                    : window_ok_mask(R.iv, W)) &
                              span_bits(sp, pb);
-        // stealing in the kernels whose registers have room for it (the deferring rank/key-group
-        // scans of c2-c5); the others would spill VGPRs to scratch
-        const uint64_t nx = sch.template next<kMode == 1 && kDefer>(ss, n_supers, lane, kWaves);
+        const uint64_t nx = sch.next(ss, n_supers, lane);
         (void)stride;
         if constexpr (kMode == 1) {
             // level 2, wave-compacted: the wave's LDS-positive windows go into the LDS list
@@ -2099,7 +2022,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         // otherwise; under I=0 such a base reads as 'A' and can only hide a mismatch, and U
         // compares as T under I=1)
         const uint32_t slowm = a.I ? ~window_ok_mask(iv, 16u) : 0u;
-        const uint64_t nx = sch.next(ss, n_supers, lane, kWaves);
+        const uint64_t nx = sch.next(ss, n_supers, lane);
         (void)stride;
         if (nx < n_supers) {  // next super-step's words, in flight during this one
             locate(nx);
@@ -2230,95 +2153,8 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
     __syncthreads();
 }
 
-// One bucket-tail reference opened: its bucket (first ents index, record count, the first
-// record's Entry) and what the record tests need from the reference.  A key reference
-// (scan_kernel's key-group path) finds its bucket from the key by rank; a head8 bucket whose
-// filter bases rule out every record is empty (cnt = 0).
-struct TailRef {
-    uint64_t gp, Gs;         // seed position (global) and the 32-base window at it
-    uint32_t ex, rem, seq;   // exception bits of the window, bases from the seed to the end, sequence
-    uint32_t first, cnt;     // the bucket's first ents index and its records
-    Entry e0;                // its first record
-};
-
-template <bool kGap>
-__device__ __forceinline__ void tail_open(const ScanArgs& a, const uint4 v, const uint4 w, TailRef& t) {
-    t.cnt = 0;
-    if (v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu) return;
-    t.gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
-    t.Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);
-    t.ex = w.z;
-    t.rem = w.w;
-    t.seq = v.w;
-    uint32_t first = v.z;
-    Entry e;
-    if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
-        const uint32_t W = (uint32_t)a.W;
-        const uint32_t h = kGap ? gap_key((uint32_t)(t.Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
-                                : (uint32_t)(t.Gs >> (64u - 2u * W));
-        const uint2 rw = a.rk[h >> 5];
-        const uint2 c = a.dents8[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
-        if (c.y & kHead8Full) {
-            first = c.x;  // the bucket's first entry
-            if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
-                const uint32_t cnt = ((c.y >> 28) & 3u) + 1u;
-                const uint32_t F = head8_filt_bases(cnt);
-                const uint32_t fm = (1u << (2u * F)) - 1u;
-                const uint32_t gf = (uint32_t)((t.Gs << (2u * W)) >> (64u - 2u * F));
-                const uint32_t xf = t.ex & (0xFFFFFFFFu >> W) & ~(0xFFFFFFFFu >> (W + F));
-                bool any = xf != 0u;
-                for (uint32_t j = 0; j < cnt; ++j) {
-                    const uint32_t xj = gf ^ ((c.y >> (2u * F * j)) & fm);
-                    any = any || __popc((xj | (xj >> 1)) & 0x55555555u) <= a.N;
-                }
-                if (!any) return;
-            }
-            e = a.ents[first];
-        } else {
-            e = head8_entry(c, h, W);
-        }
-    } else {
-        e = a.ents[first];  // its count = tail length
-    }
-    t.first = first;
-    t.cnt = e.count;
-    t.e0 = e;
-}
-
-// Record e of an opened reference: bounds, ownership, the gapped seed's exact-gap rule and
-// the fingerprint test (fp_reject); a survivor in *sv.
-template <bool kGap>
-__device__ __forceinline__ bool tail_test(const ScanArgs& a, const TailRef& t, const Entry& e, uint32_t& ncand,
-                                          uint4& sv) {
-    const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
-    const uint64_t gk = t.gp - e.hash_off;
-    if ((uint32_t)e.l1 > t.rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) return false;  // k + l1 > n / not owned
-    uint64_t G = t.Gs;
-    uint32_t ex = t.ex;
-    if (e.hash_off) {  // seed inside the primer: bounds and window from the genome
-        const uint64_t sbase = a.seq_base[t.seq];
-        if (t.gp - sbase < e.hash_off) return false;  // k < 0
-        G = ext2(a.g2, gk);
-        ex = (uint32_t)(ext1(exc, gk) >> 32);
-    }
-    if constexpr (kGap) {  // a window whose gap matches exactly is the contiguous seed's
-        const uint64_t gm = sp_lt((int)(a.gap_at + a.gap_len)) & ~sp_lt((int)a.gap_at);
-        const uint64_t xg = G ^ e.code;
-        const uint32_t inv = a.has_u ? (uint32_t)(ext1(a.ginv, gk) >> 32) : ex;  // A/C/G/T/U are valid
-        const uint32_t im = (0xFFFFFFFFu >> a.gap_at) & ~(0xFFFFFFFFu >> (a.gap_at + a.gap_len));
-        if (((xg | (xg >> 1)) & gm) == 0 && (inv & im) == 0) return false;
-    }
-    ++ncand;
-    bool exact = false;
-    if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) return false;
-    sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), t.seq);
-    return true;
-}
-
 // kGap: the references of a gapped seed scan (split tables): the key is the gapped one, and a
 // window whose gap matches the record exactly is left to the contiguous seed's scan.
-// (The same rules as tail_open / tail_test, which the fused pair check uses; written out here
-// in one body: through the helpers c4's tail pass took 0.062 ms against 0.054.)
 // One reference per thread.  (Round 4 measured two and four per thread with their head loads
 // in flight together: c4's ~16M key references took 0.33-0.37 ms either way, bound by the
 // references' own traffic, and c3's / c5's tails took 17 us longer in that form.)
@@ -2436,21 +2272,10 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
 // (256 per launch instead of 1,024 with 4-wave blocks; c4 pair 0.743 -> 0.714 ms).
 constexpr int kPairWaves = 16;
 constexpr int kPairBlock = kPairWaves * 64;
-// Bucket-tail references folded into the pair check (a.fuse_tails; one-table runs): a batch
-// of 64 references, one per lane, is opened and its records tested one step j (the j-th record
-// of every lane's bucket) at a time, as tail_kernel does; a step's survivors are compacted into
-// the wave's LDS queue and pair-checked kFuseQ at a time.  No survivor-list round trip and no
-// kernel boundary between the two stages: tail_kernel was a latency chain of its own (12-21 us
-// per run on 1/8 of c3) that pair_kernel waited out.  One pair-check call site per wave loop
-// keeps the kernel within its 128 VGPRs (two inlined copies spilled to scratch).
-constexpr uint32_t kFuseQ = 63;  // the LDS left beside the stages: 1008 B per wave
-template <bool kFuse>
 __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
-    const uint64_t n_refs = kFuse ? umin64(a.counters[a.tail_ctr], a.tails_cap) : 0ull;
     __shared__ HitStage s_st[kPairWaves];
     __shared__ uint64_t s_pst[kPairWaves][kPSlots * MP_PBATCH];
-    __shared__ uint4 s_fq[kPairWaves][kFuse ? kFuseQ : 1];
     const int lane = threadIdx.x & 63;
     HitStage& S = s_st[threadIdx.x >> 6];
     if (lane == 0) S.n = 0;
@@ -2470,93 +2295,21 @@ __global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
         const uint64_t per_wave = (n_surv + waves - 1) / waves;
         const uint32_t db = (uint32_t)umax64(MP_PAIR_MINB, umin64(per_wave < 128 ? 32 : MP_PDYN_BATCH, per_wave));
         const uint64_t nbat = (n_surv + db - 1) / db;
-        const uint64_t nref = (n_refs + 63) / 64;  // reference batches (fused tails)
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
-        // the group's survivor batches [lo_b, hi_b), then its reference batches [lo_r, hi_r):
-        // one local index space li in [0, (hi_b - lo_b) + (hi_r - lo_r))
-        const uint64_t lo_b = nbat * x / g, hi_b = nbat * (x + 1) / g;
-        const uint64_t lo_r = nref * x / g, hi_r = nref * (x + 1) / g;
-        const uint64_t ns = hi_b - lo_b, nl = ns + (hi_r - lo_r);
+        // the group's survivor batches [lo_b, lo_b + ns)
+        const uint64_t lo_b = nbat * x / g, ns = nbat * (x + 1) / g - lo_b;
         const uint64_t nw_x = (uint64_t)((gridDim.x - x + g - 1u) / g) * kPairWaves;  // waves of this group
         uint64_t li = (uint64_t)(blockIdx.x / g) * kPairWaves + (threadIdx.x >> 6);
         uint64_t* pst = s_pst[threadIdx.x >> 6];
-        if constexpr (!kFuse) {  // the survivor list alone: check a batch, then claim the next
-            while (li < ns) {
-                const uint64_t i = (lo_b + li) * db + (uint64_t)lane;
-                uint4 v = kEmptySurv;
-                if ((uint32_t)lane < db && i < n_surv) v = a.surv[i];
-                pair_check_lanes(a, v, db, lane, S, pst);
-                unsigned long long c = 0;
-                if (lane == 0) c = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
-                li = nw_x + (uint64_t)__shfl((long long)c, 0, 64);
-            }
-        } else {
-        uint4* Q = s_fq[threadIdx.x >> 6];
-        uint32_t qn = 0, ncand = 0, nsurv = 0;  // queue fill (wave-uniform), statistics
-        // the open reference batch: each lane's reference and the next record step j
-        TailRef t;
-        t.cnt = 0;
-        uint32_t j = 0;
-        bool open = false;  // wave-uniform
-        for (;;) {
+        while (li < ns) {  // check a batch, then claim the next
+            const uint64_t i = (lo_b + li) * db + (uint64_t)lane;
             uint4 v = kEmptySurv;
-            uint32_t batch = 0;  // survivors to check this pass (wave-uniform)
-            if (open) {  // one record step of the open references
-                bool ok = false;
-                uint4 sv = kEmptySurv;
-                if (j < t.cnt) {
-                    const Entry e = j ? a.ents[t.first + j] : t.e0;
-                    ok = tail_test<false>(a, t, e, ncand, sv);
-                }
-                ++j;
-                open = __any(j < t.cnt);
-                const uint64_t bm = __ballot(ok);
-                const uint32_t k = (uint32_t)__popcll(bm);
-                nsurv += ok ? 1u : 0u;
-                if (k > kFuseQ) {  // (nearly) every lane survived: check them in place
-                    v = sv;
-                    batch = 64;
-                } else if (k) {
-                    if (qn + k > kFuseQ) {  // the queue is full: check it, then refill
-                        if ((uint32_t)lane < qn) v = Q[lane];
-                        batch = qn;
-                        qn = 0;
-                        wave_sync();
-                    }
-                    if (ok) Q[qn + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull))] = sv;
-                    qn += k;
-                    wave_sync();
-                }
-            } else if (li < nl) {
-                if (li < ns) {
-                    const uint64_t i = (lo_b + li) * db + (uint64_t)lane;
-                    if ((uint32_t)lane < db && i < n_surv) v = a.surv[i];
-                    batch = db;
-                } else {
-                    const uint64_t i = (lo_r + li - ns) * 64u + (uint64_t)lane;
-                    uint4 rv = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), rw = make_uint4(0u, 0u, 0u, 0u);
-                    if (i < n_refs) {
-                        rv = a.tails[2 * i];
-                        rw = a.tails[2 * i + 1];
-                    }
-                    tail_open<false>(a, rv, rw, t);
-                    j = 0;
-                    open = __any(t.cnt != 0u);
-                }
-                unsigned long long c = 0;
-                if (lane == 0) c = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
-                li = nw_x + (uint64_t)__shfl((long long)c, 0, 64);
-            } else if (qn) {  // the queue's last survivors
-                if ((uint32_t)lane < qn) v = Q[lane];
-                batch = qn;
-                qn = 0;
-            } else {
-                break;
-            }
-            if (batch) pair_check_lanes(a, v, batch, lane, S, pst);
-        }
-        add_stats(a, ncand, nsurv, lane);
+            if ((uint32_t)lane < db && i < n_surv) v = a.surv[i];
+            pair_check_lanes(a, v, db, lane, S, pst);
+            unsigned long long c = 0;
+            if (lane == 0) c = atomicAdd(&a.counters[kPairQBase + x * kStatStride], 1ull);
+            li = nw_x + (uint64_t)__shfl((long long)c, 0, 64);
         }
     }
     // the block's stages leave with one returning atomic: one per wave at the end of the
@@ -2729,7 +2482,7 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
             s->n_cu <= 0)
             s->n_cu = 256;
         int occ = 0;  // persistent pair check: every resident block slot once
-        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel<false>, kPairBlock, 0) == hipSuccess && occ > 0)
+        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel, kPairBlock, 0) == hipSuccess && occ > 0)
                              ? (uint32_t)occ : 1u;
         s->dense_lds = dense_lds_of(t);
         if (t->split_rest) s->dense_lds = std::max(s->dense_lds, dense_lds_of(t->split_rest));
@@ -2938,22 +2691,17 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     }
     const bool timed = s->scan_timing || s->stage_timing;  // stage times start from the scan's end event
     if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
-    // one-table runs open their bucket-tail references inside pair_kernel (fused_ref_batch);
-    // the wide key groups' references keep tail_kernel (which reads their 8-B IUPAC heads)
-    bool fuse = s->opt.fuse_tails != 0 && !scan_uses_kgrp4(s, t, a);
     if (!use_split(s)) {
         bool tail = false;
         const int rc = launch_scan(s, t, a, tiles, st, &tail);
         if (rc) return rc;
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
-        if (tail && !fuse) {
+        if (tail) {
             if (t->kgrp4) hipLaunchKernelGGL((tail_kernel<false, true>), dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, a);
             else hipLaunchKernelGGL((tail_kernel<false, false>), dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }
-        fuse = fuse && tail;
     } else {
-        fuse = false;
         const Table* sub[3] = {t->split_a, t->split_b, t->split_rest};
         ScanArgs pa[3];
         bool tail[3] = {false, false, false};
@@ -2980,10 +2728,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     MID_EVENT(hipEventRecord(s->ev1, st));
     const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
                                                            : s->pair_per_cu;
-    ScanArgs pa = a;
-    pa.fuse_tails = fuse ? 1u : 0u;
-    if (fuse) hipLaunchKernelGGL(pair_kernel<true>, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, pa);
-    else hipLaunchKernelGGL(pair_kernel<false>, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, pa);
+    hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, a);
     MP_HIP_CHECK(hipGetLastError());
     MID_EVENT(hipEventRecord(s->ev2, st));
     if (mode < 2) {  // hit order on the device count: no host round trip before it; its offsets
@@ -3236,11 +2981,16 @@ MP_EXPORT int mp_search_complete(void* search, uint64_t* n_hits) {
     Search* s = (Search*)search;
     if (!s) return fail(MP_E_ARG, "mp_search_complete: null search");
     if (!s->pending) return fail(MP_E_STATE, "mp_search_complete: no run enqueued (mp_search_enqueue)");
-    MP_HIP_CHECK(hipSetDevice(s->genome->device));
+    // the run is no longer pending whatever happens below (a failed call must not leave the
+    // handle and its genome locked in MP_E_STATE); a failure marks the counters dirty
     if (n_hits) *n_hits = 0;
     s->pending = false;
     if (s->genome->n_pending) --s->genome->n_pending;
     if (s->pend_empty) return MP_OK;
+    if (hipSetDevice(s->genome->device) != hipSuccess) {
+        s->dirty = true;
+        MP_HIP_CHECK(hipSetDevice(s->genome->device));
+    }
     const int rc = search_complete(s, n_hits);
     if (rc) s->dirty = true;
     return rc;

@@ -872,4 +872,13 @@ MP_EXPORT int mp_table_split(void* table, uint32_t* seed_tables, uint32_t* rest_
     return MP_OK;
 }
 
+MP_EXPORT int mp_table_layout(void* table, uint32_t* flags) {
+    Table* t = (Table*)table;
+    if (!t || !flags) return fail(MP_E_ARG, "mp_table_layout: null pointer");
+    *flags = (t->lds_exact ? MP_LAYOUT_LDS_EXACT : 0u) | (t->rk ? MP_LAYOUT_RANK : 0u) | (t->kgrp ? MP_LAYOUT_KGRP : 0u) |
+             (t->kgrp4 ? MP_LAYOUT_KGRP4 : 0u) | (t->dgrp ? MP_LAYOUT_DENSE : 0u) | (t->split_a ? MP_LAYOUT_SPLIT : 0u) |
+             (t->filt ? MP_LAYOUT_HASHED : 0u);
+    return MP_OK;
+}
+
 MP_EXPORT void mp_table_destroy(void* table) { free_table((Table*)table); }

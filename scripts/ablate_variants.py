@@ -19,6 +19,11 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       with mp_debug_pair_counts (a function only this variant exports)
   54  pair_kernel without the primer-1 compare (every fingerprint survivor kept)
   55  pair_kernel's lane-parallel tries computed but never staged (no hits written)
+  70  end-of-scan stealing across XCD groups (round 4, DESIGN 4.1: +20 us on 1/8 c3): a wave whose
+      group is claimed out re-points its scheduler at the next group that still has more than
+      one super-step per wave left and claims single super-steps there
+  71  the key-group field filter of kgrp_pass in branch-free form (round 4, DESIGN 4.2: every
+      form computed and selected; 1/8 c3 scan 0.342 -> 0.348 ms)
   60  scan_kernel's genome-plane loads non-temporal (the stream kept out of L2's working set:
       the c4 level-2 tables, rank words + 16-B heads, are ~4.1 MB against a 4 MB L2)
 """
@@ -27,7 +32,7 @@ import shutil
 
 _L1 = "            const uint32_t c = (uint32_t)__popc(rem);\n"
 _L2 = "                constexpr int kP = (kSeedQR + 63) / 64;\n"
-_L3 = "                if constexpr (kRkf == 1) {\n                    // the few seeds that pass the key groups"
+_L3 = "                if constexpr (kRkf != 0) {\n                    // the few seeds that pass the key groups"
 _LOOP = ("    while (ss < n_supers) {\n        const SeqSpan sp = pf;\n        const uint64_t sbase = pf_sbase;\n"
          "        const uint32_t n = pf_n;\n        SuperRegs R;")
 _STAGE = "    {\n        constexpr int kStage = (int)(kLdsFilterWords / 4 / kBlock);  // eight uint4 per thread (128 KiB)\n"
@@ -36,11 +41,11 @@ _PROBE = "            const uint32_t rem = lds_probe32<kK, kGap>(s_lf, d0, d1, d
 _LP = "    if (__any(lp)) {\n"
 _TODO = "    uint64_t todo = __ballot(keep && !lp);\n"
 
-_P1 = "    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true);\n"
+_P1 = "    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1_ch, true, pr->p1q);\n"
 _LPHIT = "            stage_try_hit(a, S, lane, hit, sgk, srk, t - slo);\n"
 _T_ENTRY = "    zero_sort_counts(a);\n    // stage the seed prefilter in LDS (once per persistent workgroup)"
 _T_STAGED = "    const int lane = threadIdx.x & 63;\n    const int w = threadIdx.x >> 6;\n    const uint64_t stride = (uint64_t)gridDim.x * kWaves;"
-_T_END = "    close_chunked(a.surv, a.surv_cap, lane, C);\n    close_chunked<2>(a.tails, a.tails_cap, lane, TC);"
+_T_END = "    close_chunked(a.surv, a.surv_cap, lane, C);\n    close_chunked<2, kRkf == 2 ? kRefChunk"
 _T_TAIL = "MP_EXPORT int mp_search_set_stage_timing(void* search, int32_t on) {"
 _WORDS = ("        w0 = a.g2[j >> 5];\n        w1 = a.g2[(j >> 5) + 1];\n        const uint64_t v0 = a.ginv[j >> 6];\n"
           "        const uint64_t v1 = a.ginv[(j >> 6) + 1];\n        const uint32_t sh = (uint32_t)(j & 32);  // branch-free")
@@ -49,6 +54,52 @@ _WORDS_NT = ("        w0 = __builtin_nontemporal_load(&a.g2[j >> 5]);\n        w
              "        const uint64_t v1 = __builtin_nontemporal_load(&a.ginv[(j >> 6) + 1]);\n"
              "        const uint32_t sh = (uint32_t)(j & 32);  // branch-free")
 _T_GLOBAL = ("}  // namespace mp\n\nusing namespace mp;\n\nMP_EXPORT int mp_search_set_stage_timing")
+
+_STEAL = """    __device__ __forceinline__ bool steal(uint64_t n_supers) {  // ablation 70
+        if (gridDim.x < 8u) return false;
+        const uint32_t kW = blockDim.x >> 6;
+        const uint32_t home = blockIdx.x & 7u;
+        uint32_t x = lo;
+        for (uint32_t t = 1; t < 8u; ++t) {
+            const uint32_t nx = (x + 1u) & 7u;
+            if (nx == home) return false;
+            ctr += ((int)nx - (int)x) * (int)(2 * kStatStride);
+            x = nx;
+            const uint32_t h = (uint32_t)((n_supers * (x + 1)) >> 3);
+            const uint32_t s0 = min((uint32_t)((n_supers * x) >> 3) + ((gridDim.x - x + 7u) >> 3) * kW * chunk, h);
+            uint32_t cur = 0;
+            if ((threadIdx.x & 63) == 0) cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur);
+            const uint32_t own = ((gridDim.x - x + 7u) >> 3) * kW;
+            if (s0 + cur + own < h) {
+                lo = x;
+                hi = h;
+                S = s0;
+                hint = h;
+                young = 0;
+                return true;
+            }
+        }
+        return false;
+    }
+"""
+
+_KGRP_BF = """    if (!kGap && !a.kgrp_wild) {  // ablation 71: every field form computed and selected
+        const uint32_t present = (rw.x >> bit) & 1u;
+        const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
+        const uint64_t w64 = ((uint64_t)rw.y << 32) | rw.x;
+        const uint32_t field = (uint32_t)(w64 >> (16u + 16u * min(j, kKgrpFields - 1u))) & 0xFFFFu;
+        const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
+        const uint32_t s_ok = (uint32_t)__popc((x | (x >> 1)) & 0x55555555u) <= (uint32_t)a.N;
+        const uint32_t g3 = (pk >> (4u + 2u * (a.kgrp_F - 3u))) & 63u;
+        const uint32_t x0 = g3 ^ ((field >> 6) & 63u), x1 = g3 ^ (field & 63u);
+        const uint32_t p_ok = ((uint32_t)__popc((x0 | (x0 >> 1)) & 0x15u) <= (uint32_t)a.N) |
+                              ((uint32_t)__popc((x1 | (x1 >> 1)) & 0x15u) <= (uint32_t)a.N);
+        const uint32_t flag = (field >> 15) & 1u, pair = (field >> 14) & 1u;
+        const uint32_t ok = (uint32_t)(j >= kKgrpFields) | (flag & s_ok) | ((flag ^ 1u) & ((pair ^ 1u) | p_ok));
+        return (present & ok) != 0u;
+    }
+"""
 
 VARIANTS = {
     1: [(_L1, "            if constexpr (kMode == 1) {  // ablation 1\n"
@@ -71,7 +122,7 @@ VARIANTS = {
          (_T_END, "    const uint64_t wt2 = wall_clock64();  // ablation 40\n"),
          ("        const uint64_t nx = sch.next(ss, n_supers, lane);\n        (void)stride;\n        if constexpr (kMode == 1) {",
           "        ++n_ss;  // ablation 40\n"),
-         ("    SuperSched sch;\n    uint64_t ss = sch.first(a.counters, n_supers, w, kWaves, lane, a.sched_short);",
+         ("    SuperSched sch;\n    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kWaves, lane, a.sched_short);",
           "    uint32_t n_ss = 0;  // ablation 40\n"),
          ("    // candidate statistics\n    add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);\n}\n",
           "    if ((threadIdx.x & 63) == 0 && blockIdx.x * kWaves + (threadIdx.x >> 6) < 8192)  // ablation 40\n"
@@ -94,6 +145,12 @@ VARIANTS = {
                    "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_counts), 8 * 8) == hipSuccess ? 0 : -1;\n}\n\n")],
     54: [(_P1, "    if (true) {} else  // ablation 54\n")],
     60: [(_WORDS, _WORDS_NT, "replace")],
+    70: [("        end = min(st + chunk, hi);\n        hint = st;\n        claim(lane);\n", "        lo = x;  // ablation 70\n"),
+         ("        if (st >= hi) {\n            end = 0;\n            return n_supers;\n",
+          "        while (st >= hi) {  // ablation 70\n            if (!steal(n_supers)) break;\n            claim(lane);\n"
+          "            st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);\n        }\n"),
+         ("};\n\n// kRkf: 0 the rank queue", _STEAL)],
+    71: [("    if (!((rw.x >> bit) & 1u)) return false;  // the key is absent\n    if constexpr (kGap) {", _KGRP_BF)],
     55: [(_LPHIT, "            if (hit && t < -1000000) // ablation 55\n")],
 }
 

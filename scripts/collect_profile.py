@@ -63,7 +63,10 @@ if per_step > 1 and iso:
     iso_step = per_step * sum(iso) / len(iso)
 else:
     iso_step = sum(iso) / len(iso) if iso else None
-out = {"kernel": "mp::" + kern, "avg_duration_ns_trace": trace_ns, "counters_mean_per_dispatch": pmc,
+# the build these passes ran: the source digest the trace pass's bench line printed (bench.py
+# takes a committed profile only for the same build)
+build = json.loads(bench[-1]).get("build") if bench else None
+out = {"kernel": "mp::" + kern, "build": build, "avg_duration_ns_trace": trace_ns, "counters_mean_per_dispatch": pmc,
        "avg_duration_ns_trace_isolated": iso_step, "isolated_dispatches": len(iso), "dispatches": len(allk)}
 if per_step > 1:
     out["per_step"] = (f"{per_step} launches per search step (split seed scans): counters are the mean per "

@@ -41,7 +41,7 @@ prm = O.params(wordsize=cfg["W"], mismatches=cfg["N"], margin=cfg["M"], iupac_mo
 ref = C.search(otable, seqs, prm, 16)
 R = set(map(tuple, np.stack([ref["seq"], ref["pos1"], ref["pos2"], ref["rec"]], 1).tolist()))
 print("oracle", len(ref), flush=True)
-for label, opts in [("default", {}), ("fuse", dict(fuse_tails=True)), ("tailkernel", dict(tails="kernel")),
+for label, opts in [("default", {}), ("tailkernel", dict(tails="kernel")),
                     ("inline", dict(tails="inline"))]:
     s = _native.Search(table, genome)
     if opts:

@@ -28,7 +28,7 @@ def test_library_exports_all_symbols():
     lib = _native.lib()
     for name in _declared():
         assert hasattr(lib, name), name
-    assert lib.mp_abi_version() == 1
+    assert lib.mp_abi_version() == 2
 
 
 def test_device_count_and_loud_failure_without_gpu():

@@ -1,0 +1,55 @@
+"""bench.py --gpus N: the N-rank job it launches for itself, and the rank-count checks
+(the -T fan-out it stands in for: reference engine.py:386-422).  CPU only: no rank starts."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_launcher_command_shape():
+    cmd = bench.launcher_command(["--gpus", "8", "--steps", "20", "--warmup", "3"], 8, 29512)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=8" in cmd and "--master-port=29512" in cmd
+    i = cmd.index("--master-addr")
+    assert cmd[i + 1] == "127.0.0.1"
+    # the child re-runs this very script with the caller's arguments unchanged
+    j = cmd.index(os.path.abspath(bench.__file__))
+    assert cmd[j + 1:] == ["--gpus", "8", "--steps", "20", "--warmup", "3"]
+
+
+def test_resolve_world_without_launcher():
+    assert bench.resolve_world(None, {}) == (1, False)
+    assert bench.resolve_world(1, {}) == (1, False)
+    assert bench.resolve_world(2, {}) == (2, True)
+    assert bench.resolve_world(8, {}) == (8, True)
+    with pytest.raises(SystemExit):
+        bench.resolve_world(0, {})
+
+
+def test_resolve_world_under_launcher():
+    # the driver's form: torch.distributed.run ... bench.py --gpus N
+    assert bench.resolve_world(4, {"WORLD_SIZE": "4"}) == (4, False)
+    assert bench.resolve_world(None, {"WORLD_SIZE": "2"}) == (2, False)
+    with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
+        bench.resolve_world(8, {"WORLD_SIZE": "2"})
+
+
+def test_free_port_is_bindable():
+    import socket
+    p = bench.free_port()
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", p))
+
+
+def test_mismatch_exits_before_any_gpu_work():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr

@@ -152,10 +152,14 @@ def test_search_from_device_records_matches_host_records(tmp_path, monkeypatch):
         monkeypatch.setattr(F, "DEVICE_MIN_BYTES", dev_min)
         eng = MerPCR(wordsize=11, mismatches=1)
         assert _load_sts(eng, sts_text, str(tmp_path))
-        recs = eng.load_fasta_file(p)
+        recs = eng.load_fasta_file(p, on_device=True)
         kinds = {type(r).__name__ for r in recs}
         hits = eng.find_hits(recs)
         res.append((kinds, eng.format_hits(recs, hits), [r.sequence for r in recs]))
     assert res[0][0] == {"DeviceRecord"} and res[1][0] == {"ReaderRecord"}
     assert res[0][1] == res[1][1] and len(res[0][1]) > 50
     assert res[0][2] == res[1][2]
+    # the default (API callers that may never search): host records, no device allocation
+    monkeypatch.setattr(F, "DEVICE_MIN_BYTES", 0)
+    eng = MerPCR(wordsize=11, mismatches=1)
+    assert {type(r).__name__ for r in eng.load_fasta_file(p)} == {"ReaderRecord"}

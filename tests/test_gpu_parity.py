@@ -533,8 +533,7 @@ def _multi_case(W, n_sts, seed):
 
 @pytest.mark.parametrize("W,n_sts,opts", [(8, 3000, {}), (10, 3000, {}), (11, 6000, {}),
                                           (11, 6000, dict(tails="inline")), (11, 6000, dict(defer=False)),
-                                          # bucket tails opened inside the pair check (fuse_tails)
-                                          (11, 6000, dict(fuse_tails=True)), (12, 6000, dict(fuse_tails=True))])
+                                          (12, 6000, {})])
 def test_sharded_ranges_all_paths(W, n_sts, opts):
     """Owned (seq, k) ranges partition the hit list exactly through every scan path:
     dense_kernel (W=8), the exact-LDS scan (W=10), the ranked drain with full-head deferral
@@ -769,3 +768,44 @@ def test_wide_key_groups_vs_rank_heads(W, N, iupac, monkeypatch):
             assert _load_sts(eng, sts.text(), td)
         hits = eng.find_hits([FASTARecord(defline=">chrK", sequence=seq)])
         assert len(hits) == len(ref) and hits.tobytes() == ref.tobytes(), no4
+        # the two runs took different level-2 structures (else the A/B compares a path with itself)
+        lay = eng.device_table().layout()
+        assert ("kgrp4" in lay) == (no4 == "0"), (no4, lay)
+
+
+def test_primer_edit_in_place_vs_oracle():
+    """A primer edited in place after load: the reference still finds the record through the
+    bucket of its load-time key (engine.py:265-279, 483-486) and compares the primer it holds
+    now (engine.py:507-597).  Two edits: one after the seed (the edited primer is found), one
+    inside the seed (the genome carries the new primer, whose first W-mer is not the key, so
+    neither engine may report it)."""
+    rng = random.Random(7)
+    W = 11
+
+    def rnd(n):
+        return "".join(rng.choice("ACGT") for _ in range(n))
+
+    a1, a2, b1, b2 = rnd(22), rnd(21), rnd(20), rnd(23)
+    a1_new = a1[:15] + ("A" if a1[15] != "A" else "C") + a1[16:]      # edit past the seed
+    b1_new = ("G" if b1[0] != "G" else "T") + b1[1:]                   # edit inside the seed
+    sts_text = f"A\t{a1}\t{a2}\t200\talias A\nB\t{b1}\t{b2}\t180\n"
+    fill_a = rnd(200 - len(a1) - len(a2))
+    fill_b = rnd(180 - len(b1) - len(b2))
+    genome = rnd(5000) + a1_new + fill_a + a2 + rnd(3000) + b1_new + fill_b + b2 + rnd(4000)
+    params = dict(wordsize=W, mismatches=0, margin=50)
+    eng = MerPCR(**params)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    recs = [FASTARecord(defline=">g1 test", sequence=genome)]
+    assert _device_lines(eng, recs) == []                # neither primer as loaded is in the genome
+    plus = [r for r in eng.sts_records if r.direct == "+"]
+    plus[0].primer1 = a1_new
+    plus[1].primer1 = b1_new
+    got = _device_lines(eng, recs)
+    table = O.load_sts_lines(sts_text.splitlines(True), W, 240)
+    orec = [r for r in table.records if r.direct == "+"]
+    orec[0].primer1 = a1_new                            # same edit, key left as loaded
+    orec[1].primer1 = b1_new
+    exp = O.search_lines([("g1", genome)], table, O.params(**params))
+    assert got == exp
+    assert len(exp) == 1 and exp[0].split("\t")[2] == "A", exp

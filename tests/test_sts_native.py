@@ -65,13 +65,13 @@ def _state(eng):
     table = {k: [id(r) for r in v] for k, v in eng.sts_table.items()}
     index = {id(r): i for i, r in enumerate(eng.sts_records)}
     table = {k: [index[x] for x in v] for k, v in table.items()}
-    return recs, table, eng.max_pcr_size, list(eng._sts_keys)
+    return recs, table, eng.max_pcr_size, eng._record_keys(eng.sts_records).tolist()
 
 
 def _load(eng, path, native, caplog):
     caplog.clear()
     start = time.time()
-    eng.sts_records, eng.sts_table, eng._sts_keys, eng.max_pcr_size = [], {}, [], 0
+    eng.sts_records, eng.sts_table, eng.max_pcr_size = [], {}, 0
     with caplog.at_level(logging.INFO, logger="merpcr"):
         if native:
             ok = eng._load_sts_native(path, start)
@@ -202,3 +202,25 @@ def test_format_follows_records_edited_in_place():
     r1.id = "REPLACED"
     eng.sts_records[0] = r1
     assert "REPLACED" in eng.format_bytes(fr, h).decode()
+
+
+def test_primer_edit_in_place_keeps_load_time_key(tmp_path):
+    """The reference finds a record only through the sts_table bucket it was filed under at
+    load time (engine.py:265-279, 483-486), whatever its primer holds after an edit; the
+    record's own hash_offset is read at search time.  The device table keeps that key."""
+    p = tmp_path / "a.sts"
+    p.write_text("A\tACGTACGTACGTAAA\tTTTGGGCCCAAATTT\t200\talias\nB\tGGGACCCATTTAGCA\tACGTTGCAACGTT\t150-250\n")
+    eng = MerPCR(wordsize=8)
+    assert eng.load_sts_file(str(p))
+    before = eng._table_arrays()[0].tolist()
+    r0 = eng.sts_records[0]
+    r0.primer1 = "CCCCCCCCAAAAAAA"          # edited in place: a different first W-mer
+    after = eng._table_arrays()
+    assert after[0].tolist() == before
+    assert after[1].tolist()[0] == r0.hash_offset
+    # a record the caller adds to sts_records alone is keyed as the loader would key it
+    from merpcr_amd.core.models import STSRecord
+    extra = STSRecord(id="C", primer1="TTTTAAAACCCCG", primer2="ACGTACGTAC", pcr_size=100, alias="",
+                      offset=3, hash_offset=0, direct="+")
+    eng.sts_records.append(extra)
+    assert eng._table_arrays()[0].tolist() == before + [eng._hash_value("TTTTAAAACCCCG")[1]]
