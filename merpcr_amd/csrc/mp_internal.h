@@ -140,6 +140,7 @@ struct Table {
     int filt_direct = 1;
     uint32_t filt_log2 = 0;   // log2(filter bits)
     int lds_exact = 0;        // LDS prefilter is the exact 4^W bitmap (W <= 10)
+    uint32_t layout = 0;      // MP_LAYOUT_* bits of the structures built (empty arrays are 1-element stubs)
     int lds_k = 1;            // bits per key in the blocked LDS filter (W 11..13)
     int defer_full = 0;       // < 5% full heads: the ranked drain defers them to tail_kernel
     uint32_t* lfilt = nullptr;  // kLdsFilterWords words

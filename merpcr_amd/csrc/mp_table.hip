@@ -591,8 +591,11 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                 // present key of its group) always passes.  Taken when fewer than a quarter of
                 // a random window's seeds would pass (c4: ~0.12 with the keys without a field
                 // counted, against ~0.30 for the 8-B fields)
+                // MP_NO_KGRP4 (A/B runs and tests): 1 = never, -1 = whenever the table can
+                // carry them (the pass-rate estimate skipped)
                 const char* no4 = std::getenv("MP_NO_KGRP4");
-                if (!t->kgrp_wild && t->h12 && t->defer_full && !(no4 && std::atoi(no4))) {
+                const int no4v = no4 ? std::atoi(no4) : 0;
+                if (!t->kgrp_wild && t->h12 && t->defer_full && no4v <= 0) {
                     const uint32_t F4 = kKgrp4F;
                     const uint64_t seedm = sp_lt((int)W);
                     double pass4 = 0.0;
@@ -631,7 +634,7 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                         }
                         kgrp4[g] = make_uint4(pres, fields[0], fields[1], fields[2]);
                     }
-                    if (!(n4 && pass4 / (double)n4 < 0.25)) kgrp4.clear();
+                    if (!(n4 && (no4v < 0 || pass4 / (double)n4 < 0.25))) kgrp4.clear();
                 }
             } else if (W >= 11 && W <= 13) {
                 const uint32_t F = std::min<uint32_t>(7u, 17u - W);
@@ -695,6 +698,9 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         while ((1ull << t->rank_bits) < (uint64_t)n_rec) ++t->rank_bits;
 
         uint64_t bytes = 0;
+        t->layout = (t->lds_exact ? MP_LAYOUT_LDS_EXACT : 0u) | (rk.empty() ? 0u : MP_LAYOUT_RANK) |
+                    (kgrp.empty() ? 0u : MP_LAYOUT_KGRP) | (kgrp4.empty() ? 0u : MP_LAYOUT_KGRP4) |
+                    (dgrp.empty() ? 0u : MP_LAYOUT_DENSE) | (slots.empty() ? 0u : MP_LAYOUT_HASHED);
         if ((rc = upload(&t->filt, filt.data(), filt.size(), &bytes))) break;
         if ((rc = upload(&t->lfilt, lfilt.data(), lfilt.size(), &bytes))) break;
         if ((rc = upload(&t->slots, slots.data(), slots.size(), &bytes))) break;
@@ -875,9 +881,7 @@ MP_EXPORT int mp_table_split(void* table, uint32_t* seed_tables, uint32_t* rest_
 MP_EXPORT int mp_table_layout(void* table, uint32_t* flags) {
     Table* t = (Table*)table;
     if (!t || !flags) return fail(MP_E_ARG, "mp_table_layout: null pointer");
-    *flags = (t->lds_exact ? MP_LAYOUT_LDS_EXACT : 0u) | (t->rk ? MP_LAYOUT_RANK : 0u) | (t->kgrp ? MP_LAYOUT_KGRP : 0u) |
-             (t->kgrp4 ? MP_LAYOUT_KGRP4 : 0u) | (t->dgrp ? MP_LAYOUT_DENSE : 0u) | (t->split_a ? MP_LAYOUT_SPLIT : 0u) |
-             (t->filt ? MP_LAYOUT_HASHED : 0u);
+    *flags = t->layout | (t->split_a ? MP_LAYOUT_SPLIT : 0u);
     return MP_OK;
 }
 

@@ -17,3 +17,8 @@ tail -2 gpurun_out/${TAG}_smoke.log
 timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 \
     || { echo "bench failed rc=$?"; tail -20 gpurun_out/${TAG}_bench.log; exit 1; }
 tail -1 gpurun_out/${TAG}_bench.log
+# the N-rank path with no outside launcher: bench.py --gpus 2 starts torch.distributed.run itself
+timeout -k 10 400 python -u bench.py --gpus 2 --rehearse-one-gpu --steps 5 --warmup 2 \
+    > gpurun_out/${TAG}_rehearse2.log 2>&1 \
+    || { echo "rehearse2 failed rc=$?"; tail -20 gpurun_out/${TAG}_rehearse2.log; exit 1; }
+grep '^{' gpurun_out/${TAG}_rehearse2.log | tail -1
