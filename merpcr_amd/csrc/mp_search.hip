@@ -113,6 +113,11 @@ struct ScanArgs {
 // The gapped key of a 16-base funnel x (base 0 on top), left-aligned like a contiguous key:
 // the top gap_at bases, then the bases after the gap (the low bits below the key are junk,
 // as in the contiguous form).  One shift and one bit-field insert.
+// kGap = kGapW8 (c5's split): the W = 8 gapped seed's shape as compile-time constants, so that
+// its level 1 needs no key assembly for the filter word and the second filter bit (below),
+// and the scan holds three fewer scalars (its SGPRs spill into VGPR lanes)
+constexpr int kGapW8 = 8;
+constexpr uint32_t kGapW8At = 8, kGapW8Len = 3, kGapW8Post = 3;
 __device__ __forceinline__ uint32_t gap_key(uint32_t x, uint32_t gap_at, uint32_t gap_len) {
     const uint32_t hm = ~(0xFFFFFFFFu >> (2u * gap_at));
     return (x & hm) | ((x << (2u * gap_len)) & ~hm);
@@ -1335,7 +1340,8 @@ __device__ __forceinline__ uint32_t probe32(const ScanArgs& a, const uint32_t* _
 
 // Level 1 only, kMode 1: the blocked LDS filter bits of the lane's 32 windows (bit 31-T):
 // all kK bits of lds_block_mask set in the key's word.
-template <int kK, bool kGap = false>
+// kGap: 0 contiguous, 1 gapped (shape in gap_at / gap_len), kGapW8 the W = 8 gapped shape.
+template <int kK, int kGap = 0>
 __device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds, uint32_t d0, uint32_t d1, uint32_t d2,
                                                 uint32_t shw, uint32_t gap_at = 0u, uint32_t gap_len = 0u) {
     uint32_t lmask = 0;
@@ -1343,7 +1349,22 @@ __device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds
         ((
             [&] {
                 uint32_t x = kmer_top<T>(d0, d1, d2);
-                if constexpr (kGap) x = gap_key(x, gap_at, gap_len);
+                if constexpr (kGap == kGapW8) {
+                    // the gapped key g = x's top 16 bits (bases 0..7) ++ x's bases 11..13: the word
+                    // index (g's top 15 bits) is x's, and the second bit (g's bits 14..10, below
+                    // the top 16) is x's bits 8..4; only the first bit needs g (bit 16 ++ 15..12)
+                    constexpr uint32_t kShw = 32 - 2 * kSplitSeed;  // the W' = 11 key's low bits
+                    static_assert(kLdsFilterLog2 - 5 <= 2 * (int)kGapW8At && kShw + 5 <= 2 * kGapW8At,
+                                  "word index inside the ungapped bases, second bit below them");
+                    const uint32_t wv = lds[x >> (37 - kLdsFilterLog2)];
+                    const uint32_t b1 = (((x & 0xFFFF0000u) | ((x << (2 * kGapW8Len)) & 0xFFFFu)) >> (32 - kLdsFilterLog2)) & 31u;
+                    uint32_t on = __builtin_amdgcn_ubfe(wv, b1, 1u);
+                    if constexpr (kK >= 2) on &= __builtin_amdgcn_ubfe(wv, (x >> (kShw - 2 * kGapW8Len)) & 31u, 1u);
+                    static_assert(kK <= 2, "the W = 8 gapped form takes one or two bits per key");
+                    lmask |= on << (31 - T);
+                    return;
+                }
+                if constexpr (kGap != 0) x = gap_key(x, gap_at, gap_len);
                 const uint32_t wv = lds[x >> (37 - kLdsFilterLog2)];
                 uint32_t on = __builtin_amdgcn_ubfe(wv, (x >> (32 - kLdsFilterLog2)) & 31u, 1u);
                 if constexpr (kK >= 2) on &= __builtin_amdgcn_ubfe(wv, (x >> shw) & 31u, 1u);
@@ -1396,11 +1417,15 @@ __device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, 
 // bases after the seed's span (the low 2 gap_post bits); a window passes when its gap differs
 // in 1..N positions, or has an invalid base (bit 31 of pk) -- with neither, the contiguous seed
 // of the split finds the window -- and gap and post bases together differ in at most N.
-template <bool kGap = false>
+// kGap = kGapW8: the W = 8 shape and N = 1 as constants.
+template <int kGap = 0>
 __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
     const uint32_t bit = pk & 15u;
     if (!((rw.x >> bit) & 1u)) return false;  // the key is absent
-    if constexpr (kGap) {
+    if constexpr (kGap != 0) {
+        constexpr bool kC = kGap == kGapW8;
+        const uint32_t glen = kC ? kGapW8Len : a.gap_len, gpost = kC ? kGapW8Post : a.gap_post;
+        const uint32_t F = kC ? kGapW8Len + kGapW8Post : a.kgrp_F, N = kC ? 1u : (uint32_t)a.N;
         const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
         if (j >= kKgrpFields) return true;
         const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
@@ -1409,15 +1434,15 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
             // two records (gap_len <= 3): either record's gap differs in 1..N positions, or the
             // window's gap holds an invalid base
             if (pk >> 31) return true;
-            const uint32_t gm = (1u << (2u * a.gap_len)) - 1u;
-            const uint32_t g = (pk >> (4u + 2u * a.gap_post)) & gm;
+            const uint32_t gm = (1u << (2u * glen)) - 1u;
+            const uint32_t g = (pk >> (4u + 2u * gpost)) & gm;
             const uint32_t x0 = g ^ ((field >> 6) & gm), x1 = g ^ (field & gm);
             const uint32_t m0 = (uint32_t)__popc((x0 | (x0 >> 1)) & 0x555u), m1 = (uint32_t)__popc((x1 | (x1 >> 1)) & 0x555u);
-            return (m0 >= 1u && m0 <= (uint32_t)a.N) || (m1 >= 1u && m1 <= (uint32_t)a.N);
+            return (m0 >= 1u && m0 <= N) || (m1 >= 1u && m1 <= N);
         }
-        const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
+        const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * F)) - 1u);
         const uint32_t m = (x | (x >> 1)) & 0x55555555u;
-        return (uint32_t)__popc(m) <= (uint32_t)a.N && ((m >> (2u * a.gap_post)) != 0u || (pk >> 31) != 0u);
+        return (uint32_t)__popc(m) <= N && ((m >> (2u * gpost)) != 0u || (pk >> 31) != 0u);
     }
     if (a.kgrp_wild) {
         if (pk >> 31) return true;
@@ -1560,9 +1585,13 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
 // groups (kgrp4, uint4 per 32 keys: presence and three ten-base fields).  1 and 2 leave the seeds
 // that pass as key references for tail_kernel.
 template <int kMode, bool kInline, int kK = 1, bool kDefer = false, int kH16 = 0, int kRkf = 0,
-          bool kGap = false>
+          int kGap = 0>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
-    static_assert(!kGap || (kMode == 1 && kRkf), "gapped seeds take the key-group path");
+    static_assert(kGap == 0 || (kMode == 1 && kRkf), "gapped seeds take the key-group path");
+    // the gapped seed's shape: compile-time for kGapW8 (c5), else the table's
+    constexpr bool kGC = kGap == kGapW8;
+    const uint32_t g_at = kGC ? kGapW8At : a.gap_at, g_len = kGC ? kGapW8Len : a.gap_len;
+    const uint32_t g_post = kGC ? kGapW8Post : a.gap_post;
     __shared__ uint32_t s_lf[kLdsFilterWords];
     __shared__ WaveLds s_wl[kWaves];
 
@@ -1641,8 +1670,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         const uint32_t pb = R.base + (uint32_t)lane * kLanePos;
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
         // a gapped seed's windows: both of its pieces clean
-        const uint32_t okm = (kGap ? window_ok_mask(R.iv, a.gap_at) &
-                                         window_ok_mask(R.iv << (a.gap_at + a.gap_len), W - a.gap_at)
+        const uint32_t okm = (kGap ? window_ok_mask(R.iv, g_at) &
+                                         window_ok_mask(R.iv << (g_at + g_len), (kGC ? kSplitSeed : W) - g_at)
                                    : window_ok_mask(R.iv, W)) &
                              span_bits(sp, pb);
         const uint64_t nx = sch.next(ss, n_supers, lane);
@@ -1652,10 +1681,10 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // {key, offset} (the queue's arrays), then every lane probes one list entry per
             // pass -- full lanes, all passes' rank-word loads in flight together -- and the
             // seeds are compacted back into the same arrays as {offset, rank}
-            const uint32_t rem = lds_probe32<kK, kGap>(s_lf, d0, d1, d2, shw, a.gap_at, a.gap_len) & okm;
+            const uint32_t rem = lds_probe32<kK, kGap>(s_lf, d0, d1, d2, shw, g_at, g_len) & okm;
             // I = 1 key groups: windows whose first W + F bases are not all A/C/G/T/U; gapped
             // seeds: windows with an invalid base in the gap
-            const uint32_t fbad = kGap ? ~window_ok_mask(R.iv << a.gap_at, a.gap_len)
+            const uint32_t fbad = kGap ? ~window_ok_mask(R.iv << g_at, g_len)
                                        : (kRkf == 2 ? ~window_ok_mask(R.iv, W + kKgrp4F)
                                                     : ((kRkf && a.kgrp_wild) ? ~window_ok_mask(R.iv, W + a.kgrp_F) : 0u));
             const uint32_t c = (uint32_t)__popc(rem);
@@ -1704,7 +1733,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                             const uint32_t B = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d1);
                             const uint32_t C = (uint32_t)__builtin_amdgcn_ds_bpermute(sa, (int)d2);
                             const uint32_t i = po[q] & 31u;
-                            const uint32_t key = (kGap ? gap_key(funnel3(A, B, C, i), a.gap_at, a.gap_len)
+                            const uint32_t key = (kGap ? gap_key(funnel3(A, B, C, i), g_at, g_len)
                                                        : funnel3(A, B, C, i)) >> shw;
                             // the field's bases: after the key, or a gapped seed's gap and the
                             // bases after its span (2 gap_len bases after the gap's start)
@@ -1717,10 +1746,10 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                                 fb = (r ? __builtin_amdgcn_alignbit(hi, lo, 32u - r) : hi) >> (32u - 2u * kKgrp4F);
                                 pk[q] = (fb << 5) | (key & (kKgrp4Keys - 1u)) | ((qe >> 15) << 31);
                                 rw[q] = a.kgrp4[v ? (key >> kKgrp4Log2) : 0u];
-                            } else if constexpr (kGap) {
-                                const uint32_t f = funnel3(A, B, C, i + a.gap_at);
-                                fb = ((f >> (32u - 2u * a.gap_len)) << (2u * a.gap_post)) |
-                                     (a.gap_post ? (f << (4u * a.gap_len)) >> (32u - 2u * a.gap_post) : 0u);
+                            } else if constexpr (kGap != 0) {
+                                const uint32_t f = funnel3(A, B, C, i + g_at);
+                                fb = ((f >> (32u - 2u * g_len)) << (2u * g_post)) |
+                                     (g_post ? (f << (4u * g_len)) >> (32u - 2u * g_post) : 0u);
                             } else {
                                 fb = funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F);
                             }
@@ -2599,8 +2628,13 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
     if (t->gap_len) {  // gapped seed: the key-group path, every passing seed deferred to tail_kernel
         if (!(t->filt_direct && !t->lds_exact && t->kgrp_F >= 2 && a.W >= 11 && a.W <= 13 && a.defer_full))
             return fail(MP_E_STATE, "gapped seed table without key groups");
-        if (t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+        // c5's shape (W = 8, N = 1) with its gap as constants; other W 7..9 shapes from the table
+        const bool w8 = t->gap_at == kGapW8At && t->gap_len == kGapW8Len && t->gap_post == kGapW8Post && a.N == 1 &&
+                        t->kgrp_F == kGapW8Len + kGapW8Post && a.W == (int)kSplitSeed && !std::getenv("MP_GAP_GENERIC");
+        if (w8 && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true, kGapW8>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (w8) hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true, kGapW8>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
         MP_HIP_CHECK(hipGetLastError());
         *tail = true;
         return MP_OK;
