@@ -1417,8 +1417,10 @@ __device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, 
 // bases after the seed's span (the low 2 gap_post bits); a window passes when its gap differs
 // in 1..N positions, or has an invalid base (bit 31 of pk) -- with neither, the contiguous seed
 // of the split finds the window -- and gap and post bases together differ in at most N.
-// kGap = kGapW8: the W = 8 shape and N = 1 as constants.
-template <int kGap = 0>
+// kGap = kGapW8: the W = 8 shape and N = 1 as constants.  kFix (I = 0 tables of W = 11, the
+// c2 / c3 / split-contiguous shape): F = kFixF, no I = 1 fields, N = kFix - 1.
+constexpr uint32_t kFixW = 11, kFixF = 6;
+template <int kGap = 0, int kFix = 0>
 __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t pk) {
     const uint32_t bit = pk & 15u;
     if (!((rw.x >> bit) & 1u)) return false;  // the key is absent
@@ -1444,7 +1446,7 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         const uint32_t m = (x | (x >> 1)) & 0x55555555u;
         return (uint32_t)__popc(m) <= N && ((m >> (2u * gpost)) != 0u || (pk >> 31) != 0u);
     }
-    if (a.kgrp_wild) {
+    if (!kFix && a.kgrp_wild) {
         if (pk >> 31) return true;
         const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
         if (j >= kKgrpWildFields) return true;
@@ -1453,18 +1455,19 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
         const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
         return (uint32_t)__popc((x | (x >> 1)) & 0x555u & ~(field >> 12)) <= (uint32_t)a.N;
     }
+    const uint32_t F = kFix ? kFixF : a.kgrp_F, N = kFix ? (uint32_t)(kFix - 1) : (uint32_t)a.N;
     const uint32_t j = (uint32_t)__popc(__builtin_amdgcn_ubfe(rw.x, 0u, bit));
     if (j >= kKgrpFields) return true;
     const uint32_t field = j == 0u ? (rw.x >> 16) : (j == 1u ? (rw.y & 0xFFFFu) : (rw.y >> 16));
     if (!(field & kKgrpFlag)) {
         if (!(field & kKgrpPair)) return true;
         // two records: the window's bases W..W+2 (the top 3 of its F) against each record's
-        const uint32_t g3 = (pk >> (4u + 2u * (a.kgrp_F - 3u))) & 63u;
+        const uint32_t g3 = (pk >> (4u + 2u * (F - 3u))) & 63u;
         const uint32_t x0 = g3 ^ ((field >> 6) & 63u), x1 = g3 ^ (field & 63u);
-        return __popc((x0 | (x0 >> 1)) & 0x15u) <= a.N || __popc((x1 | (x1 >> 1)) & 0x15u) <= a.N;
+        return (uint32_t)__popc((x0 | (x0 >> 1)) & 0x15u) <= N || (uint32_t)__popc((x1 | (x1 >> 1)) & 0x15u) <= N;
     }
-    const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * a.kgrp_F)) - 1u);
-    return __popc((x | (x >> 1)) & 0x55555555u) <= a.N;
+    const uint32_t x = ((pk >> 4) ^ field) & ((1u << (2u * F)) - 1u);
+    return (uint32_t)__popc((x | (x >> 1)) & 0x55555555u) <= N;
 }
 
 // Level-2 probe of the wide I = 1 key groups (kgrp4, see kKgrp4Keys).  `pk`: the window's
@@ -1585,9 +1588,10 @@ struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives besid
 // groups (kgrp4, uint4 per 32 keys: presence and three ten-base fields).  1 and 2 leave the seeds
 // that pass as key references for tail_kernel.
 template <int kMode, bool kInline, int kK = 1, bool kDefer = false, int kH16 = 0, int kRkf = 0,
-          int kGap = 0>
+          int kGap = 0, int kFix = 0>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     static_assert(kGap == 0 || (kMode == 1 && kRkf), "gapped seeds take the key-group path");
+    static_assert(kFix == 0 || (kMode == 1 && kRkf == 1 && kGap == 0), "kFix: the I = 0 key-group scan");
     // the gapped seed's shape: compile-time for kGapW8 (c5), else the table's
     constexpr bool kGC = kGap == kGapW8;
     const uint32_t g_at = kGC ? kGapW8At : a.gap_at, g_len = kGC ? kGapW8Len : a.gap_len;
@@ -1614,7 +1618,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     const int w = threadIdx.x >> 6;
     const uint64_t stride = (uint64_t)gridDim.x * kWaves;
     const uint64_t n_supers = a.spans[a.n_spans].super0;
-    const uint32_t W = (uint32_t)a.W;
+    const uint32_t W = kFix ? kFixW : (uint32_t)a.W;
     const uint32_t shw = 32u - 2u * W;
     WaveLds& L = s_wl[w];
     uint32_t ncand = 0;
@@ -1686,7 +1690,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             // seeds: windows with an invalid base in the gap
             const uint32_t fbad = kGap ? ~window_ok_mask(R.iv << g_at, g_len)
                                        : (kRkf == 2 ? ~window_ok_mask(R.iv, W + kKgrp4F)
-                                                    : ((kRkf && a.kgrp_wild) ? ~window_ok_mask(R.iv, W + a.kgrp_F) : 0u));
+                                                    : ((kRkf && !kFix && a.kgrp_wild) ? ~window_ok_mask(R.iv, W + a.kgrp_F) : 0u));
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
@@ -1751,7 +1755,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                                 fb = ((f >> (32u - 2u * g_len)) << (2u * g_post)) |
                                      (g_post ? (f << (4u * g_len)) >> (32u - 2u * g_post) : 0u);
                             } else {
-                                fb = funnel3(A, B, C, i + W) >> (32u - 2u * a.kgrp_F);
+                                fb = funnel3(A, B, C, i + W) >> (32u - 2u * (kFix ? kFixF : a.kgrp_F));
                             }
                             if constexpr (kRkf != 2) {
                                 pk[q] = (fb << 4) | (key & 15u) | ((qe >> 15) << 31);
@@ -1783,7 +1787,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                             const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
                             bool hit;
                             if constexpr (kRkf == 2) hit = kgrp_pass4(a, rw[q], pk[q]) && e < nr;
-                            else hit = e < nr && kgrp_pass<kGap>(a, rw[q], pk[q]);
+                            else hit = e < nr && kgrp_pass<kGap, kFix>(a, rw[q], pk[q]);
                             const uint64_t hm = __ballot(hit);
                             if (hit) L.rq.q[qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint16_t)po[q];
                             qn += (uint32_t)__popcll(hm);
@@ -2622,6 +2626,11 @@ static bool scan_uses_kgrp4(const Search* s, const Table* t, const ScanArgs& a) 
 
 // The scan kernel of table t (dense_kernel, or scan_kernel in the form the table and the
 // handle's options select).  *tail: the run needs tail_kernel over this scan's references.
+static void launch_fixed(int fix, uint32_t grid, hipStream_t st, const ScanArgs& a) {
+    if (fix == 1) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 1, 0, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 1, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+}
+
 static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t tiles, hipStream_t st, bool* tail) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU);
     *tail = false;
@@ -2651,6 +2660,9 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
                      !s->opt.no_rank_filter && t->filt_direct && !t->lds_exact && a.W >= 11 && a.W <= 13;
     // I = 1 tables whose 8-B fields are too short (c4): the wide key groups
     const bool rkf4 = scan_uses_kgrp4(s, t, a);
+    // the I = 0 key-group scan with its shape as constants (kFix: W = 11, F = 6, N <= 1)
+    const int fix = (a.W == (int)kFixW && a.I == 0 && !t->kgrp_wild && t->kgrp_F == kFixF && a.N <= 1 &&
+                     !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
     if (dense) {
         const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
                                                             (uint64_t)s->n_cu * (uint64_t)s->dense_per_cu);
@@ -2673,6 +2685,8 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (rkf4 && t->lds_k == 1)
             hipLaunchKernelGGL((scan_kernel<1, false, 1, true, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (t->filt_direct && t->lds_k == 2 && a.defer_full && rkf && fix)  // c2 / c3: W = 11, I = 0, N <= 1
+            launch_fixed(fix, grid, st, a);
         else if (t->filt_direct && t->lds_k == 2 && a.defer_full && rkf)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->filt_direct && t->lds_k == 3 && a.defer_full && rkf)  // MP_LDS_K=3 (A/B)
