@@ -1474,6 +1474,8 @@ __device__ __forceinline__ bool kgrp_pass(const ScanArgs& a, uint2 rw, uint32_t 
 // bases W..W+F-1 << 5 | the key's low 5 bits, bit 31 set when the window's first W + F bases
 // are not all A/C/G/T/U (it then passes on presence alone).  True = the seed goes on (as a
 // key reference).
+// kFix: N = kFix - 1 as a constant.
+template <int kFix = 0>
 __device__ __forceinline__ bool kgrp_pass4(const ScanArgs& a, uint4 rw, uint32_t pk) {
     static_assert(kKgrp4F == 10 && kKgrp4Fields == 3, "field layout: three 32-bit fields");
     const uint32_t bit = pk & 31u;
@@ -1488,7 +1490,7 @@ __device__ __forceinline__ bool kgrp_pass4(const ScanArgs& a, uint4 rw, uint32_t
     pl = (pl | (pl << 4)) & 0x0F0F0F0Fu;
     pl = (pl | (pl << 2)) & 0x33333333u;
     pl = (pl | (pl << 1)) & 0x55555555u;
-    return __popc((x | (x >> 1)) & pl) <= a.N;
+    return (uint32_t)__popc((x | (x >> 1)) & pl) <= (kFix ? (uint32_t)(kFix - 1) : (uint32_t)a.N);
 }
 
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
@@ -1591,7 +1593,8 @@ template <int kMode, bool kInline, int kK = 1, bool kDefer = false, int kH16 = 0
           int kGap = 0, int kFix = 0>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     static_assert(kGap == 0 || (kMode == 1 && kRkf), "gapped seeds take the key-group path");
-    static_assert(kFix == 0 || (kMode == 1 && kRkf == 1 && kGap == 0), "kFix: the I = 0 key-group scan");
+    // kFix: W = 11 and N = kFix - 1 as constants; for kRkf 1 (I = 0 key groups) also F = 6
+    static_assert(kFix == 0 || (kMode == 1 && kRkf != 0 && kGap == 0), "kFix: the key-group scans");
     // the gapped seed's shape: compile-time for kGapW8 (c5), else the table's
     constexpr bool kGC = kGap == kGapW8;
     const uint32_t g_at = kGC ? kGapW8At : a.gap_at, g_len = kGC ? kGapW8Len : a.gap_len;
@@ -1786,7 +1789,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         if ((uint32_t)q * 64u < nr) {
                             const uint32_t e = (uint32_t)q * 64u + (uint32_t)lane;
                             bool hit;
-                            if constexpr (kRkf == 2) hit = kgrp_pass4(a, rw[q], pk[q]) && e < nr;
+                            if constexpr (kRkf == 2) hit = kgrp_pass4<kFix>(a, rw[q], pk[q]) && e < nr;
                             else hit = e < nr && kgrp_pass<kGap, kFix>(a, rw[q], pk[q]);
                             const uint64_t hm = __ballot(hit);
                             if (hit) L.rq.q[qn + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint16_t)po[q];
@@ -2305,7 +2308,15 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
 // (256 per launch instead of 1,024 with 4-wave blocks; c4 pair 0.743 -> 0.714 ms).
 constexpr int kPairWaves = 16;
 constexpr int kPairBlock = kPairWaves * 64;
-__global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a) {
+// kI, kN, kX >= 0: the compare rule's I, N and X as constants (the common configurations;
+// -1: the run's).  The generic form spilled 103 SGPRs into VGPR lanes: its exec-mask saves
+// for every rule branch and the rule's scalars did not fit.
+template <int kI = -1, int kN = -1, int kX = -1>
+__global__ __launch_bounds__(kPairBlock, 1) void pair_kernel(ScanArgs a_) {
+    ScanArgs a = a_;
+    if constexpr (kI >= 0) a.I = kI;
+    if constexpr (kN >= 0) a.N = kN;
+    if constexpr (kX >= 0) a.X = kX;
     const uint64_t n_surv = umin64(a.counters[2], a.surv_cap);  // written by the scan / tail kernels
     __shared__ HitStage s_st[kPairWaves];
     __shared__ uint64_t s_pst[kPairWaves][kPSlots * MP_PBATCH];
@@ -2515,7 +2526,7 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
             s->n_cu <= 0)
             s->n_cu = 256;
         int occ = 0;  // persistent pair check: every resident block slot once
-        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel, kPairBlock, 0) == hipSuccess && occ > 0)
+        s->pair_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pair_kernel<>, kPairBlock, 0) == hipSuccess && occ > 0)
                              ? (uint32_t)occ : 1u;
         s->dense_lds = dense_lds_of(t);
         if (t->split_rest) s->dense_lds = std::max(s->dense_lds, dense_lds_of(t->split_rest));
@@ -2631,6 +2642,12 @@ static void launch_fixed(int fix, uint32_t grid, hipStream_t st, const ScanArgs&
     else hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 1, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a);
 }
 
+static void launch_fixed4(int fix, uint32_t grid, hipStream_t st, const ScanArgs& a) {
+    if (fix == 1) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2, 0, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+    else if (fix == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2, 0, 3>), dim3(grid), dim3(kBlock), 0, st, a);
+}
+
 static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t tiles, hipStream_t st, bool* tail) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU);
     *tail = false;
@@ -2663,6 +2680,7 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
     // the I = 0 key-group scan with its shape as constants (kFix: W = 11, F = 6, N <= 1)
     const int fix = (a.W == (int)kFixW && a.I == 0 && !t->kgrp_wild && t->kgrp_F == kFixF && a.N <= 1 &&
                      !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
+    const int fix4 = (a.W == (int)kFixW && a.N <= 2 && !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
     if (dense) {
         const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
                                                             (uint64_t)s->n_cu * (uint64_t)s->dense_per_cu);
@@ -2681,6 +2699,8 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
         else hipLaunchKernelGGL((scan_kernel<2, true>), dim3(grid), dim3(kBlock), 0, st, a);
     } else {
         if (t->lds_exact) hipLaunchKernelGGL((scan_kernel<0, false>), dim3(grid), dim3(kBlock), 0, st, a);
+        else if (rkf4 && t->lds_k == 2 && fix4)  // c4: W = 11, N <= 2 as constants
+            launch_fixed4(fix4, grid, st, a);
         else if (rkf4 && t->lds_k == 2)
             hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (rkf4 && t->lds_k == 1)
@@ -2776,7 +2796,12 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     MID_EVENT(hipEventRecord(s->ev1, st));
     const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
                                                            : s->pair_per_cu;
-    hipLaunchKernelGGL(pair_kernel, dim3((uint32_t)s->n_cu * pair_per_cu), dim3(kPairBlock), 0, st, a);
+    const dim3 pg((uint32_t)s->n_cu * pair_per_cu);
+    const bool pgen = std::getenv("MP_PAIR_GENERIC") != nullptr;
+    if (!pgen && a.I == 0 && a.N == 0 && a.X == 1) hipLaunchKernelGGL((pair_kernel<0, 0, 1>), pg, dim3(kPairBlock), 0, st, a);
+    else if (!pgen && a.I == 0 && a.N == 1 && a.X == 1) hipLaunchKernelGGL((pair_kernel<0, 1, 1>), pg, dim3(kPairBlock), 0, st, a);
+    else if (!pgen && a.I == 1 && a.N == 2 && a.X == 1) hipLaunchKernelGGL((pair_kernel<1, 2, 1>), pg, dim3(kPairBlock), 0, st, a);
+    else hipLaunchKernelGGL(pair_kernel<>, pg, dim3(kPairBlock), 0, st, a);
     MP_HIP_CHECK(hipGetLastError());
     MID_EVENT(hipEventRecord(s->ev2, st));
     if (mode < 2) {  // hit order on the device count: no host round trip before it; its offsets
