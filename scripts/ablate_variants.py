@@ -13,6 +13,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
   31  no LDS staging and no loop
   40  per-wave wall-clock stamps (entry, LDS staged, loop end, exit) of scan_kernel, read back
       with mp_debug_wave_times (a function only this variant exports)
+  42  variant 40 plus the end time of each of a wave's first 32 key-group super-steps
+      (mp_debug_ss_times: 8192 waves x 32 stamps; 0 = not reached)
   50  pair_kernel without the lane-parallel try loop
   51  pair_kernel without any try (prologue, primer-1 compare and staging only)
   52  pair_kernel counting its per-survivor (non-lane-parallel) survivors by reason, read back
@@ -36,7 +38,7 @@ _L3 = "                if constexpr (kRkf != 0) {\n                    // the fe
 _LOOP = ("    while (ss < n_supers) {\n        const SeqSpan sp = pf;\n        const uint64_t sbase = pf_sbase;\n"
          "        const uint32_t n = pf_n;\n        SuperRegs R;")
 _STAGE = "    {\n        constexpr int kStage = (int)(kLdsFilterWords / 4 / kBlock);  // eight uint4 per thread (128 KiB)\n"
-_PROBE = "            const uint32_t rem = lds_probe32<kK, kGap>(s_lf, d0, d1, d2, shw, a.gap_at, a.gap_len) & okm;\n"
+_PROBE = "            const uint32_t rem = lds_probe32<kK, kGap>(s_lf, d0, d1, d2, shw, g_at, g_len) & okm;\n"
 
 _LP = "    if (__any(lp)) {\n"
 _TODO = "    uint64_t todo = __ballot(keep && !lp);\n"
@@ -130,6 +132,7 @@ VARIANTS = {
          ("struct SuperSched {", "__device__ ulonglong4 g_wave_times[8192];  // ablation 40\n"),
          (_T_TAIL, "MP_EXPORT int mp_debug_wave_times(ulonglong4* out, uint32_t n) {  // ablation 40\n"
                    "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_times), n * sizeof(ulonglong4)) == hipSuccess ? 0 : -1;\n}\n\n")],
+    42: None,  # variant 40 plus per-super-step stamps (below)
     50: [(_LP, "    if (false)  // ablation 50\n")],
     51: [(_LP, "    if (false)  // ablation 51\n"), (_TODO, "    keep = false;  // ablation 51\n")],
     52: [(_TODO, "    if (keep && !lp) {  // ablation 52\n"
@@ -150,9 +153,19 @@ VARIANTS = {
           "        while (st >= hi) {  // ablation 70\n            if (!steal(n_supers)) break;\n            claim(lane);\n"
           "            st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);\n        }\n"),
          ("};\n\n// kRkf: 0 the rank queue", _STEAL)],
-    71: [("    if (!((rw.x >> bit) & 1u)) return false;  // the key is absent\n    if constexpr (kGap) {", _KGRP_BF)],
+    71: [("    if (!((rw.x >> bit) & 1u)) return false;  // the key is absent\n    if constexpr (kGap != 0) {", _KGRP_BF)],
     55: [(_LPHIT, "            if (hit && t < -1000000) // ablation 55\n")],
 }
+
+
+VARIANTS[42] = VARIANTS[40] + [
+    ("            (void)first;\n            ss = nx;\n            continue;",
+     "            if ((threadIdx.x & 63) == 0 && n_ss <= 32 && blockIdx.x * kWaves + (threadIdx.x >> 6) < 8192)  // ablation 42\n"
+     "                g_ss_times[(blockIdx.x * kWaves + (threadIdx.x >> 6)) * 32 + n_ss - 1] = wall_clock64();\n"),
+    ("struct SuperSched {", "__device__ unsigned long long g_ss_times[8192 * 32];  // ablation 42\n"),
+    (_T_TAIL, "MP_EXPORT int mp_debug_ss_times(unsigned long long* out) {  // ablation 42\n"
+              "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ss_times), 8192 * 32 * 8) == hipSuccess ? 0 : -1;\n}\n\n"),
+]
 
 
 def make_source_dir(variant: int, csrc: str, root: str) -> str:

@@ -22,10 +22,11 @@ ap.add_argument("--no-build", action="store_true", help="use the variant library
 args = ap.parse_args()
 from merpcr_amd import _build  # noqa: E402
 import ablate_variants  # noqa: E402
-path = os.path.join(_build.LIBDIR, "libmerpcr_hip_ablate40.so")
+VAR = int(os.environ.get("MP_WAVE_VARIANT", "40"))
+path = os.path.join(_build.LIBDIR, f"libmerpcr_hip_ablate{VAR}.so")
 if not (args.no_build and os.path.exists(path)):
-    src = ablate_variants.make_source_dir(40, _build.CSRC, os.path.join(tempfile.gettempdir(), "mp_ablate_40"))
-    _build.build_native(lib=path, src_dir=src, tag="_ablate40")
+    src = ablate_variants.make_source_dir(VAR, _build.CSRC, os.path.join(tempfile.gettempdir(), f"mp_ablate_{VAR}"))
+    _build.build_native(lib=path, src_dir=src, tag=f"_ablate{VAR}")
 if args.build_only:
     sys.exit(0)
 import torch  # noqa: E402
@@ -78,3 +79,16 @@ loop = us[:, 2] - us[:, 1]
 print(f"loop per wave: mean {loop.mean():.1f} min {loop.min():.1f} max {loop.max():.1f} us; waves {len(t)}")
 hist = np.histogram(us[:, 2], bins=12)
 print("loop-end histogram:", [(round(float(e), 1), int(c)) for e, c in zip(hist[1], hist[0])])
+if hasattr(lib, "mp_debug_ss_times"):  # variant 42: each wave's first 32 super-step ends
+    ss = (ctypes.c_uint64 * (8192 * 32))()
+    lib.mp_debug_ss_times.argtypes = [ctypes.c_void_p]
+    assert lib.mp_debug_ss_times(ctypes.cast(ss, ctypes.c_void_p)) == 0
+    a = np.frombuffer(ss, dtype=np.uint64).reshape(8192, 32).astype(np.int64)[ids]
+    st = (np.frombuffer(out, dtype=np.uint64).reshape(8192, 4).astype(np.int64)[ids, 1])[:, None]
+    prev = np.concatenate([st, a[:, :-1]], axis=1)
+    dur = (a - prev) / 100.0
+    ok = a > 0
+    print("super-step k of a wave (us): mean duration by k, waves reaching it")
+    print([(k, round(float(dur[ok[:, k], k].mean()), 2), int(ok[:, k].sum())) for k in range(32) if ok[:, k].any()])
+    fin = (a[:, 0] - t0) / 100.0
+    print(f"first super-step end: min {fin.min():.1f} med {np.median(fin):.1f} max {fin.max():.1f} us")
