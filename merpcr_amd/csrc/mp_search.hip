@@ -2198,13 +2198,80 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
 #define MP_TAIL_BPC 2
 #endif
 constexpr uint32_t kTailBPC = MP_TAIL_BPC;  // blocks per CU
-// kH12: the table has wide key groups (kgrp4), whose key references read the 8-B IUPAC heads
-template <bool kGap = false, bool kH12 = false>
+constexpr uint32_t kRingSeg = 256, kRingSegs = kTailBuf / kRingSeg;
+static_assert(kRingSegs == 8, "ring laps: position / kTailBuf");
+// tail_kernel<kRing>'s survivor push (wave-converged: every lane calls): the wave's
+// survivors get consecutive ring positions from one LDS atomic, wait until their segments
+// are back from the previous lap, are written, and are counted into their segments; a
+// segment that this wave completes is copied to the survivor list by this wave.
+__device__ __forceinline__ void ring_push(const ScanArgs& a, uint4* buf, uint32_t& head, uint32_t* done,
+                                          uint32_t* lap, bool ok, const uint4& sv, int lane) {
+    const uint64_t m = __ballot(ok);
+    if (!m) return;
+    const uint32_t n = (uint32_t)__popcll(m);
+    uint32_t p0 = 0;
+    if (lane == 0) p0 = atomicAdd(&head, n);
+    p0 = (uint32_t)__shfl((int)p0, 0, 64);
+    // the (at most two) segments of [p0, p0 + n): back from the previous lap?
+    const uint32_t pl = p0 + n - 1u;
+    for (;;) {  // wave-uniform
+        const uint32_t l0 = __hip_atomic_load(&lap[(p0 / kRingSeg) % kRingSegs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t l1 = __hip_atomic_load(&lap[(pl / kRingSeg) % kRingSegs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (l0 == p0 / kTailBuf && l1 == pl / kTailBuf) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (ok) buf[(p0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) % kTailBuf] = sv;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    // written counts: the first segment's share, then the rest in the second
+    const uint32_t s0 = p0 / kRingSeg, s1 = pl / kRingSeg;
+    const uint32_t c0 = s0 == s1 ? n : (s1 * kRingSeg - p0);
+    uint32_t full = 0;  // bit 0: segment s0 completed by this wave, bit 1: segment s1
+    if (lane == 0) {
+        if (atomicAdd(&done[s0 % kRingSegs], c0) + c0 == kRingSeg) full |= 1u;
+        if (s1 != s0 && atomicAdd(&done[s1 % kRingSegs], n - c0) + (n - c0) == kRingSeg) full |= 2u;
+    }
+    full = (uint32_t)__shfl((int)full, 0, 64);
+    for (uint32_t q = 0; q < 2; ++q) {
+        if (!((full >> q) & 1u)) continue;  // wave-uniform
+        const uint32_t sg = (q ? s1 : s0) % kRingSegs;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        unsigned long long g = 0;
+        if (lane == 0) g = atomicAdd(&a.counters[2], (unsigned long long)kRingSeg);
+        g = shfl64((uint64_t)g, 0);
+#pragma unroll
+        for (uint32_t t = 0; t < kRingSeg / 64u; ++t) {
+            const uint32_t k = t * 64u + (uint32_t)lane;
+            if (g + k < a.surv_cap) a.surv[g + k] = buf[sg * kRingSeg + k];
+        }
+        // every lane's copy has read its slots before the segment is handed back
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) {
+            done[sg] = 0;
+            __hip_atomic_fetch_add(&lap[sg], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// kH12: the table has wide key groups (kgrp4), whose key references read the 8-B IUPAC heads.
+// kRing: no block barrier in the loop.  Survivors go into an LDS ring of kRingSegs segments
+// of kRingSeg entries: a wave reserves its survivors' slots with one LDS atomic, writes them,
+// and adds them to their segments' written counts; the wave that completes a segment copies
+// it to the survivor list with one global atomic (one per kRingSeg survivors).  A wave whose
+// slots fall in a segment not yet flushed from the ring's previous lap waits for it (its
+// earlier slots are all written, so the wait cannot close a cycle).  The block-synchronous
+// loop (two barriers per 1,024 references) kept every wave of a block at the pace of its
+// slowest chain (ref -> rank word -> head -> entries).
+template <bool kGap = false, bool kH12 = false, bool kRing = false>
 __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     __shared__ uint4 s_buf[kTailBuf];
     __shared__ uint32_t s_n;
     __shared__ unsigned long long s_base;
+    __shared__ uint32_t s_done[kRingSegs], s_lap[kRingSegs];
     if (threadIdx.x == 0) s_n = 0;
+    if (threadIdx.x < kRingSegs) {
+        s_done[threadIdx.x] = 0;
+        s_lap[threadIdx.x] = 0;
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const uint64_t n_refs = umin64(a.counters[a.tail_ctr], a.tails_cap);
@@ -2221,6 +2288,7 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
             v = a.tails[2 * i];
             w = a.tails[2 * i + 1];
         }
+        uint32_t cnt = 0;
         if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
             const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
             const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
@@ -2257,16 +2325,28 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
             } else {
                 e = a.ents[first];                                       // its count = tail length
             }
-            const uint32_t cnt = e.count;
-            for (uint32_t j = 0; j < cnt; ++j) {
+            cnt = e.count;
+            // kRing: every lane runs the wave's largest count, so that the ring pushes below
+            // are wave-converged (a lane waiting on the ring inside a divergent branch could
+            // block the lane that would flush it)
+            uint32_t jn = cnt;
+            if constexpr (kRing) {
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) jn = max(jn, (uint32_t)__shfl_xor((int)jn, o, 64));
+            }
+            for (uint32_t j = 0; j < jn; ++j) {
+              bool ok = false;
+              uint4 sv{};
+              do {
+                if (j >= cnt) break;
                 if (j) e = a.ents[first + j];
                 const uint64_t gk = gp - e.hash_off;
-                if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) continue;  // k + l1 > n / not owned
+                if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) break;  // k + l1 > n / not owned
                 uint64_t G = Gs;
                 uint32_t ex = w.z;
                 if (e.hash_off) {  // seed inside the primer: bounds and window from the genome
                     const uint64_t sbase = a.seq_base[v.w];
-                    if (gp - sbase < e.hash_off) continue;  // k < 0
+                    if (gp - sbase < e.hash_off) break;  // k < 0
                     G = ext2(a.g2, gk);
                     ex = (uint32_t)(ext1(exc, gk) >> 32);
                 }
@@ -2275,13 +2355,18 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                     const uint64_t xg = G ^ e.code;
                     const uint32_t inv = a.has_u ? (uint32_t)(ext1(a.ginv, gk) >> 32) : ex;  // A/C/G/T/U are valid
                     const uint32_t im = (0xFFFFFFFFu >> a.gap_at) & ~(0xFFFFFFFFu >> (a.gap_at + a.gap_len));
-                    if (((xg | (xg >> 1)) & gm) == 0 && (inv & im) == 0) continue;
+                    if (((xg | (xg >> 1)) & gm) == 0 && (inv & im) == 0) break;
                 }
                 ++ncand;
                 bool exact = false;
-                if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) continue;
+                if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) break;
                 ++nsurv;
-                const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
+                ok = true;
+                sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
+              } while (false);
+              if constexpr (kRing) {
+                ring_push(a, s_buf, s_n, s_done, s_lap, ok, sv, lane);
+              } else if (ok) {
                 const uint32_t at = atomicAdd(&s_n, 1u);
                 if (at < kTailBuf) {
                     s_buf[at] = sv;
@@ -2289,13 +2374,31 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                     const unsigned long long g = atomicAdd(&a.counters[2], 1ull);
                     if (g < a.surv_cap) a.surv[g] = sv;
                 }
+              }
             }
         }
-        __syncthreads();
-        if (s_n >= kTailBuf / 2) tail_flush(a, s_buf, s_n, s_base);  // every thread reads s_n between barriers
-        __syncthreads();
+        if constexpr (!kRing) {
+            __syncthreads();
+            if (s_n >= kTailBuf / 2) tail_flush(a, s_buf, s_n, s_base);  // every thread reads s_n between barriers
+            __syncthreads();
+        }
     }
-    tail_flush(a, s_buf, s_n, s_base);
+    if constexpr (kRing) {
+        // every wave's pushes are written; only the segment holding the last position can be
+        // partial (each full one was flushed by the wave that completed it)
+        __syncthreads();
+        const uint32_t head = s_n, part = head % kRingSeg;
+        if (part && threadIdx.x < 64) {
+            const uint32_t seg0 = ((head / kRingSeg) % kRingSegs) * kRingSeg;
+            unsigned long long g = 0;
+            if (lane == 0) g = atomicAdd(&a.counters[2], (unsigned long long)part);
+            g = shfl64((uint64_t)g, 0);
+            for (uint32_t t = (uint32_t)lane; t < part; t += 64u)
+                if (g + t < a.surv_cap) a.surv[g + t] = s_buf[seg0 + t];
+        }
+    } else {
+        tail_flush(a, s_buf, s_n, s_base);
+    }
     add_stats(a, ncand, nsurv, lane);
 }
 
@@ -2751,6 +2854,25 @@ static bool use_split(const Search* s) {
 // A split table scans its seeds one after another (the contiguous seed, the gapped seed, the
 // rest's dense scan), each appending to the one survivor list; the two seed scans keep their
 // bucket-tail references in the two halves of the tail list (counters 4 and 5).
+// The bucket-tail pass: the gapped seed's form, the wide key groups' IUPAC heads, and the
+// barrier-free ring form (MP_TAIL_RING=1, A/B).
+static void launch_tail(const Search* s, bool gap, bool h12, hipStream_t st, const ScanArgs& a) {
+    static const bool ring = [] {
+        const char* e = std::getenv("MP_TAIL_RING");
+        return e && std::atoi(e) != 0;
+    }();
+    const dim3 g((uint32_t)s->n_cu * kTailBPC), b(kTailBlock);
+    if (ring) {
+        if (gap) hipLaunchKernelGGL((tail_kernel<true, false, true>), g, b, 0, st, a);
+        else if (h12) hipLaunchKernelGGL((tail_kernel<false, true, true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((tail_kernel<false, false, true>), g, b, 0, st, a);
+    } else {
+        if (gap) hipLaunchKernelGGL((tail_kernel<true, false>), g, b, 0, st, a);
+        else if (h12) hipLaunchKernelGGL((tail_kernel<false, true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((tail_kernel<false, false>), g, b, 0, st, a);
+    }
+}
+
 static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStream_t st, int mode) {
     Table* t = s->table;
     if (s->dirty) {  // an abandoned run may have left counts behind
@@ -2765,8 +2887,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         if (rc) return rc;
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
         if (tail) {
-            if (t->kgrp4) hipLaunchKernelGGL((tail_kernel<false, true>), dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, a);
-            else hipLaunchKernelGGL((tail_kernel<false, false>), dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, a);
+            launch_tail(s, false, t->kgrp4 != nullptr, st, a);
             MP_HIP_CHECK(hipGetLastError());
         }
     } else {
@@ -2788,8 +2909,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
         for (int i = 0; i < 3; ++i) {
             if (!sub[i] || !tail[i]) continue;
-            if (sub[i]->gap_len) hipLaunchKernelGGL(tail_kernel<true>, dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, pa[i]);
-            else hipLaunchKernelGGL(tail_kernel<false>, dim3((uint32_t)s->n_cu * kTailBPC), dim3(kTailBlock), 0, st, pa[i]);
+            launch_tail(s, sub[i]->gap_len != 0, false, st, pa[i]);
             MP_HIP_CHECK(hipGetLastError());
         }
     }

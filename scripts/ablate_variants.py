@@ -133,21 +133,6 @@ VARIANTS = {
          (_T_TAIL, "MP_EXPORT int mp_debug_wave_times(ulonglong4* out, uint32_t n) {  // ablation 40\n"
                    "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_times), n * sizeof(ulonglong4)) == hipSuccess ? 0 : -1;\n}\n\n")],
     42: None,  # variant 40 plus per-super-step stamps (below)
-    50: [(_LP, "    if (false)  // ablation 50\n")],
-    51: [(_LP, "    if (false)  // ablation 51\n"), (_TODO, "    keep = false;  // ablation 51\n")],
-    52: [(_TODO, "    if (keep && !lp) {  // ablation 52\n"
-                 "        atomicAdd(&g_pair_counts[0], 1ull);\n"
-                 "        atomicAdd(&g_pair_counts[fast ? 2 : 1], 1ull);\n"
-                 "        if (r.l2 > 32u) atomicAdd(&g_pair_counts[3], 1ull);\n"
-                 "        if (lo + hi + 1 > 101) atomicAdd(&g_pair_counts[4], 1ull);\n"
-                 "    }\n"
-                 "    if (keep) atomicAdd(&g_pair_counts[5], 1ull);  // ablation 52\n"
-                 "    if (keep && lp) atomicAdd(&g_pair_counts[6], 1ull);  // ablation 52\n"),
-         ("// Pair-check staging per survivor", "__device__ unsigned long long g_pair_counts[8];  // ablation 52\n"),
-         (_T_TAIL, "MP_EXPORT int mp_debug_pair_counts(unsigned long long* out) {  // ablation 52\n"
-                   "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_counts), 8 * 8) == hipSuccess ? 0 : -1;\n}\n\n")],
-    54: [(_P1, "    if (true) {} else  // ablation 54\n")],
-    60: [(_WORDS, _WORDS_NT, "replace")],
     70: [("        end = min(st + chunk, hi);\n        hint = st;\n        claim(lane);\n", "        lo = x;  // ablation 70\n"),
          ("        if (st >= hi) {\n            end = 0;\n            return n_supers;\n",
           "        while (st >= hi) {  // ablation 70\n            if (!steal(n_supers)) break;\n            claim(lane);\n"
