@@ -504,24 +504,35 @@ __device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint3
 }
 // Exclusive scan of nb bucket counts by one 1024-thread workgroup: off[0..nb] (off[nb] =
 // total) and cursor[0..nb) = off.  The counts pass through LDS (s_v4: kOffTile counts) in
-// tiles: coalesced loads and stores, 8 consecutive counts per thread inside a tile, a wave
-// shuffle scan and one LDS word per wave (s_w: 16).  (64 consecutive counts per thread in
-// registers made every access a 64-line gather: c4's 65,536 buckets took 80 us.)
-constexpr uint32_t kOffTile = 8192;
+// tiles: coalesced loads and stores (all kOffTile / 1024 loads of a thread in flight at once:
+// one memory round trip per tile), kOffPer consecutive counts per thread inside a tile, a
+// wave shuffle scan and one LDS word per wave (s_w: 16).  (64 consecutive counts per thread
+// straight from memory made every access a 64-line gather: c4's 65,536 buckets took 80 us;
+// tiles of 8,192 took 36 us, eight round trips and 24 barriers.)
+constexpr uint32_t kOffTile = 32768;
+constexpr uint32_t kOffPer = kOffTile / 1024;
 __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32_t nb, uint32_t* off,
                                                      uint32_t* cursor, uint4* s_v4, uint32_t* s_w) {
+    static_assert(kOffPer % 4 == 0, "whole uint4 per thread");
     uint32_t* s_v = reinterpret_cast<uint32_t*>(s_v4);
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t carry = 0;
     for (uint32_t base = 0; base < nb; base += kOffTile) {
+        uint32_t ld[kOffPer];
 #pragma unroll
-        for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
+        for (uint32_t j = 0; j < kOffPer; ++j) {
             const uint32_t i = j * 1024 + t;
-            s_v[i] = base + i < nb ? cnt[base + i] : 0u;
+            ld[j] = base + i < nb ? cnt[base + i] : 0u;
         }
+#pragma unroll
+        for (uint32_t j = 0; j < kOffPer; ++j) s_v[j * 1024 + t] = ld[j];
         __syncthreads();
-        uint4 q0 = s_v4[2 * t], q1 = s_v4[2 * t + 1];
-        const uint32_t sum = q0.x + q0.y + q0.z + q0.w + q1.x + q1.y + q1.z + q1.w;
+        uint32_t sum = 0;  // the thread's counts are read twice from LDS: sum, then the scan
+#pragma unroll
+        for (uint32_t j = 0; j < kOffPer / 4; ++j) {
+            const uint4 q = s_v4[(kOffPer / 4) * t + j];
+            sum += q.x + q.y + q.z + q.w;
+        }
         uint32_t x = sum;  // inclusive scan over the wave
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -538,19 +549,18 @@ __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32
             tot += sw;
         }
         uint32_t run = carry + wpre + x - sum, v;
-        v = q0.x; q0.x = run; run += v;
-        v = q0.y; q0.y = run; run += v;
-        v = q0.z; q0.z = run; run += v;
-        v = q0.w; q0.w = run; run += v;
-        v = q1.x; q1.x = run; run += v;
-        v = q1.y; q1.y = run; run += v;
-        v = q1.z; q1.z = run; run += v;
-        q1.w = run;
-        s_v4[2 * t] = q0;
-        s_v4[2 * t + 1] = q1;
+#pragma unroll
+        for (uint32_t j = 0; j < kOffPer / 4; ++j) {
+            uint4 q = s_v4[(kOffPer / 4) * t + j];
+            v = q.x; q.x = run; run += v;
+            v = q.y; q.y = run; run += v;
+            v = q.z; q.z = run; run += v;
+            v = q.w; q.w = run; run += v;
+            s_v4[(kOffPer / 4) * t + j] = q;
+        }
         __syncthreads();
 #pragma unroll
-        for (uint32_t j = 0; j < kOffTile / 1024; ++j) {
+        for (uint32_t j = 0; j < kOffPer; ++j) {
             const uint32_t i = j * 1024 + t;
             if (base + i < nb) {
                 const uint32_t o = s_v[i];
