@@ -171,6 +171,7 @@ struct Table {
     DevRec* recs = nullptr;
     uint32_t* rank = nullptr;      // rec -> position in (hash_off, rec) order
     uint32_t* inv_rank = nullptr;  // position -> rec
+    uint2* rank_rec = nullptr;     // position -> {rec, its size}: the hit decode's one load
     uint64_t* planes = nullptr;    // 4 u64 per 32-base primer chunk
     PairRec* prec = nullptr;       // per record: DevRec, rank, both primers' first plane chunks
     uint64_t planes_words = 0;
@@ -508,11 +509,15 @@ __device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint3
 // one memory round trip per tile), kOffPer consecutive counts per thread inside a tile, a
 // wave shuffle scan and one LDS word per wave (s_w: 16).  (64 consecutive counts per thread
 // straight from memory made every access a 64-line gather: c4's 65,536 buckets took 80 us;
-// tiles of 8,192 took 36 us, eight round trips and 24 barriers.)
-constexpr uint32_t kOffTile = 32768;
+// tiles of 8,192 took 36 us, eight round trips and 24 barriers; 32,768 spilled.)
+constexpr uint32_t kOffTile = 16384;
 constexpr uint32_t kOffPer = kOffTile / 1024;
+// crowded (optional): the buckets of more than crowd_lo and at most crowd_hi counts are
+// listed at crowded[1..] (in no order), their number in *s_crowd (LDS, zeroed by the caller).
 __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32_t nb, uint32_t* off,
-                                                     uint32_t* cursor, uint4* s_v4, uint32_t* s_w) {
+                                                     uint32_t* cursor, uint4* s_v4, uint32_t* s_w,
+                                                     uint32_t* crowded = nullptr, uint32_t* s_crowd = nullptr,
+                                                     uint32_t crowd_lo = 0, uint32_t crowd_hi = 0) {
     static_assert(kOffPer % 4 == 0, "whole uint4 per thread");
     uint32_t* s_v = reinterpret_cast<uint32_t*>(s_v4);
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -526,6 +531,11 @@ __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32
         }
 #pragma unroll
         for (uint32_t j = 0; j < kOffPer; ++j) s_v[j * 1024 + t] = ld[j];
+        if (crowded) {
+#pragma unroll
+            for (uint32_t j = 0; j < kOffPer; ++j)
+                if (ld[j] > crowd_lo && ld[j] <= crowd_hi) crowded[1 + atomicAdd(s_crowd, 1u)] = base + j * 1024 + t;
+        }
         __syncthreads();
         uint32_t sum = 0;  // the thread's counts are read twice from LDS: sum, then the scan
 #pragma unroll

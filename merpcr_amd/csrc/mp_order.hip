@@ -26,6 +26,7 @@ static unsigned bits_for(uint64_t v) {
 // larger than kSortCap (hits piled on a few positions, e.g. a dense repeat) sets
 // h_out[kSortOverflow]; the host then sorts with rocPRIM instead.
 constexpr uint32_t kSortCap = 2048;
+constexpr uint32_t kRankCap = 256;  // buckets over this are "crowded" (bitonic, one workgroup each)
 constexpr unsigned kMaxBucketBits = 16;
 
 // Exclusive scan of the bucket counts by one 1024-thread workgroup (bucket_offsets_block,
@@ -41,9 +42,15 @@ __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restric
                                                        uint32_t* __restrict__ crowded) {
     __shared__ uint4 s_v4[kOffTile / 4];
     __shared__ uint32_t s_w[16];
-    if (threadIdx.x == 0) crowded[0] = 0;  // the previous run's crowded sort is complete (stream order)
+    __shared__ uint32_t s_crowd;
+    if (threadIdx.x == 0) s_crowd = 0;
     if (h_out) finish_fold(counters, n_words, h_out, rcount);
-    bucket_offsets_block(cnt, nb, off, cursor, s_v4, s_w);
+    __syncthreads();
+    // the crowded buckets (kRankCap < keys <= kSortCap) are listed here, so that the mode-1
+    // sort can start them first, beside the others (sort_decode_mode1)
+    bucket_offsets_block(cnt, nb, off, cursor, s_v4, s_w, crowded, &s_crowd, kRankCap, kSortCap);
+    __syncthreads();
+    if (threadIdx.x == 0) crowded[0] = s_crowd;  // the previous run's sort is complete (stream order)
 }
 
 // A bucket the device order cannot hold: flagged in the host word (the device counters are
@@ -108,7 +115,7 @@ __device__ inline SeqRange bucket_seqs(uint32_t b, unsigned shift, unsigned low_
 // sequence is searched within sr (bucket_seqs).
 __device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits, unsigned low_bits,
                                   const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
-                                  SeqRange sr, const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
+                                  SeqRange sr, const uint2* __restrict__ rank_rec,
                                   mp_hit* __restrict__ out) {
     const uint64_t gk = key >> low_bits;
     const uint32_t rank = (uint32_t)((key & ((1ull << low_bits) - 1ull)) >> try_bits);
@@ -120,9 +127,10 @@ __device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits
         else b = mid;
     }
     const uint64_t k = gk - seq_base[a];
-    const uint32_t rec = inv_rank[rank];
+    const uint2 rr = rank_rec[rank];  // {record, size}: one load, not inv_rank then the record
+    const uint32_t rec = rr.x;
     const uint64_t len = seq_len[a];
-    const uint64_t size = recs[rec].size;
+    const uint64_t size = rr.y;
     const uint64_t e = size > len - k ? len - k : size;
     mp_hit h;
     h.pos1 = k;
@@ -142,12 +150,11 @@ __device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits
 // workgroup of this kernel the order stage's critical path.  (One workgroup per bucket left
 // c4's 65,536 workgroups of ~24 keys dispatch-bound: 94 us.)
 constexpr uint32_t kBucketsPerBlock = 4;
-constexpr uint32_t kRankCap = 256;
 __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
                                                           uint32_t nb, unsigned shift, unsigned try_bits, unsigned low_bits,
                                                           const uint64_t* __restrict__ seq_base,
                                                           const uint64_t* __restrict__ seq_len, uint32_t n_seq,
-                                                          const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
+                                                          const uint2* __restrict__ rank_rec,
                                                           mp_hit* __restrict__ out, unsigned long long* __restrict__ h_out,
                                                           uint32_t* __restrict__ crowded) {
     __shared__ uint64_t s_k[kRankCap];
@@ -157,7 +164,6 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
         const bool in = b0 + wave < nb;  // nb < kBucketsPerBlock under a forced sort_bucket_bits
         const uint32_t start = in ? off[b0 + wave] : 0u, m = in ? off[b0 + wave + 1] - start : 0u;
         if (m > kSortCap && lane == 0) flag_overflow(h_out);
-        if (m > kRankCap && m <= kSortCap && lane == 0) crowded[1 + atomicAdd(&crowded[0], 1u)] = b0 + wave;
         if (m > 0 && m <= 64) {  // wave-uniform; no barrier inside
             const uint64_t key = lane < m ? keys[start + lane] : ~0ull;
             uint32_t r = 0;
@@ -166,7 +172,7 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
                 r += kj < key || (kj == key && j < lane);  // ties: stable
             }
             const SeqRange sr = bucket_seqs(b0 + wave, shift, low_bits, seq_base, n_seq, lane);
-            if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
+            if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
         }
         if (!__syncthreads_or(m > 64 && m <= kRankCap)) return;  // every wave reaches this barrier
     }
@@ -180,7 +186,7 @@ __global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __rest
             const uint64_t key = s_k[i];
             uint32_t r = 0;
             for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
-            decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
+            decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
         }
         __syncthreads();  // s_k is refilled by the next bucket
     }
@@ -202,67 +208,129 @@ __device__ __forceinline__ uint64_t cx_lane(uint64_t e, uint32_t i, uint32_t j, 
 // stage with j <= 64 is a register compare or a shuffle, and only the stages with j >= 128
 // (10 of the 66 for 2,048 keys) go through LDS with a barrier each.  (All 66 through LDS,
 // one barrier each: c4's crowded buckets took 109 us.)
+// One crowded bucket b (kRankCap < keys <= kSortCap) sorted and decoded by the whole
+// 1024-thread workgroup (s_k: kSortCap keys of LDS).
+__device__ __forceinline__ void crowded_bucket(uint32_t b, uint64_t* s_k, const uint64_t* __restrict__ keys,
+                                               const uint32_t* __restrict__ off, unsigned shift, unsigned try_bits,
+                                               unsigned low_bits, const uint64_t* __restrict__ seq_base,
+                                               const uint64_t* __restrict__ seq_len, uint32_t n_seq,
+                                               const uint2* __restrict__ rank_rec, mp_hit* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u, base = (threadIdx.x >> 6) * 128u;
+    const uint32_t i0 = base + lane, i1 = i0 + 64u;
+    const uint32_t start = off[b], m = off[b + 1] - start;
+    uint32_t P = 2 * kRankCap;
+    while (P < m) P <<= 1;
+    const bool on = base < P;  // wave-uniform: this wave holds keys of the padded bucket
+    uint64_t e0 = i0 < m ? keys[start + i0] : ~0ull, e1 = i1 < m ? keys[start + i1] : ~0ull;
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        if (k > 128u) {  // stages j >= 128 across waves, through LDS
+            if (on) {
+                s_k[i0] = e0;
+                s_k[i1] = e1;
+            }
+            __syncthreads();
+            for (uint32_t j = k >> 1; j >= 128u; j >>= 1) {
+                for (uint32_t t = threadIdx.x; t < P / 2; t += blockDim.x) {
+                    const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));  // the pair's lower index
+                    const uint32_t ij = i | j;
+                    const uint64_t x = s_k[i], y = s_k[ij];
+                    if ((x > y) == ((i & k) == 0)) {
+                        s_k[i] = y;
+                        s_k[ij] = x;
+                    }
+                }
+                __syncthreads();
+            }
+            if (on) {
+                e0 = s_k[i0];
+                e1 = s_k[i1];
+            }
+            __syncthreads();  // every wave has read before the next k writes
+        }
+        if (on) {
+            if (k >= 128u) {  // j = 64: the lane's own two keys (i0 is the lower index)
+                const bool up = (i0 & k) == 0;
+                const uint64_t lo = e0 < e1 ? e0 : e1, hi = e0 < e1 ? e1 : e0;
+                e0 = up ? lo : hi;
+                e1 = up ? hi : lo;
+            }
+            for (uint32_t j = (k >> 1) < 32u ? (k >> 1) : 32u; j > 0; j >>= 1) {
+                e0 = cx_lane(e0, i0, j, k);
+                e1 = cx_lane(e1, i1, j, k);
+            }
+        }
+    }
+    if (on) {
+        const SeqRange sr = bucket_seqs(b, shift, low_bits, seq_base, n_seq, lane);
+        if (i0 < m) decode_hit(e0, start + i0, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
+        if (i1 < m) decode_hit(e1, start + i1, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
+    }
+}
+
 __global__ __launch_bounds__(1024) void crowded_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
                                                             unsigned shift, unsigned try_bits, unsigned low_bits,
                                                             const uint64_t* __restrict__ seq_base,
                                                             const uint64_t* __restrict__ seq_len, uint32_t n_seq,
-                                                            const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs,
+                                                            const uint2* __restrict__ rank_rec,
                                                             mp_hit* __restrict__ out, const uint32_t* __restrict__ crowded) {
     __shared__ uint64_t s_k[kSortCap];
     static_assert(kSortCap == 2 * 1024, "two keys per thread of the 1024-thread workgroup");
     const uint32_t n = crowded[0];
-    const uint32_t lane = threadIdx.x & 63u, base = (threadIdx.x >> 6) * 128u;
-    const uint32_t i0 = base + lane, i1 = i0 + 64u;
-    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {  // block-uniform
-        const uint32_t b = crowded[1 + c];
-        const uint32_t start = off[b], m = off[b + 1] - start;
-        uint32_t P = 2 * kRankCap;
-        while (P < m) P <<= 1;
-        const bool on = base < P;  // wave-uniform: this wave holds keys of the padded bucket
-        uint64_t e0 = i0 < m ? keys[start + i0] : ~0ull, e1 = i1 < m ? keys[start + i1] : ~0ull;
-        for (uint32_t k = 2; k <= P; k <<= 1) {
-            if (k > 128u) {  // stages j >= 128 across waves, through LDS
-                if (on) {
-                    s_k[i0] = e0;
-                    s_k[i1] = e1;
-                }
-                __syncthreads();
-                for (uint32_t j = k >> 1; j >= 128u; j >>= 1) {
-                    for (uint32_t t = threadIdx.x; t < P / 2; t += blockDim.x) {
-                        const uint32_t i = ((t & ~(j - 1)) << 1) | (t & (j - 1));  // the pair's lower index
-                        const uint32_t ij = i | j;
-                        const uint64_t x = s_k[i], y = s_k[ij];
-                        if ((x > y) == ((i & k) == 0)) {
-                            s_k[i] = y;
-                            s_k[ij] = x;
-                        }
-                    }
-                    __syncthreads();
-                }
-                if (on) {
-                    e0 = s_k[i0];
-                    e1 = s_k[i1];
-                }
-                __syncthreads();  // every wave has read before the next k writes
+    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x)  // block-uniform
+        crowded_bucket(crowded[1 + c], s_k, keys, off, shift, try_bits, low_bits, seq_base, seq_len, n_seq, rank_rec, out);
+}
+
+// Order mode 1 in one launch (round 5): the first n_cblk workgroups sort the crowded buckets
+// that bucket_offsets listed (bitonic, crowded_bucket), and the others take kMode1Buckets
+// buckets each (a wave per bucket of up to 64 keys, the workgroup for 65..kRankCap).  Crowded
+// sorts are the longest, and as the lowest workgroup indices they start first, beside the
+// rest; as two launches (bucket_sort_decode, then crowded_sort_decode) c4 spent 68 + 69 us.
+constexpr uint32_t kMode1Buckets = 16;
+__global__ __launch_bounds__(1024) void sort_decode_mode1(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
+                                                          uint32_t nb, unsigned shift, unsigned try_bits, unsigned low_bits,
+                                                          const uint64_t* __restrict__ seq_base,
+                                                          const uint64_t* __restrict__ seq_len, uint32_t n_seq,
+                                                          const uint2* __restrict__ rank_rec, mp_hit* __restrict__ out,
+                                                          unsigned long long* __restrict__ h_out,
+                                                          const uint32_t* __restrict__ crowded, uint32_t n_cblk) {
+    __shared__ uint64_t s_k[kSortCap];
+    if (blockIdx.x < n_cblk) {  // block-uniform
+        const uint32_t n = crowded[0];
+        for (uint32_t c = blockIdx.x; c < n; c += n_cblk)
+            crowded_bucket(crowded[1 + c], s_k, keys, off, shift, try_bits, low_bits, seq_base, seq_len, n_seq, rank_rec, out);
+        return;
+    }
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t b0 = (blockIdx.x - n_cblk) * kMode1Buckets;
+    {
+        const bool in = b0 + wave < nb;
+        const uint32_t start = in ? off[b0 + wave] : 0u, m = in ? off[b0 + wave + 1] - start : 0u;
+        if (m > kSortCap && lane == 0) flag_overflow(h_out);
+        if (m > 0 && m <= 64) {  // wave-uniform; no barrier inside
+            const uint64_t key = lane < m ? keys[start + lane] : ~0ull;
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < m; ++j) {
+                const uint64_t kj = __shfl(key, (int)j, 64);
+                r += kj < key || (kj == key && j < lane);  // ties: stable
             }
-            if (on) {
-                if (k >= 128u) {  // j = 64: the lane's own two keys (i0 is the lower index)
-                    const bool up = (i0 & k) == 0;
-                    const uint64_t lo = e0 < e1 ? e0 : e1, hi = e0 < e1 ? e1 : e0;
-                    e0 = up ? lo : hi;
-                    e1 = up ? hi : lo;
-                }
-                for (uint32_t j = (k >> 1) < 32u ? (k >> 1) : 32u; j > 0; j >>= 1) {
-                    e0 = cx_lane(e0, i0, j, k);
-                    e1 = cx_lane(e1, i1, j, k);
-                }
-            }
+            const SeqRange sr = bucket_seqs(b0 + wave, shift, low_bits, seq_base, n_seq, lane);
+            if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
         }
-        if (on) {
-            const SeqRange sr = bucket_seqs(b, shift, low_bits, seq_base, n_seq, lane);
-            if (i0 < m) decode_hit(e0, start + i0, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
-            if (i1 < m) decode_hit(e1, start + i1, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
+        if (!__syncthreads_or(m > 64 && m <= kRankCap)) return;  // every wave reaches this barrier
+    }
+    for (uint32_t q = 0; q < kMode1Buckets && b0 + q < nb; ++q) {  // block-uniform loop
+        const uint32_t start = off[b0 + q], m = off[b0 + q + 1] - start;
+        if (m <= 64 || m > kRankCap) continue;  // done by its wave above / a crowded workgroup
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
+        const SeqRange sr = bucket_seqs(b0 + q, shift, low_bits, seq_base, n_seq, lane);  // every lane of every wave
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+            const uint64_t key = s_k[i];
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
+            decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
         }
+        __syncthreads();  // s_k is refilled by the next bucket
     }
 }
 
@@ -276,7 +344,7 @@ constexpr uint32_t kSlotWaves = 4;
 __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
     const uint64_t* __restrict__ slots, uint32_t slot_cap, const uint32_t* __restrict__ off, uint32_t nb,
     unsigned shift, unsigned try_bits, unsigned low_bits, const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
-    uint32_t n_seq, const uint32_t* __restrict__ inv_rank, const DevRec* __restrict__ recs, mp_hit* __restrict__ out,
+    uint32_t n_seq, const uint2* __restrict__ rank_rec, mp_hit* __restrict__ out,
     unsigned long long* __restrict__ h_out) {
     __shared__ uint64_t s_k[kSlotWaves][kSlotCap];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -297,7 +365,7 @@ __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
             const uint64_t kj = __shfl(key, (int)j, 64);
             r += kj < key || (kj == key && j < lane);  // ties: stable (keys are unique anyway)
         }
-        if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
+        if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
         return;
     }
     uint64_t* k = s_k[wave];
@@ -309,7 +377,7 @@ __global__ __launch_bounds__(64 * kSlotWaves) void sort_decode_slots(
         const uint64_t key = k[i];
         uint32_t r = 0;
         for (uint32_t j = 0; j < m; ++j) r += k[j] < key || (k[j] == key && j < i);
-        decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, inv_rank, recs, out);
+        decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
     }
 }
 
@@ -380,7 +448,7 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     if (mode == 0) {
         hipLaunchKernelGGL(sort_decode_slots, dim3((P.nb + kSlotWaves - 1) / kSlotWaves), dim3(64 * kSlotWaves), 0, st,
                            s->slots, P.slot_cap, off, P.nb, P.shift, P.try_bits, P.low_bits, g->d_base, g->d_len, g->n_seq,
-                           s->table->inv_rank, s->table->recs, s->out, s->d_hcnt);
+                           s->table->rank_rec, s->out, s->d_hcnt);
         MP_HIP_CHECK(hipGetLastError());
         return MP_OK;
     }
@@ -388,17 +456,26 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, sort_region_counts(s),
                        s->cap / kHitRegions, P.shift, cursor, s->tmp_hi);
     MP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
-                       s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits,
-                       g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out, s->d_hcnt, sort_crowded(s));
-    MP_HIP_CHECK(hipGetLastError());
     // crowded buckets: MP_CROWD_GRID workgroups (tuning; default one per CU)
     static const uint32_t crowd_grid = [] {
         const char* e = std::getenv("MP_CROWD_GRID");
         return e ? (uint32_t)std::max(1, std::atoi(e)) : 0u;
     }();
-    hipLaunchKernelGGL(crowded_sort_decode, dim3(crowd_grid ? crowd_grid : (uint32_t)s->n_cu), dim3(1024), 0, st, s->tmp_hi, off, P.shift, P.try_bits,
-                       P.low_bits, g->d_base, g->d_len, g->n_seq, s->table->inv_rank, s->table->recs, s->out,
+    const uint32_t cg = crowd_grid ? crowd_grid : (uint32_t)s->n_cu;
+    static const bool split = std::getenv("MP_ORDER_SPLIT") != nullptr;  // A/B: the two-launch form
+    if (!split) {
+        hipLaunchKernelGGL(sort_decode_mode1, dim3(cg + (P.nb + kMode1Buckets - 1) / kMode1Buckets), dim3(1024), 0, st,
+                           s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits, g->d_base, g->d_len, g->n_seq,
+                           s->table->rank_rec, s->out, s->d_hcnt, sort_crowded(s), cg);
+        MP_HIP_CHECK(hipGetLastError());
+        return MP_OK;
+    }
+    hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
+                       s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits,
+                       g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out, s->d_hcnt, sort_crowded(s));
+    MP_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(crowded_sort_decode, dim3(cg), dim3(1024), 0, st, s->tmp_hi, off, P.shift, P.try_bits,
+                       P.low_bits, g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out,
                        sort_crowded(s));
     MP_HIP_CHECK(hipGetLastError());
     return MP_OK;

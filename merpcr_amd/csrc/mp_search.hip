@@ -2485,8 +2485,7 @@ __global__ __launch_bounds__(1024) void finish_kernel(unsigned long long* __rest
 
 __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, uint64_t n,
                               const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
-                              uint32_t n_seq, const uint32_t* __restrict__ inv_rank,
-                              const DevRec* __restrict__ recs, mp_hit* __restrict__ out) {
+                              uint32_t n_seq, const uint2* __restrict__ rank_rec, mp_hit* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t gk = hi[i];
@@ -2498,10 +2497,11 @@ __global__ void decode_kernel(const uint64_t* __restrict__ hi, const uint64_t* _
         else b = mid;
     }
     const uint64_t k = gk - seq_base[a];
-    const uint32_t rec = inv_rank[l >> 32];
+    const uint2 rr = rank_rec[l >> 32];
+    const uint32_t rec = rr.x;
     const int32_t d = try_offset((uint32_t)l);
     const uint64_t len = seq_len[a];
-    const uint64_t size = recs[rec].size;
+    const uint64_t size = rr.y;
     const uint64_t e = size > len - k ? len - k : size;
     mp_hit h;
     h.pos1 = k;
@@ -2987,7 +2987,7 @@ static int redo_order(Search* s, hipStream_t st, int from, uint64_t nh, bool rai
         if (nh) {
             const uint32_t blocks = (uint32_t)((nh + 255) / 256);
             hipLaunchKernelGGL(decode_kernel, dim3(blocks), dim3(256), 0, st, hi, lo, nh,
-                               g->d_base, g->d_len, g->n_seq, t->inv_rank, t->recs, s->out);
+                               g->d_base, g->d_len, g->n_seq, t->rank_rec, s->out);
             MP_HIP_CHECK(hipGetLastError());
         }
         MP_HIP_CHECK(hipStreamSynchronize(st));

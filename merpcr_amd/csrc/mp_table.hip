@@ -53,7 +53,7 @@ static void free_table(Table* t) {
     free_table(t->split_a); free_table(t->split_b); free_table(t->split_rest);
     hipFree(t->dents12);
     hipFree(t->filt); hipFree(t->lfilt); hipFree(t->rk); hipFree(t->dents); hipFree(t->dents8); hipFree(t->dents16); hipFree(t->kgrp); hipFree(t->kgrp4); hipFree(t->binfo); hipFree(t->dfilt); hipFree(t->dgrp); hipFree(t->dgesc); hipFree(t->dsum); hipFree(t->dents_pad); hipFree(t->slots); hipFree(t->ents);
-    hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->planes); hipFree(t->prec);
+    hipFree(t->recs); hipFree(t->rank); hipFree(t->inv_rank); hipFree(t->rank_rec); hipFree(t->planes); hipFree(t->prec);
     hipFree(t->pchars);
     delete t;
 }
@@ -720,6 +720,11 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         if ((rc = upload(&t->recs, recs.data(), recs.size(), &bytes))) break;
         if ((rc = upload(&t->rank, rank.data(), rank.size(), &bytes))) break;
         if ((rc = upload(&t->inv_rank, order.data(), order.size(), &bytes))) break;
+        {
+            std::vector<uint2> rr(n_rec);
+            for (uint32_t i = 0; i < n_rec; ++i) rr[i] = make_uint2(order[i], recs[order[i]].size);
+            if ((rc = upload(&t->rank_rec, rr.data(), rr.size(), &bytes))) break;
+        }
         planes.push_back(0); planes.push_back(0); planes.push_back(0); planes.push_back(0);
         {
             std::vector<PairRec> prec(n_rec);
