@@ -46,8 +46,7 @@ __global__ __launch_bounds__(1024) void bucket_offsets(const uint32_t* __restric
     if (threadIdx.x == 0) s_crowd = 0;
     if (h_out) finish_fold(counters, n_words, h_out, rcount);
     __syncthreads();
-    // the crowded buckets (kRankCap < keys <= kSortCap) are listed here, so that the mode-1
-    // sort can start them first, beside the others (sort_decode_mode1)
+    // the crowded buckets (kRankCap < keys <= kSortCap) for crowded_sort_decode
     bucket_offsets_block(cnt, nb, off, cursor, s_v4, s_w, crowded, &s_crowd, kRankCap, kSortCap);
     __syncthreads();
     if (threadIdx.x == 0) crowded[0] = s_crowd;  // the previous run's sort is complete (stream order)
@@ -280,60 +279,6 @@ __global__ __launch_bounds__(1024) void crowded_sort_decode(const uint64_t* __re
         crowded_bucket(crowded[1 + c], s_k, keys, off, shift, try_bits, low_bits, seq_base, seq_len, n_seq, rank_rec, out);
 }
 
-// Order mode 1 in one launch (round 5): the first n_cblk workgroups sort the crowded buckets
-// that bucket_offsets listed (bitonic, crowded_bucket), and the others take kMode1Buckets
-// buckets each (a wave per bucket of up to 64 keys, the workgroup for 65..kRankCap).  Crowded
-// sorts are the longest, and as the lowest workgroup indices they start first, beside the
-// rest; as two launches (bucket_sort_decode, then crowded_sort_decode) c4 spent 68 + 69 us.
-constexpr uint32_t kMode1Buckets = 16;
-__global__ __launch_bounds__(1024) void sort_decode_mode1(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
-                                                          uint32_t nb, unsigned shift, unsigned try_bits, unsigned low_bits,
-                                                          const uint64_t* __restrict__ seq_base,
-                                                          const uint64_t* __restrict__ seq_len, uint32_t n_seq,
-                                                          const uint2* __restrict__ rank_rec, mp_hit* __restrict__ out,
-                                                          unsigned long long* __restrict__ h_out,
-                                                          const uint32_t* __restrict__ crowded, uint32_t n_cblk) {
-    __shared__ uint64_t s_k[kSortCap];
-    if (blockIdx.x < n_cblk) {  // block-uniform
-        const uint32_t n = crowded[0];
-        for (uint32_t c = blockIdx.x; c < n; c += n_cblk)
-            crowded_bucket(crowded[1 + c], s_k, keys, off, shift, try_bits, low_bits, seq_base, seq_len, n_seq, rank_rec, out);
-        return;
-    }
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t b0 = (blockIdx.x - n_cblk) * kMode1Buckets;
-    {
-        const bool in = b0 + wave < nb;
-        const uint32_t start = in ? off[b0 + wave] : 0u, m = in ? off[b0 + wave + 1] - start : 0u;
-        if (m > kSortCap && lane == 0) flag_overflow(h_out);
-        if (m > 0 && m <= 64) {  // wave-uniform; no barrier inside
-            const uint64_t key = lane < m ? keys[start + lane] : ~0ull;
-            uint32_t r = 0;
-            for (uint32_t j = 0; j < m; ++j) {
-                const uint64_t kj = __shfl(key, (int)j, 64);
-                r += kj < key || (kj == key && j < lane);  // ties: stable
-            }
-            const SeqRange sr = bucket_seqs(b0 + wave, shift, low_bits, seq_base, n_seq, lane);
-            if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
-        }
-        if (!__syncthreads_or(m > 64 && m <= kRankCap)) return;  // every wave reaches this barrier
-    }
-    for (uint32_t q = 0; q < kMode1Buckets && b0 + q < nb; ++q) {  // block-uniform loop
-        const uint32_t start = off[b0 + q], m = off[b0 + q + 1] - start;
-        if (m <= 64 || m > kRankCap) continue;  // done by its wave above / a crowded workgroup
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
-        const SeqRange sr = bucket_seqs(b0 + q, shift, low_bits, seq_base, n_seq, lane);  // every lane of every wave
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-            const uint64_t key = s_k[i];
-            uint32_t r = 0;
-            for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
-            decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
-        }
-        __syncthreads();  // s_k is refilled by the next bucket
-    }
-}
-
 // Order mode 0: pair_kernel left every bucket's keys in its slot (bucket b at b * slot_cap,
 // in arrival order) and, from its last block, the bucket offsets.  One wave per bucket ranks
 // the bucket's keys -- up to 64 by shuffles, up to slot_cap by counting through the wave's
@@ -462,14 +407,6 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
         return e ? (uint32_t)std::max(1, std::atoi(e)) : 0u;
     }();
     const uint32_t cg = crowd_grid ? crowd_grid : (uint32_t)s->n_cu;
-    static const bool split = std::getenv("MP_ORDER_SPLIT") != nullptr;  // A/B: the two-launch form
-    if (!split) {
-        hipLaunchKernelGGL(sort_decode_mode1, dim3(cg + (P.nb + kMode1Buckets - 1) / kMode1Buckets), dim3(1024), 0, st,
-                           s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits, g->d_base, g->d_len, g->n_seq,
-                           s->table->rank_rec, s->out, s->d_hcnt, sort_crowded(s), cg);
-        MP_HIP_CHECK(hipGetLastError());
-        return MP_OK;
-    }
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
                        s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits,
                        g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out, s->d_hcnt, sort_crowded(s));

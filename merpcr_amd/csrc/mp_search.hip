@@ -107,6 +107,8 @@ struct ScanArgs {
     // bases and the gap_post bases after the seed's span.
     uint32_t gap_at, gap_len, gap_post;
     uint32_t tail_ctr;      // counters[] slot of this scan's bucket-tail list (4; 5 for the gapped scan)
+    uint64_t tail_static;   // bucket-tail slots reserved statically, kStaticRefs per scan wave (the
+                            // list is [0, tail_static + counters[tail_ctr]))
     uint32_t sched_base;    // counters[] index of this scan's 8 chunk counters (kSchedBase, kSchedSplit...)
 };
 
@@ -858,13 +860,16 @@ constexpr uint32_t kRefChunk = MP_REF_CHUNK;
 #define MP_REF_CHUNK1 64
 #endif
 constexpr uint32_t kRefChunk1 = MP_REF_CHUNK1;  // the 8-B key groups' references (c3: 5.5M)
+constexpr uint32_t kStaticRefs = 64;  // bucket-tail slots each scan wave owns before its first reservation
 
 // kChunk: slots per reservation (a multiple of 64).  Every reservation is one returning atomic
 // on one address, and same-address atomics serialise at ~88 per microsecond: lists written at
 // more than ~5M entries per millisecond of scan take larger chunks (kRefChunk).
+// off0: the list's statically reserved slots (the counter counts from there).
 template <int kStride = 1, uint32_t kChunk = 64>
 __device__ __forceinline__ void append_chunked(unsigned long long* counter, uint4* buf, uint64_t cap, bool on,
-                                               const uint4& v, int lane, SurvChunk& C, const uint4& v2 = uint4{}) {
+                                               const uint4& v, int lane, SurvChunk& C, const uint4& v2 = uint4{},
+                                               uint64_t off0 = 0) {
     static_assert(kChunk % 64u == 0u, "whole waves of slots");
     const uint64_t m = __ballot(on);
     if (!m) return;
@@ -875,7 +880,7 @@ __device__ __forceinline__ void append_chunked(unsigned long long* counter, uint
     if (cnt > avail) {
         unsigned long long b = 0;
         if (lane == 0) b = atomicAdd(counter, (unsigned long long)kChunk);
-        nbase = shfl64((uint64_t)b, 0);
+        nbase = off0 + shfl64((uint64_t)b, 0);
     }
     if (on) {
         const uint32_t r = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
@@ -1031,7 +1036,7 @@ __device__ __forceinline__ void heads_and_tails(const ScanArgs& a, const SuperRe
         const uint64_t gp = sbase + pos;
         append_chunked<2>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, tail,
                           make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), e0.xstart, R.seq), lane, TC,
-                          make_uint4((uint32_t)Gp, (uint32_t)(Gp >> 32), exp_, n - pos));
+                          make_uint4((uint32_t)Gp, (uint32_t)(Gp >> 32), exp_, n - pos), a.tail_static);
     }
 }
 
@@ -1160,7 +1165,7 @@ __device__ __forceinline__ void drain_compact(const ScanArgs& a, const SuperRegs
     const uint64_t gp = sbase + p;
     append_chunked<2>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, defer,
                       make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), c.x, R.seq), lane, TC,
-                      make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
+                      make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p), a.tail_static);
 }
 
 // drain_seeds for the ranked queue (kMode 1, 1): the head comes straight from the
@@ -1626,7 +1631,18 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     WaveLds& L = s_wl[w];
     uint32_t ncand = 0;
     SurvChunk C{0, kChunkNone, 0u};
+    // the wave's first kStaticRefs bucket-tail slots are its own, [gwave * kStaticRefs, + kStaticRefs):
+    // when every wave took its first chunk with an atomic, the 4,096 reservations of a scan's
+    // first super-steps queued on one address (~88 per us) and the first two super-steps of a
+    // wave took 34 and 21 us against ~6.5 (per-super-step stamps, ablation 42).  Expressed as
+    // a chunk of kTC slots of which kTC - kStaticRefs are used.
+    constexpr uint32_t kTC = kRkf == 2 ? kRefChunk : (kRkf ? kRefChunk1 : 64u);
+    static_assert(kTC >= kStaticRefs, "static slots within one chunk");
+    // (Inline-tail scans rarely leave a reference: theirs start with no chunk.)
     SurvChunk TC{0, kChunkNone, 0u};
+    if constexpr (!kInline)
+        TC = SurvChunk{((uint64_t)blockIdx.x * kWaves + (uint64_t)(threadIdx.x >> 6)) * kStaticRefs - (kTC - kStaticRefs),
+                       kTC - kStaticRefs, 0u};
 
     SuperSched sch;
     uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kWaves, lane, a.sched_short);
@@ -1807,7 +1823,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         const uint64_t gp = sbase + p;
                         append_chunked<2, kRkf == 2 ? kRefChunk : kRefChunk1>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
                                                      make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), kKeyRef, R.seq), lane, TC,
-                                                     make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p));
+                                                     make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p), a.tail_static);
                     }
                     wave_sync();  // the next round rewrites the list
                     r0 += kSeedQR;
@@ -1870,7 +1886,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         ss = nx;
     }
     close_chunked(a.surv, a.surv_cap, lane, C);
-    close_chunked<2, kRkf == 2 ? kRefChunk : (kRkf ? kRefChunk1 : 64u)>(a.tails, a.tails_cap, lane, TC);
+    close_chunked<2, kTC>(a.tails, a.tails_cap, lane, TC);
     // candidate statistics
     add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);
 }
@@ -2198,83 +2214,16 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
 #define MP_TAIL_BPC 2
 #endif
 constexpr uint32_t kTailBPC = MP_TAIL_BPC;  // blocks per CU
-constexpr uint32_t kRingSeg = 256, kRingSegs = kTailBuf / kRingSeg;
-static_assert(kRingSegs == 8, "ring laps: position / kTailBuf");
-// tail_kernel<kRing>'s survivor push (wave-converged: every lane calls): the wave's
-// survivors get consecutive ring positions from one LDS atomic, wait until their segments
-// are back from the previous lap, are written, and are counted into their segments; a
-// segment that this wave completes is copied to the survivor list by this wave.
-__device__ __forceinline__ void ring_push(const ScanArgs& a, uint4* buf, uint32_t& head, uint32_t* done,
-                                          uint32_t* lap, bool ok, const uint4& sv, int lane) {
-    const uint64_t m = __ballot(ok);
-    if (!m) return;
-    const uint32_t n = (uint32_t)__popcll(m);
-    uint32_t p0 = 0;
-    if (lane == 0) p0 = atomicAdd(&head, n);
-    p0 = (uint32_t)__shfl((int)p0, 0, 64);
-    // the (at most two) segments of [p0, p0 + n): back from the previous lap?
-    const uint32_t pl = p0 + n - 1u;
-    for (;;) {  // wave-uniform
-        const uint32_t l0 = __hip_atomic_load(&lap[(p0 / kRingSeg) % kRingSegs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t l1 = __hip_atomic_load(&lap[(pl / kRingSeg) % kRingSegs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (l0 == p0 / kTailBuf && l1 == pl / kTailBuf) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    if (ok) buf[(p0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) % kTailBuf] = sv;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    // written counts: the first segment's share, then the rest in the second
-    const uint32_t s0 = p0 / kRingSeg, s1 = pl / kRingSeg;
-    const uint32_t c0 = s0 == s1 ? n : (s1 * kRingSeg - p0);
-    uint32_t full = 0;  // bit 0: segment s0 completed by this wave, bit 1: segment s1
-    if (lane == 0) {
-        if (atomicAdd(&done[s0 % kRingSegs], c0) + c0 == kRingSeg) full |= 1u;
-        if (s1 != s0 && atomicAdd(&done[s1 % kRingSegs], n - c0) + (n - c0) == kRingSeg) full |= 2u;
-    }
-    full = (uint32_t)__shfl((int)full, 0, 64);
-    for (uint32_t q = 0; q < 2; ++q) {
-        if (!((full >> q) & 1u)) continue;  // wave-uniform
-        const uint32_t sg = (q ? s1 : s0) % kRingSegs;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        unsigned long long g = 0;
-        if (lane == 0) g = atomicAdd(&a.counters[2], (unsigned long long)kRingSeg);
-        g = shfl64((uint64_t)g, 0);
-#pragma unroll
-        for (uint32_t t = 0; t < kRingSeg / 64u; ++t) {
-            const uint32_t k = t * 64u + (uint32_t)lane;
-            if (g + k < a.surv_cap) a.surv[g + k] = buf[sg * kRingSeg + k];
-        }
-        // every lane's copy has read its slots before the segment is handed back
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) {
-            done[sg] = 0;
-            __hip_atomic_fetch_add(&lap[sg], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
-}
-
-// kH12: the table has wide key groups (kgrp4), whose key references read the 8-B IUPAC heads.
-// kRing: no block barrier in the loop.  Survivors go into an LDS ring of kRingSegs segments
-// of kRingSeg entries: a wave reserves its survivors' slots with one LDS atomic, writes them,
-// and adds them to their segments' written counts; the wave that completes a segment copies
-// it to the survivor list with one global atomic (one per kRingSeg survivors).  A wave whose
-// slots fall in a segment not yet flushed from the ring's previous lap waits for it (its
-// earlier slots are all written, so the wait cannot close a cycle).  The block-synchronous
-// loop (two barriers per 1,024 references) kept every wave of a block at the pace of its
-// slowest chain (ref -> rank word -> head -> entries).
-template <bool kGap = false, bool kH12 = false, bool kRing = false>
+// kH12: the table has wide key groups (kgrp4), whose key references read the 8-B IUPAC heads
+template <bool kGap = false, bool kH12 = false>
 __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     __shared__ uint4 s_buf[kTailBuf];
     __shared__ uint32_t s_n;
     __shared__ unsigned long long s_base;
-    __shared__ uint32_t s_done[kRingSegs], s_lap[kRingSegs];
     if (threadIdx.x == 0) s_n = 0;
-    if (threadIdx.x < kRingSegs) {
-        s_done[threadIdx.x] = 0;
-        s_lap[threadIdx.x] = 0;
-    }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const uint64_t n_refs = umin64(a.counters[a.tail_ctr], a.tails_cap);
+    const uint64_t n_refs = umin64(a.tail_static + a.counters[a.tail_ctr], a.tails_cap);
     const uint64_t* exc = a.has_u ? a.gexc : a.ginv;
     uint32_t ncand = 0, nsurv = 0;
     // key references of a table with wide key groups: the 8-B IUPAC heads (kgrp_pass4); a run-time
@@ -2288,7 +2237,6 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
             v = a.tails[2 * i];
             w = a.tails[2 * i + 1];
         }
-        uint32_t cnt = 0;
         if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
             const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
             const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
@@ -2325,28 +2273,16 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
             } else {
                 e = a.ents[first];                                       // its count = tail length
             }
-            cnt = e.count;
-            // kRing: every lane runs the wave's largest count, so that the ring pushes below
-            // are wave-converged (a lane waiting on the ring inside a divergent branch could
-            // block the lane that would flush it)
-            uint32_t jn = cnt;
-            if constexpr (kRing) {
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) jn = max(jn, (uint32_t)__shfl_xor((int)jn, o, 64));
-            }
-            for (uint32_t j = 0; j < jn; ++j) {
-              bool ok = false;
-              uint4 sv{};
-              do {
-                if (j >= cnt) break;
+            const uint32_t cnt = e.count;
+            for (uint32_t j = 0; j < cnt; ++j) {
                 if (j) e = a.ents[first + j];
                 const uint64_t gk = gp - e.hash_off;
-                if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) break;  // k + l1 > n / not owned
+                if ((uint32_t)e.l1 > rem + e.hash_off || gk < a.g_lo || gk >= a.g_hi) continue;  // k + l1 > n / not owned
                 uint64_t G = Gs;
                 uint32_t ex = w.z;
                 if (e.hash_off) {  // seed inside the primer: bounds and window from the genome
                     const uint64_t sbase = a.seq_base[v.w];
-                    if (gp - sbase < e.hash_off) break;  // k < 0
+                    if (gp - sbase < e.hash_off) continue;  // k < 0
                     G = ext2(a.g2, gk);
                     ex = (uint32_t)(ext1(exc, gk) >> 32);
                 }
@@ -2355,18 +2291,13 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                     const uint64_t xg = G ^ e.code;
                     const uint32_t inv = a.has_u ? (uint32_t)(ext1(a.ginv, gk) >> 32) : ex;  // A/C/G/T/U are valid
                     const uint32_t im = (0xFFFFFFFFu >> a.gap_at) & ~(0xFFFFFFFFu >> (a.gap_at + a.gap_len));
-                    if (((xg | (xg >> 1)) & gm) == 0 && (inv & im) == 0) break;
+                    if (((xg | (xg >> 1)) & gm) == 0 && (inv & im) == 0) continue;
                 }
                 ++ncand;
                 bool exact = false;
-                if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) break;
+                if (fp_reject(a, G, ex, e.l1, e.code, e.pmask, exact)) continue;
                 ++nsurv;
-                ok = true;
-                sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
-              } while (false);
-              if constexpr (kRing) {
-                ring_push(a, s_buf, s_n, s_done, s_lap, ok, sv, lane);
-              } else if (ok) {
+                const uint4 sv = make_uint4((uint32_t)gk, (uint32_t)(gk >> 32), e.rec | (exact ? 0x80000000u : 0u), v.w);
                 const uint32_t at = atomicAdd(&s_n, 1u);
                 if (at < kTailBuf) {
                     s_buf[at] = sv;
@@ -2374,31 +2305,13 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                     const unsigned long long g = atomicAdd(&a.counters[2], 1ull);
                     if (g < a.surv_cap) a.surv[g] = sv;
                 }
-              }
             }
         }
-        if constexpr (!kRing) {
-            __syncthreads();
-            if (s_n >= kTailBuf / 2) tail_flush(a, s_buf, s_n, s_base);  // every thread reads s_n between barriers
-            __syncthreads();
-        }
-    }
-    if constexpr (kRing) {
-        // every wave's pushes are written; only the segment holding the last position can be
-        // partial (each full one was flushed by the wave that completed it)
         __syncthreads();
-        const uint32_t head = s_n, part = head % kRingSeg;
-        if (part && threadIdx.x < 64) {
-            const uint32_t seg0 = ((head / kRingSeg) % kRingSegs) * kRingSeg;
-            unsigned long long g = 0;
-            if (lane == 0) g = atomicAdd(&a.counters[2], (unsigned long long)part);
-            g = shfl64((uint64_t)g, 0);
-            for (uint32_t t = (uint32_t)lane; t < part; t += 64u)
-                if (g + t < a.surv_cap) a.surv[g + t] = s_buf[seg0 + t];
-        }
-    } else {
-        tail_flush(a, s_buf, s_n, s_base);
+        if (s_n >= kTailBuf / 2) tail_flush(a, s_buf, s_n, s_base);  // every thread reads s_n between barriers
+        __syncthreads();
     }
+    tail_flush(a, s_buf, s_n, s_base);
     add_stats(a, ncand, nsurv, lane);
 }
 
@@ -2582,7 +2495,9 @@ static size_t dense_lds_of(const Table* t) {
     return b;
 }
 
-constexpr uint64_t kDefaultHitCap = 1 << 16, kDefaultSurvCap = 1 << 20, kDefaultTailCap = 1 << 18;
+// (the tail list's first 64 slots per scan wave are static: 262,144 on a full-chip grid, per
+// half of a split run)
+constexpr uint64_t kDefaultHitCap = 1 << 16, kDefaultSurvCap = 1 << 20, kDefaultTailCap = 1 << 20;
 
 }  // namespace mp
 
@@ -2854,23 +2769,12 @@ static bool use_split(const Search* s) {
 // A split table scans its seeds one after another (the contiguous seed, the gapped seed, the
 // rest's dense scan), each appending to the one survivor list; the two seed scans keep their
 // bucket-tail references in the two halves of the tail list (counters 4 and 5).
-// The bucket-tail pass: the gapped seed's form, the wide key groups' IUPAC heads, and the
-// barrier-free ring form (MP_TAIL_RING=1, A/B).
+// The bucket-tail pass: the gapped seed's form, or the wide key groups' IUPAC heads.
 static void launch_tail(const Search* s, bool gap, bool h12, hipStream_t st, const ScanArgs& a) {
-    static const bool ring = [] {
-        const char* e = std::getenv("MP_TAIL_RING");
-        return e && std::atoi(e) != 0;
-    }();
     const dim3 g((uint32_t)s->n_cu * kTailBPC), b(kTailBlock);
-    if (ring) {
-        if (gap) hipLaunchKernelGGL((tail_kernel<true, false, true>), g, b, 0, st, a);
-        else if (h12) hipLaunchKernelGGL((tail_kernel<false, true, true>), g, b, 0, st, a);
-        else hipLaunchKernelGGL((tail_kernel<false, false, true>), g, b, 0, st, a);
-    } else {
-        if (gap) hipLaunchKernelGGL((tail_kernel<true, false>), g, b, 0, st, a);
-        else if (h12) hipLaunchKernelGGL((tail_kernel<false, true>), g, b, 0, st, a);
-        else hipLaunchKernelGGL((tail_kernel<false, false>), g, b, 0, st, a);
-    }
+    if (gap) hipLaunchKernelGGL((tail_kernel<true, false>), g, b, 0, st, a);
+    else if (h12) hipLaunchKernelGGL((tail_kernel<false, true>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((tail_kernel<false, false>), g, b, 0, st, a);
 }
 
 static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStream_t st, int mode) {
@@ -3010,7 +2914,10 @@ static int search_complete(Search* s, uint64_t* n_hits) {
     // a handle); kernels never write past a capacity.
     // (the hit list overflows when one of its regions does: cnt[kHitMaxRegion] > cap / kHitRegions)
     // (a split run's two seed scans each hold half the tail list: counters 4 and 5)
-    auto tails_need = [&]() { return use_split(s) ? 2 * std::max(cnt[4], cnt[5]) : cnt[4]; };
+    // (each list, or half, starts with a.tail_static static slots)
+    auto tails_need = [&]() {
+        return use_split(s) ? 2 * (a.tail_static + std::max(cnt[4], cnt[5])) : a.tail_static + cnt[4];
+    };
     for (int attempt = 0;
          cnt[2] > s->surv_cap || tails_need() > s->tails_cap || cnt[kHitMaxRegion] > s->cap / kHitRegions; ++attempt) {
         if (attempt == 3) return fail(MP_E_STATE, "mp_search_run: list overflow after growth");
@@ -3156,6 +3063,10 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
         a.g_lo = g_lo; a.g_hi = g_hi;
         a.sched_short = s->sched_short;
+        // the scan grid's static bucket-tail slots (launch_scan's grid; a dense scan has none,
+        // and its run launches no tail pass)
+        a.tail_static = (uint64_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU) *
+                        kWaves * kStaticRefs;
         // keys over 64 bits, or a forced rocPRIM sort: mode 2
         const int mode = run_order_mode(s);
         s->pend_mode = mode;
