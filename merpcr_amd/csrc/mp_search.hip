@@ -109,6 +109,7 @@ struct ScanArgs {
     uint32_t tail_ctr;      // counters[] slot of this scan's bucket-tail list (4; 5 for the gapped scan)
     uint64_t tail_static;   // bucket-tail slots reserved statically, kStaticRefs per scan wave (the
                             // list is [0, tail_static + counters[tail_ctr]))
+    uint32_t ref16;         // key references in the 16-B form (Ref16); else 32-B bucket references
     uint32_t sched_base;    // counters[] index of this scan's 8 chunk counters (kSchedBase, kSchedSplit...)
 };
 
@@ -1399,6 +1400,17 @@ __device__ __forceinline__ uint32_t kmer_dyn4(uint32_t d0, uint32_t d1, uint32_t
 // tail_kernel finds the bucket from the seed window's key.
 constexpr uint32_t kKeyRef = 0x80000000u;
 
+// 16-B key reference (round 5; the key-group scans, when the genome's padded length is under
+// 2^40 bases and it has fewer than 2^23 - 1 sequences): {seed position (40 bits), an
+// exception flag, the sequence (23 bits), the 32-base window at the seed}.  The 32-B form also
+// carried the window's exception bits and the bases left to the sequence's end; tail_kernel
+// now takes the latter from seq_base / seq_len and re-reads the former from the genome only
+// for a window that holds an exception base (the flag).  c4 writes and reads back ~16M
+// references per run.
+__device__ __forceinline__ uint4 ref16_make(uint64_t gp, uint32_t seq, uint64_t G, uint32_t ex) {
+    return make_uint4((uint32_t)gp, (uint32_t)(gp >> 32) | (ex ? 0x100u : 0u) | (seq << 9), (uint32_t)G, (uint32_t)(G >> 32));
+}
+
 // 32-bit funnel of bases p..p+15 of a lane's 48 bases (A, B, C = bases 0-15, 16-31,
 // 32-47), p in [0, 48); bases past 47 read as 0.
 __device__ __forceinline__ uint32_t funnel3(uint32_t A, uint32_t B, uint32_t C, uint32_t p) {
@@ -1821,9 +1833,13 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         uint32_t x;
                         window_from_regs(a, R, sbase, p, true, G, x);
                         const uint64_t gp = sbase + p;
-                        append_chunked<2, kRkf == 2 ? kRefChunk : kRefChunk1>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
-                                                     make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), kKeyRef, R.seq), lane, TC,
-                                                     make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p), a.tail_static);
+                        if (a.ref16)  // wave-uniform
+                            append_chunked<1, kTC>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
+                                                   ref16_make(gp, R.seq, G, x), lane, TC, uint4{}, a.tail_static);
+                        else
+                            append_chunked<2, kTC>(&a.counters[a.tail_ctr], a.tails, a.tails_cap, on,
+                                                   make_uint4((uint32_t)gp, (uint32_t)(gp >> 32), kKeyRef, R.seq), lane, TC,
+                                                   make_uint4((uint32_t)G, (uint32_t)(G >> 32), x, n - p), a.tail_static);
                     }
                     wave_sync();  // the next round rewrites the list
                     r0 += kSeedQR;
@@ -1886,7 +1902,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         ss = nx;
     }
     close_chunked(a.surv, a.surv_cap, lane, C);
-    close_chunked<2, kTC>(a.tails, a.tails_cap, lane, TC);
+    if (a.ref16) close_chunked<1, kTC>(a.tails, a.tails_cap, lane, TC);
+    else close_chunked<2, kTC>(a.tails, a.tails_cap, lane, TC);
     // candidate statistics
     add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);
 }
@@ -2215,7 +2232,8 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
 #endif
 constexpr uint32_t kTailBPC = MP_TAIL_BPC;  // blocks per CU
 // kH12: the table has wide key groups (kgrp4), whose key references read the 8-B IUPAC heads
-template <bool kGap = false, bool kH12 = false>
+// kRef16: the references are in the 16-B form (ScanArgs::ref16).
+template <bool kGap = false, bool kH12 = false, bool kRef16 = false>
 __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     __shared__ uint4 s_buf[kTailBuf];
     __shared__ uint32_t s_n;
@@ -2233,7 +2251,20 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride) {  // block-uniform
         const uint64_t i = b + threadIdx.x;
         uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
-        if (i < n_refs) {
+        if (kRef16) {
+            // 16-B key reference (ref16_make) -> the 32-B form's fields: the bases left from the
+            // sequence tables, the window's exception bits from the genome when flagged
+            if (i < n_refs) v = a.tails[i];
+            if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
+                const uint64_t gp = (uint64_t)v.x | ((uint64_t)(v.y & 0xFFu) << 32);
+                const uint32_t seq = v.y >> 9;
+                w.x = v.z;
+                w.y = v.w;
+                w.z = (v.y & 0x100u) ? (uint32_t)(ext1(exc, gp) >> 32) : 0u;
+                w.w = (uint32_t)(a.seq_len[seq] - (gp - a.seq_base[seq]));
+                v = make_uint4(v.x, v.y & 0xFFu, kKeyRef, seq);
+            }
+        } else if (i < n_refs) {
             v = a.tails[2 * i];
             w = a.tails[2 * i + 1];
         }
@@ -2666,10 +2697,17 @@ static void launch_fixed4(int fix, uint32_t grid, hipStream_t st, const ScanArgs
     else hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2, 0, 3>), dim3(grid), dim3(kBlock), 0, st, a);
 }
 
-static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t tiles, hipStream_t st, bool* tail) {
+// *ref16: the run's key references are in the 16-B form (the key-group scans; a0.ref16 says
+// whether the genome allows it), as the tail pass must read them.
+static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t tiles, hipStream_t st, bool* tail,
+                       uint32_t* ref16) {
+    ScanArgs a = a0;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU);
     *tail = false;
+    *ref16 = 0;
     if (t->gap_len) {  // gapped seed: the key-group path, every passing seed deferred to tail_kernel
+        a.ref16 = a0.ref16;
+        *ref16 = a.ref16;
         if (!(t->filt_direct && !t->lds_exact && t->kgrp_F >= 2 && a.W >= 11 && a.W <= 13 && a.defer_full))
             return fail(MP_E_STATE, "gapped seed table without key groups");
         // c5's shape (W = 8, N = 1) with its gap as constants; other W 7..9 shapes from the table
@@ -2699,6 +2737,11 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a, uint64_t ti
     const int fix = (a.W == (int)kFixW && a.I == 0 && !t->kgrp_wild && t->kgrp_F == kFixF && a.N <= 1 &&
                      !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
     const int fix4 = (a.W == (int)kFixW && a.N <= 2 && !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
+    // the forms below that leave key references (kRkf 1 and 2)
+    const bool keyref = !dense && !inl && !t->lds_exact &&
+                        ((rkf4 && (t->lds_k == 1 || t->lds_k == 2)) || (t->filt_direct && a.defer_full && rkf));
+    a.ref16 = keyref ? a0.ref16 : 0u;
+    *ref16 = a.ref16;
     if (dense) {
         const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
                                                             (uint64_t)s->n_cu * (uint64_t)s->dense_per_cu);
@@ -2772,9 +2815,15 @@ static bool use_split(const Search* s) {
 // The bucket-tail pass: the gapped seed's form, or the wide key groups' IUPAC heads.
 static void launch_tail(const Search* s, bool gap, bool h12, hipStream_t st, const ScanArgs& a) {
     const dim3 g((uint32_t)s->n_cu * kTailBPC), b(kTailBlock);
-    if (gap) hipLaunchKernelGGL((tail_kernel<true, false>), g, b, 0, st, a);
-    else if (h12) hipLaunchKernelGGL((tail_kernel<false, true>), g, b, 0, st, a);
-    else hipLaunchKernelGGL((tail_kernel<false, false>), g, b, 0, st, a);
+    if (a.ref16) {
+        if (gap) hipLaunchKernelGGL((tail_kernel<true, false, true>), g, b, 0, st, a);
+        else if (h12) hipLaunchKernelGGL((tail_kernel<false, true, true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((tail_kernel<false, false, true>), g, b, 0, st, a);
+    } else {
+        if (gap) hipLaunchKernelGGL((tail_kernel<true, false>), g, b, 0, st, a);
+        else if (h12) hipLaunchKernelGGL((tail_kernel<false, true>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((tail_kernel<false, false>), g, b, 0, st, a);
+    }
 }
 
 static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStream_t st, int mode) {
@@ -2787,11 +2836,12 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     if (timed) MP_HIP_CHECK(hipEventRecord(s->ev0, st));
     if (!use_split(s)) {
         bool tail = false;
-        const int rc = launch_scan(s, t, a, tiles, st, &tail);
+        ScanArgs ta = a;
+        const int rc = launch_scan(s, t, a, tiles, st, &tail, &ta.ref16);
         if (rc) return rc;
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
         if (tail) {
-            launch_tail(s, false, t->kgrp4 != nullptr, st, a);
+            launch_tail(s, false, t->kgrp4 != nullptr, st, ta);
             MP_HIP_CHECK(hipGetLastError());
         }
     } else {
@@ -2807,7 +2857,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
             pa[i].tails_cap = half;
             pa[i].tail_ctr = i == 1 ? 5u : 4u;
             pa[i].sched_base = i == 0 ? (uint32_t)kSchedBase : (uint32_t)(kSchedSplit + (i - 1) * 8 * kStatStride);
-            const int rc = launch_scan(s, sub[i], pa[i], tiles, st, &tail[i]);
+            const int rc = launch_scan(s, sub[i], pa[i], tiles, st, &tail[i], &pa[i].ref16);
             if (rc) return rc;
         }
         if (timed) MP_HIP_CHECK(hipEventRecord(s->evt, st));
@@ -3067,6 +3117,8 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         // and its run launches no tail pass)
         a.tail_static = (uint64_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU) *
                         kWaves * kStaticRefs;
+        // 16-B key references need the position in 40 bits and the sequence in 23 (ref16_make)
+        a.ref16 = (g->total < (1ull << 40) && g->n_seq + 1u < (1u << 23) && !std::getenv("MP_REF32")) ? 1u : 0u;
         // keys over 64 bits, or a forced rocPRIM sort: mode 2
         const int mode = run_order_mode(s);
         s->pend_mode = mode;
