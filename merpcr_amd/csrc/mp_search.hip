@@ -2706,8 +2706,7 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
     *tail = false;
     *ref16 = 0;
     if (t->gap_len) {  // gapped seed: the key-group path, every passing seed deferred to tail_kernel
-        a.ref16 = a0.ref16;
-        *ref16 = a.ref16;
+        a.ref16 = 0u;  // (32-B references: see keyref below)
         if (!(t->filt_direct && !t->lds_exact && t->kgrp_F >= 2 && a.W >= 11 && a.W <= 13 && a.defer_full))
             return fail(MP_E_STATE, "gapped seed table without key groups");
         // c5's shape (W = 8, N = 1) with its gap as constants; other W 7..9 shapes from the table
@@ -2738,8 +2737,9 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
                      !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
     const int fix4 = (a.W == (int)kFixW && a.N <= 2 && !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
     // the forms below that leave key references (kRkf 1 and 2)
-    const bool keyref = !dense && !inl && !t->lds_exact &&
-                        ((rkf4 && (t->lds_k == 1 || t->lds_k == 2)) || (t->filt_direct && a.defer_full && rkf));
+    // (16-B references only for the wide key groups: c4 leaves ~16M, whose traffic they halve;
+    // c3's 5.5M took 12 us longer in tail_kernel, which looks up the bases left per reference)
+    const bool keyref = !dense && !inl && !t->lds_exact && rkf4 && (t->lds_k == 1 || t->lds_k == 2);
     a.ref16 = keyref ? a0.ref16 : 0u;
     *ref16 = a.ref16;
     if (dense) {

@@ -47,7 +47,7 @@ _P1 = "    if (keep && !(v.z >> 31)) keep = primer_ok(a, gk, r.l1, r.p1_pl, r.p1
 _LPHIT = "            stage_try_hit(a, S, lane, hit, sgk, srk, t - slo);\n"
 _T_ENTRY = "    zero_sort_counts(a);\n    // stage the seed prefilter in LDS (once per persistent workgroup)"
 _T_STAGED = "    const int lane = threadIdx.x & 63;\n    const int w = threadIdx.x >> 6;\n    const uint64_t stride = (uint64_t)gridDim.x * kWaves;"
-_T_END = "    close_chunked(a.surv, a.surv_cap, lane, C);\n    close_chunked<2, kTC>"
+_T_END = "    close_chunked(a.surv, a.surv_cap, lane, C);\n    if (a.ref16) close_chunked<1, kTC>"
 _T_TAIL = "MP_EXPORT int mp_search_set_stage_timing(void* search, int32_t on) {"
 _WORDS = ("        w0 = a.g2[j >> 5];\n        w1 = a.g2[(j >> 5) + 1];\n        const uint64_t v0 = a.ginv[j >> 6];\n"
           "        const uint64_t v1 = a.ginv[(j >> 6) + 1];\n        const uint32_t sh = (uint32_t)(j & 32);  // branch-free")
