@@ -2248,28 +2248,13 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     // choice here cost c3's tail 17 us
     const uint2* kref_heads = kH12 ? a.dents12 : a.dents8;
     const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
-    // The next iteration's reference is loaded once this one's bucket loads are issued, so that
-    // its memory latency overlaps them (in-order vmcnt: issued earlier, it would gate them).
-    uint4 pv, pw;
-    auto fetch = [&](uint64_t i) {
-        pv = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-        pw = make_uint4(0u, 0u, 0u, 0u);
-        if (i < n_refs) {
-            if constexpr (kRef16) {
-                pv = a.tails[i];
-            } else {
-                pv = a.tails[2 * i];
-                pw = a.tails[2 * i + 1];
-            }
-        }
-    };
-    fetch((uint64_t)blockIdx.x * kTailBlock + threadIdx.x);
     for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride) {  // block-uniform
         const uint64_t i = b + threadIdx.x;
-        uint4 v = pv, w = pw;
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
         if (kRef16) {
             // 16-B key reference (ref16_make) -> the 32-B form's fields: the bases left from the
             // sequence tables, the window's exception bits from the genome when flagged
+            if (i < n_refs) v = a.tails[i];
             if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
                 const uint64_t gp = (uint64_t)v.x | ((uint64_t)(v.y & 0xFFu) << 32);
                 const uint32_t seq = v.y >> 9;
@@ -2279,26 +2264,22 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 w.w = (uint32_t)(a.seq_len[seq] - (gp - a.seq_base[seq]));
                 v = make_uint4(v.x, v.y & 0xFFu, kKeyRef, seq);
             }
+        } else if (i < n_refs) {
+            v = a.tails[2 * i];
+            w = a.tails[2 * i + 1];
         }
-        const bool live = !(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu);
-        // a key reference's bucket head: rank word, then the head
-        const uint32_t W = (uint32_t)a.W;
-        const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
-        const uint32_t h = kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
-                                : (uint32_t)(Gs >> (64u - 2u * W));
-        uint2 c = make_uint2(0u, 0u);
-        if (live && v.z == kKeyRef) {
-            const uint2 rw = a.rk[h >> 5];
-            c = kref_heads[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
-        }
-        __asm__ volatile("" ::: "memory");  // the prefetch stays behind the head load
-        if (b + stride < n_refs) fetch(i + stride);
-        if (live) {
+        if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
             const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            const uint64_t Gs = (uint64_t)w.x | ((uint64_t)w.y << 32);  // window at the seed
             const uint32_t rem = w.w;                                    // bases from the seed to the end
             uint32_t first = v.z;
             Entry e;
             if (v.z == kKeyRef) {  // a seed that passed the key groups: its bucket by key rank
+                const uint32_t W = (uint32_t)a.W;
+                const uint32_t h = kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
+                                        : (uint32_t)(Gs >> (64u - 2u * W));
+                const uint2 rw = a.rk[h >> 5];
+                const uint2 c = kref_heads[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
                 if (c.y & kHead8Full) {
                     first = c.x;  // the bucket's first entry
                     if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
