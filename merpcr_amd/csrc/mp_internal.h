@@ -273,10 +273,6 @@ struct Search {
     unsigned long long* h_cnt = nullptr;
     unsigned long long* d_hcnt = nullptr;   // h_cnt as the device sees it
     hipEvent_t evd = nullptr;               // the run's completion (polled, not slept on)
-    // order mode 1: crowded buckets sorted on a second stream beside the others (created on
-    // the first mode-1 run)
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool stage_timing = true;               // events around tail/pair/order too (mp_search_set_stage_timing)
     bool scan_timing = true;                // the scan kernel's own two events (mp_search_set_scan_timing)
     bool dirty = false;                     // counters not known to be zero (an abandoned run): memset first
@@ -509,8 +505,8 @@ __device__ __forceinline__ void bucket_runs(uint32_t b, bool on, int lane, uint3
 }
 // Exclusive scan of nb bucket counts by one 1024-thread workgroup: off[0..nb] (off[nb] =
 // total) and cursor[0..nb) = off.  The counts pass through LDS (s_v4: kOffTile counts) in
-// tiles: coalesced loads and stores (all kOffTile / 1024 loads of a thread in flight at once,
-// the next tile's issued before this one is scanned), kOffPer consecutive counts per thread inside a tile, a
+// tiles: coalesced loads and stores (all kOffTile / 1024 loads of a thread in flight at once:
+// one memory round trip per tile), kOffPer consecutive counts per thread inside a tile, a
 // wave shuffle scan and one LDS word per wave (s_w: 16).  (64 consecutive counts per thread
 // straight from memory made every access a 64-line gather: c4's 65,536 buckets took 80 us;
 // tiles of 8,192 took 36 us, eight round trips and 24 barriers; 32,768 spilled.)
@@ -526,16 +522,13 @@ __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32
     uint32_t* s_v = reinterpret_cast<uint32_t*>(s_v4);
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t carry = 0;
-    uint32_t ld[kOffPer];
-    auto load_tile = [&](uint32_t base) {
+    for (uint32_t base = 0; base < nb; base += kOffTile) {
+        uint32_t ld[kOffPer];
 #pragma unroll
         for (uint32_t j = 0; j < kOffPer; ++j) {
             const uint32_t i = j * 1024 + t;
             ld[j] = base + i < nb ? cnt[base + i] : 0u;
         }
-    };
-    load_tile(0);
-    for (uint32_t base = 0; base < nb; base += kOffTile) {
 #pragma unroll
         for (uint32_t j = 0; j < kOffPer; ++j) s_v[j * 1024 + t] = ld[j];
         if (crowded) {
@@ -543,7 +536,6 @@ __device__ __forceinline__ void bucket_offsets_block(const uint32_t* cnt, uint32
             for (uint32_t j = 0; j < kOffPer; ++j)
                 if (ld[j] > crowd_lo && ld[j] <= crowd_hi) crowded[1 + atomicAdd(s_crowd, 1u)] = base + j * 1024 + t;
         }
-        if (base + kOffTile < nb) load_tile(base + kOffTile);  // the next tile in flight during this one
         __syncthreads();
         uint32_t sum = 0;  // the thread's counts are read twice from LDS: sum, then the scan
 #pragma unroll

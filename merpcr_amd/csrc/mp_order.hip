@@ -407,34 +407,14 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
         return e ? (uint32_t)std::max(1, std::atoi(e)) : 0u;
     }();
     const uint32_t cg = crowd_grid ? crowd_grid : (uint32_t)s->n_cu;
-    // The crowded buckets (listed by bucket_offsets) are sorted on the handle's second stream
-    // while bucket_sort_decode takes the others: one after the other, c4 spent 64 + 73 us.
-    // (Both read the scattered keys and write disjoint output slots.)  MP_ORDER_ONE_STREAM=1
-    // keeps them on one stream (A/B).
-    static const bool one_stream = std::getenv("MP_ORDER_ONE_STREAM") != nullptr;
-    hipStream_t cst = st;
-    if (!one_stream) {
-        if (!s->aux) {
-            MP_HIP_CHECK(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
-            MP_HIP_CHECK(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-            MP_HIP_CHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
-        }
-        MP_HIP_CHECK(hipEventRecord(s->ev_fork, st));
-        MP_HIP_CHECK(hipStreamWaitEvent(s->aux, s->ev_fork, 0));
-        cst = s->aux;
-    }
-    hipLaunchKernelGGL(crowded_sort_decode, dim3(cg), dim3(1024), 0, cst, s->tmp_hi, off, P.shift, P.try_bits,
-                       P.low_bits, g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out,
-                       sort_crowded(s));
-    MP_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
                        s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits,
                        g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out, s->d_hcnt, sort_crowded(s));
     MP_HIP_CHECK(hipGetLastError());
-    if (!one_stream) {
-        MP_HIP_CHECK(hipEventRecord(s->ev_join, s->aux));
-        MP_HIP_CHECK(hipStreamWaitEvent(st, s->ev_join, 0));
-    }
+    hipLaunchKernelGGL(crowded_sort_decode, dim3(cg), dim3(1024), 0, st, s->tmp_hi, off, P.shift, P.try_bits,
+                       P.low_bits, g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out,
+                       sort_crowded(s));
+    MP_HIP_CHECK(hipGetLastError());
     return MP_OK;
 }
 

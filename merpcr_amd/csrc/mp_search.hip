@@ -2481,9 +2481,6 @@ static void free_search(Search* s) {
     if (s->ev3) hipEventDestroy(s->ev3);
     if (s->evt) hipEventDestroy(s->evt);
     if (s->evd) hipEventDestroy(s->evd);
-    if (s->ev_fork) hipEventDestroy(s->ev_fork);
-    if (s->ev_join) hipEventDestroy(s->ev_join);
-    if (s->aux) hipStreamDestroy(s->aux);
     if (s->h_cnt) hipHostFree(s->h_cnt);
     delete s;
 }
