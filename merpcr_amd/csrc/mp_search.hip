@@ -110,8 +110,6 @@ struct ScanArgs {
     uint64_t tail_static;   // bucket-tail slots reserved statically, kStaticRefs per scan wave (the
                             // list is [0, tail_static + counters[tail_ctr]))
     uint32_t ref16;         // key references in the 16-B form (Ref16); else 32-B bucket references
-    const uint4* pre;       // the key-group table, pulled into every XCD's L2 at the scan's start
-    uint32_t pre_n16;       // its size in 16-B words (0: no prefetch)
     uint32_t sched_base;    // counters[] index of this scan's 8 chunk counters (kSchedBase, kSchedSplit...)
 };
 
@@ -864,7 +862,6 @@ constexpr uint32_t kRefChunk = MP_REF_CHUNK;
 #endif
 constexpr uint32_t kRefChunk1 = MP_REF_CHUNK1;  // the 8-B key groups' references (c3: 5.5M)
 constexpr uint32_t kStaticRefs = 64;  // bucket-tail slots each scan wave owns before its first reservation
-constexpr uint32_t kPreRows = 4;      // 16-B words per thread of the scan's L2 prefetch (2 MB over 32 blocks)
 
 // kChunk: slots per reservation (a multiple of 64).  Every reservation is one returning atomic
 // on one address, and same-address atomics serialise at ~88 per microsecond: lists written at
@@ -1625,7 +1622,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     zero_sort_counts(a);
     // stage the seed prefilter in LDS (once per persistent workgroup): all eight 16-B loads of
     // a thread in flight before the first LDS store (one L2 round trip, not eight)
-    uint32_t pre_x = 0;
     {
         constexpr int kStage = (int)(kLdsFilterWords / 4 / kBlock);  // eight uint4 per thread (128 KiB)
         static_assert(kLdsFilterWords / 4 == kStage * kBlock, "whole uint4 rows per thread");
@@ -1633,22 +1629,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         uint4 v[kStage];
 #pragma unroll
         for (int k = 0; k < kStage; ++k) v[k] = src[threadIdx.x + k * kBlock];
-        // The key-group table into this XCD's L2 (its blocks x, x + 8, ... read one slice each,
-        // beside the filter): else the grid's first level-2 probes all miss at once
-        if constexpr (kRkf != 0) {
-            if (a.pre_n16 && gridDim.x >= 8u) {
-                const uint32_t per = (a.pre_n16 + (gridDim.x >> 3) - 1u) / (gridDim.x >> 3);
-                const uint32_t j0 = (blockIdx.x >> 3) * per;
-#pragma unroll
-                for (uint32_t k = 0; k < kPreRows; ++k) {
-                    const uint32_t j = threadIdx.x + k * kBlock;
-                    if (j < per && j0 + j < a.pre_n16) {
-                        const uint4 q = a.pre[j0 + j];
-                        pre_x ^= q.x ^ q.y ^ q.z ^ q.w;
-                    }
-                }
-            }
-        }
 #pragma unroll
         for (int k = 0; k < kStage; ++k) reinterpret_cast<uint4*>(s_lf)[threadIdx.x + k * kBlock] = v[k];
     }
@@ -1658,9 +1638,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     const int w = threadIdx.x >> 6;
     const uint64_t stride = (uint64_t)gridDim.x * kWaves;
     const uint64_t n_supers = a.spans[a.n_spans].super0;
-    // the prefetched words are used (so the loads stay): into the wave's queue, which the
-    // super-steps overwrite before reading
-    if (lane == 0) s_wl[w].rq.q[0] = (uint16_t)pre_x;
     const uint32_t W = kFix ? kFixW : (uint32_t)a.W;
     const uint32_t shw = 32u - 2u * W;
     WaveLds& L = s_wl[w];
@@ -2688,15 +2665,6 @@ static void scan_fields(ScanArgs& a, const Table* t, const Search* s) {
     a.defer_full = t->defer_full && (!s->opt.no_defer || t->gap_len);
     a.kgrp = reinterpret_cast<const uint2*>(t->kgrp); a.kgrp_F = t->kgrp_F; a.kgrp_wild = t->kgrp_wild;
     a.kgrp4 = t->kgrp4;
-    // the key-group table of a W = 11 table (2 MB: every XCD's L2 takes it); larger ones are not
-    // prefetched (MP_NO_PREFETCH=1: none, A/B)
-    {
-        static const bool no_pre = std::getenv("MP_NO_PREFETCH") != nullptr;
-        const uint64_t n16 = t->kgrp4 ? (1ull << (2 * t->prm.wordsize)) / kKgrp4Keys
-                                      : (t->kgrp ? (1ull << (2 * t->prm.wordsize)) / kKgrpKeys / 2 : 0);
-        a.pre = t->kgrp4 ? t->kgrp4 : reinterpret_cast<const uint4*>(t->kgrp);
-        a.pre_n16 = (!no_pre && n16 && n16 <= 32ull * kPreRows * kBlock) ? (uint32_t)n16 : 0u;
-    }
     a.filt = t->filt; a.filt_log2 = t->filt_log2; a.rk = t->rk; a.dents = t->dents; a.dents8 = t->dents8; a.dents16 = t->dents16; a.dents12 = t->dents12; a.lfilt = t->lfilt;
     a.slots = t->slots; a.slot_log2 = t->slot_log2;
     a.ents = t->ents;
