@@ -1510,6 +1510,34 @@ __device__ __forceinline__ bool kgrp_pass4(const ScanArgs& a, uint4 rw, uint32_t
     return (uint32_t)__popc((x | (x >> 1)) & pl) <= (kFix ? (uint32_t)(kFix - 1) : (uint32_t)a.N);
 }
 
+// The span of super-step x (wave-uniform; every lane active) and the next span's first
+// super-step.  Up to 63 spans (c3-c5: 24): one load per lane and a ballot -- a scan's first
+// super-step had waited for a binary search of ~5 dependent loads (its first super-step took
+// 15 us against ~6.2, per-super-step stamps); more spans: the binary search.
+__device__ __forceinline__ void span_find(const ScanArgs& a, uint64_t x, int lane, SeqSpan& pf, uint64_t& pf_end) {
+    if (a.n_spans < 64u) {
+        SeqSpan my{};
+        my.super0 = ~0ull;
+        if ((uint32_t)lane <= a.n_spans) my = a.spans[lane];  // spans[n_spans]: the sentinel
+        const int lo = __popcll(__ballot(my.super0 <= x)) - 1;
+        pf.super0 = shfl64(my.super0, lo);
+        pf.seq = (uint32_t)__shfl((int)my.seq, lo, 64);
+        pf.p_lo = (uint32_t)__shfl((int)my.p_lo, lo, 64);
+        pf.p_hi = (uint32_t)__shfl((int)my.p_hi, lo, 64);
+        pf.p_al = (uint32_t)__shfl((int)my.p_al, lo, 64);
+        pf_end = shfl64(my.super0, lo + 1);
+        return;
+    }
+    uint32_t lo = 0, hi = a.n_spans;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.spans[mid].super0 <= x) lo = mid;
+        else hi = mid;
+    }
+    pf = a.spans[lo];
+    pf_end = a.spans[lo + 1].super0;
+}
+
 // Persistent scan: every wave walks global super-steps blockIdx*kWaves + w, + all waves,
 // ...; a super-step is 2048 consecutive window positions of one sequence, 32 per lane.
 // The next super-step's plane words are loaded before the current one is processed.
@@ -1664,16 +1692,9 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     pf.super0 = 1;
     uint64_t pf_end = 0, pf_sbase = 0;
     uint32_t pf_n = 0;
-    auto locate = [&](uint64_t x) {
+    auto locate = [&](uint64_t x) {  // wave-uniform x, every lane active
         if (x >= pf.super0 && x < pf_end) return;
-        uint32_t lo = 0, hi = a.n_spans;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.spans[mid].super0 <= x) lo = mid;
-            else hi = mid;
-        }
-        pf = a.spans[lo];
-        pf_end = a.spans[lo + 1].super0;
+        span_find(a, x, lane, pf, pf_end);
         pf_sbase = a.seq_base[pf.seq];
         pf_n = (uint32_t)a.seq_len[pf.seq];
     };
@@ -2048,16 +2069,9 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     pf.super0 = 1;
     uint64_t pf_end = 0, pf_sbase = 0;
     uint32_t pf_n = 0;
-    auto locate = [&](uint64_t x) {
+    auto locate = [&](uint64_t x) {  // wave-uniform x, every lane active
         if (x >= pf.super0 && x < pf_end) return;
-        uint32_t lo = 0, hi = a.n_spans;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.spans[mid].super0 <= x) lo = mid;
-            else hi = mid;
-        }
-        pf = a.spans[lo];
-        pf_end = a.spans[lo + 1].super0;
+        span_find(a, x, lane, pf, pf_end);
         pf_sbase = a.seq_base[pf.seq];
         pf_n = (uint32_t)a.seq_len[pf.seq];
     };
