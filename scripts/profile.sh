@@ -15,8 +15,8 @@ run() {  # name, bench-args, rocprof args...
       > "$OUT/$name.log" 2>&1 || { echo "pass $name failed rc=$?"; tail -5 "$OUT/$name.log"; exit 1; }
   echo "pass $name ok"
 }
-run trace "$*" --kernel-trace --stats
-Q="--no-cpu-baseline --steps 5 --warmup 1 $*"
+run trace "--no-pmc $*" --kernel-trace --stats
+Q="--no-cpu-baseline --no-pmc --steps 5 --warmup 1 $*"
 run fetch "$Q" --pmc FETCH_SIZE --kernel-include-regex $KRE
 run write "$Q" --pmc WRITE_SIZE --kernel-include-regex $KRE
 run sq "$Q" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY --kernel-include-regex $KRE
