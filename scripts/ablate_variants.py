@@ -9,6 +9,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       scan pass two seed scans could share (the c5 single-pass question)
   2   level 1 and the positives' offset list
   3   level 1, the list and the level-2 loads (consumed, nothing more)
+  6   the key-group scans without their key-reference writes (the field filter and compaction
+      kept): what the references themselves cost in the scan
   30  no super-step loop (launch, LDS staging, statistics)
   31  no LDS staging and no loop
   40  per-wave wall-clock stamps (entry, LDS staged, loop end, exit) of scan_kernel, read back
@@ -132,6 +134,8 @@ VARIANTS = {
          ("struct SuperSched {", "__device__ ulonglong4 g_wave_times[8192];  // ablation 40\n"),
          (_T_TAIL, "MP_EXPORT int mp_debug_wave_times(ulonglong4* out, uint32_t n) {  // ablation 40\n"
                    "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_times), n * sizeof(ulonglong4)) == hipSuccess ? 0 : -1;\n}\n\n")],
+    6: [("                        if (a.ref16)  // wave-uniform\n",
+          "                        if (e < 0xFFFFFFFFu) continue;  // ablation 6\n")],
     42: None,  # variant 40 plus per-super-step stamps (below)
     70: [("        end = min(st + chunk, hi);\n        hint = st;\n        claim(lane);\n", "        lo = x;  // ablation 70\n"),
          ("        if (st >= hi) {\n            end = 0;\n            return n_supers;\n",
