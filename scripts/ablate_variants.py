@@ -28,6 +28,10 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       one super-step per wave left and claims single super-steps there
   71  the key-group field filter of kgrp_pass in branch-free form (round 4, DESIGN 4.2: every
       form computed and selected; 1/8 c3 scan 0.342 -> 0.348 ms)
+  80  tail_kernel reading its references (and the sequence tables / exception word they need)
+      and nothing more
+  81  tail_kernel up to the key's rank word and bucket head (no entries, no fingerprint test)
+  82  tail_kernel with survivors counted, not stored: no LDS buffer, no barriers, no flushes
   60  scan_kernel's genome-plane loads non-temporal (the stream kept out of L2's working set:
       the c4 level-2 tables, rank words + 16-B heads, are ~4.1 MB against a 4 MB L2)
 """
@@ -136,6 +140,13 @@ VARIANTS = {
                    "    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_times), n * sizeof(ulonglong4)) == hipSuccess ? 0 : -1;\n}\n\n")],
     6: [("                        if (a.ref16)  // wave-uniform\n",
           "                        if (e < 0xFFFFFFFFu) continue;  // ablation 6\n")],
+    80: [("        if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {\n            const uint64_t gp = (uint64_t)v.x | ((uint64_t)v.y << 32);",
+          "        ncand += (v.x != 0xFFFFFFFFu) ? ((w.w ^ w.z) & 1u) : 0u;  // ablation 80\n        v.x = v.y = 0xFFFFFFFFu;\n")],
+    81: [("                if (c.y & kHead8Full) {\n                    first = c.x;  // the bucket's first entry",
+          "                ncand += c.y & 1u;  // ablation 81\n                e.count = 0;\n                if (false)\n")],
+    82: [("                const uint32_t at = atomicAdd(&s_n, 1u);\n", "                ncand += sv.x & 1u;  // ablation 82\n                continue;\n"),
+         ("        __syncthreads();\n        if (s_n >= kTailBuf / 2)", "        if (false)  // ablation 82\n"),
+         ("        __syncthreads();\n    }\n    tail_flush(a, s_buf, s_n, s_base);", "        if (false)  // ablation 82\n")],
     42: None,  # variant 40 plus per-super-step stamps (below)
     70: [("        end = min(st + chunk, hi);\n        hint = st;\n        claim(lane);\n", "        lo = x;  // ablation 70\n"),
          ("        if (st >= hi) {\n            end = 0;\n            return n_supers;\n",

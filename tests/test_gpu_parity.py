@@ -735,18 +735,20 @@ def test_iupac_wide_key_groups_with_genome_ambiguity():
     assert got == exp
 
 
-@pytest.mark.parametrize("W,N,iupac", [(11, 2, 0.1), (11, 1, 0.3), (12, 2, 0.1), (13, 2, 0.1), (13, 2, 0.2)])
-def test_wide_key_groups_vs_rank_heads(W, N, iupac, monkeypatch):
+@pytest.mark.parametrize("W,N,iupac,n_sts", [(11, 2, 0.1, 30000), (11, 2, 0.1, 100000), (11, 1, 0.3, 30000),
+                                             (12, 2, 0.1, 40000), (13, 2, 0.1, 40000), (13, 2, 0.2, 40000)])
+def test_wide_key_groups_vs_rank_heads(W, N, iupac, n_sts, monkeypatch):
     """The I = 1 scan through the wide key groups (kgrp4, the default for c4-shaped tables)
     and through the rank words and 8-B IUPAC heads (MP_NO_KGRP4=1, read when the table is
     built) give the C oracle's hit list byte for byte: primers with IUPAC bases after the
     seed, short primers (fields past the primer's end), multi-record keys, groups with more
     than three present keys, N runs and planted amplicons.  MP_NO_KGRP4=-1 builds the wide key
     groups whenever the table can carry them (the pass-rate estimate skipped); a table that
-    takes the I = 1 8-B fields instead (kgrp_wild) is checked on that path in both runs."""
+    takes the I = 1 8-B fields instead (kgrp_wild) is checked on that path in both runs.
+    100k STS at W = 11 (c4's table): ~6% of the groups hold four or more keys and ~2% of the
+    keys have two records."""
     from merpcr_amd import synth
     from oracle import c_oracle as C
-    n_sts = {11: 30000, 12: 40000, 13: 40000}[W]
     sts = synth.make_sts(n_sts, seed=11 + W, W=W, iupac=iupac)
     rng = np.random.default_rng(W)
     glen = 3_000_000
@@ -755,7 +757,8 @@ def test_wide_key_groups_vs_rank_heads(W, N, iupac, monkeypatch):
         a = int(rng.integers(0, glen - 3000))
         g[a:a + int(rng.integers(50, 3000))] = ord("N")
     amps, starts = synth.amplicons(sts, glen, 5, N, 50, W)
-    for amp, st in list(zip(amps, starts))[::2]:
+    step = max(2, -(-460 // (glen // len(amps))))  # every step-th slot: planted amplicons do not overlap
+    for amp, st in list(zip(amps, starts))[::step]:
         if st + len(amp) <= glen:
             g[st:st + len(amp)] = np.frombuffer(amp, dtype=np.uint8)
     seq = g.tobytes().decode("ascii")
