@@ -26,7 +26,11 @@ static unsigned bits_for(uint64_t v) {
 // larger than kSortCap (hits piled on a few positions, e.g. a dense repeat) sets
 // h_out[kSortOverflow]; the host then sorts with rocPRIM instead.
 constexpr uint32_t kSortCap = 2048;
-constexpr uint32_t kRankCap = 256;  // buckets over this are "crowded" (bitonic, one workgroup each)
+// Buckets of more than kRankCap keys are "crowded" (crowded_sort_decode): up to kWaveSortCap
+// keys a wave sorts in its registers (wave_bitonic), larger ones the whole workgroup (bitonic
+// through LDS).
+constexpr uint32_t kRankCap = 256;
+constexpr uint32_t kWaveSortCap = 1024;
 constexpr unsigned kMaxBucketBits = 16;
 
 // Exclusive scan of the bucket counts by one 1024-thread workgroup (bucket_offsets_block,
@@ -139,58 +143,6 @@ __device__ inline void decode_hit(uint64_t key, uint64_t slot, unsigned try_bits
     out[slot] = h;
 }
 
-// kBucketsPerBlock buckets per 256-thread workgroup.  A bucket of at most 64 keys (the common
-// case: ~32 per bucket at capacity) is ranked by its own wave, counting the smaller keys
-// (unique: one hit per (k, record, try)) over shuffles.  The workgroup then takes the larger
-// ones up to 256 keys one after another, ranking by counting through LDS.  Buckets over 256
-// (c4: IUPAC primers over N runs pile up to 2,048 hits on a position) go to the crowded list
-// for crowded_sort_decode, one 1024-thread workgroup each: a 256-thread workgroup sorting
-// them one after another (bitonic, 66 barrier stages for 2,048 keys) made the longest
-// workgroup of this kernel the order stage's critical path.  (One workgroup per bucket left
-// c4's 65,536 workgroups of ~24 keys dispatch-bound: 94 us.)
-constexpr uint32_t kBucketsPerBlock = 4;
-__global__ __launch_bounds__(256) void bucket_sort_decode(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off,
-                                                          uint32_t nb, unsigned shift, unsigned try_bits, unsigned low_bits,
-                                                          const uint64_t* __restrict__ seq_base,
-                                                          const uint64_t* __restrict__ seq_len, uint32_t n_seq,
-                                                          const uint2* __restrict__ rank_rec,
-                                                          mp_hit* __restrict__ out, unsigned long long* __restrict__ h_out,
-                                                          uint32_t* __restrict__ crowded) {
-    __shared__ uint64_t s_k[kRankCap];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t b0 = blockIdx.x * kBucketsPerBlock;
-    {
-        const bool in = b0 + wave < nb;  // nb < kBucketsPerBlock under a forced sort_bucket_bits
-        const uint32_t start = in ? off[b0 + wave] : 0u, m = in ? off[b0 + wave + 1] - start : 0u;
-        if (m > kSortCap && lane == 0) flag_overflow(h_out);
-        if (m > 0 && m <= 64) {  // wave-uniform; no barrier inside
-            const uint64_t key = lane < m ? keys[start + lane] : ~0ull;
-            uint32_t r = 0;
-            for (uint32_t j = 0; j < m; ++j) {
-                const uint64_t kj = __shfl(key, (int)j, 64);
-                r += kj < key || (kj == key && j < lane);  // ties: stable
-            }
-            const SeqRange sr = bucket_seqs(b0 + wave, shift, low_bits, seq_base, n_seq, lane);
-            if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
-        }
-        if (!__syncthreads_or(m > 64 && m <= kRankCap)) return;  // every wave reaches this barrier
-    }
-    for (uint32_t q = 0; q < kBucketsPerBlock && b0 + q < nb; ++q) {  // block-uniform loop
-        const uint32_t start = off[b0 + q], m = off[b0 + q + 1] - start;
-        if (m <= 64 || m > kRankCap) continue;  // done by its wave above / crowded_sort_decode
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) s_k[i] = keys[start + i];
-        const SeqRange sr = bucket_seqs(b0 + q, shift, low_bits, seq_base, n_seq, lane);  // every lane of every wave
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-            const uint64_t key = s_k[i];
-            uint32_t r = 0;
-            for (uint32_t j = 0; j < m; ++j) r += s_k[j] < key || (s_k[j] == key && j < i);  // ties: stable
-            decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
-        }
-        __syncthreads();  // s_k is refilled by the next bucket
-    }
-}
-
 // One in-wave bitonic compare-exchange stage (j <= 32) on a lane's two keys: e0 at index
 // i0 = base + lane, e1 at i0 + 64; partners by shuffle, direction from bit k of the index.
 __device__ __forceinline__ uint64_t cx_lane(uint64_t e, uint32_t i, uint32_t j, uint32_t k) {
@@ -201,13 +153,125 @@ __device__ __forceinline__ uint64_t cx_lane(uint64_t e, uint32_t i, uint32_t j, 
     return (lower == up) ? (e < o ? e : o) : (e > o ? e : o);
 }
 
-// The crowded buckets (kRankCap < keys <= kSortCap) of a mode-1 run, one per 1024-thread
-// workgroup (persistent over the list): bitonic sort of the bucket padded to a power of two.
+// The value lane ^ J holds (J < 64, a compile-time constant), without the LDS crossbar where a
+// VALU permute does it: DPP quad permutes for J = 1, 2; a half-row mirror then a reversed quad
+// (lane ^ 7 ^ 3) for J = 4; a row rotate by 8 for J = 8; the swizzle unit for J = 16;
+// v_permlane32_swap for J = 32 (lanes 32-63 of the first operand swap with lanes 0-31 of the
+// second: with both = v, the first result holds v[lane - 32] in the upper half and the second
+// v[lane + 32] in the lower).
+template <uint32_t J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, uint32_t lane) {
+    if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    else if constexpr (J == 4) {
+        const int m = __builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, m, 0x1B, 0xF, 0xF, false);      // quad_perm [3,2,1,0]
+    } else if constexpr (J == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else if constexpr (J == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (16 << 10) | 0x1F);  // xor 16
+    else {
+        static_assert(J == 32, "lane partner within the wave");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return lane < 32u ? (uint32_t)r[1] : (uint32_t)r[0];
+    }
+}
+
+// Bitonic sort (ascending) of the 64 * kR keys one wave holds, kR per lane: element
+// i = 64 r + lane is register r of the lane.  Stages with j >= 64 pair two registers of the
+// same lane (their direction, bit k >= 128 of i, is the register's); stages with j < 64 pair
+// lanes (xor_lane).  No LDS array, no barrier.  Templates over (k, j) unroll every stage, so
+// register indices and permute patterns are constants.  (A run-time (k, j) loop over one
+// specialised stage per j, 5x less code, took c4's crowded buckets from 54 to 86 us.)
+template <int kR, uint32_t K, uint32_t J>
+__device__ __forceinline__ void bitonic_stage(uint64_t (&e)[kR], uint32_t lane) {
+    if constexpr (J >= 64u) {
+        constexpr uint32_t jr = J / 64u;
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kR; ++r) {
+            if ((r & jr) == 0u) {
+                const bool up = ((r * 64u) & K) == 0u;
+                const uint64_t x = e[r], y = e[r | jr];
+                const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
+                e[r] = up ? lo : hi;
+                e[r | jr] = up ? hi : lo;
+            }
+        }
+    } else {
+        const bool lower = (lane & J) == 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)kR; ++r) {
+            const uint64_t o = ((uint64_t)xor_lane<J>((uint32_t)(e[r] >> 32), lane) << 32) | xor_lane<J>((uint32_t)e[r], lane);
+            const bool up = ((r * 64u + lane) & K) == 0u;
+            e[r] = (lower == up) ? (e[r] < o ? e[r] : o) : (e[r] > o ? e[r] : o);
+        }
+    }
+    if constexpr (J > 1u) bitonic_stage<kR, K, J / 2u>(e, lane);
+}
+
+template <int kR, uint32_t K = 2>
+__device__ __forceinline__ void wave_bitonic(uint64_t (&e)[kR], uint32_t lane) {
+    bitonic_stage<kR, K, K / 2u>(e, lane);
+    if constexpr (K < 64u * (uint32_t)kR) wave_bitonic<kR, 2u * K>(e, lane);
+}
+
+// One bucket of 64 < m <= 64 kR keys, sorted and decoded by its wave.
+template <int kR>
+__device__ __forceinline__ void wave_sort_decode(const uint64_t* __restrict__ keys, uint32_t start, uint32_t m,
+                                                 uint32_t lane, unsigned try_bits, unsigned low_bits,
+                                                 const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len,
+                                                 SeqRange sr, const uint2* __restrict__ rank_rec, mp_hit* __restrict__ out) {
+    uint64_t e[kR];
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kR; ++r) e[r] = r * 64u + lane < m ? keys[start + r * 64u + lane] : ~0ull;
+    wave_bitonic<kR>(e, lane);
+#pragma unroll
+    for (uint32_t r = 0; r < (uint32_t)kR; ++r)
+        if (r * 64u + lane < m) decode_hit(e[r], start + r * 64u + lane, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
+}
+
+// One wave per bucket, kBucketsPerBlock waves per workgroup, no barrier.  A bucket of at most
+// 64 keys (the common case: ~32 per bucket at capacity) is ranked by counting the smaller keys
+// (unique: one hit per (k, record, try)) over shuffles; up to kRankCap keys by a register
+// bitonic sort of 256 slots (wave_bitonic).  Larger buckets are on the crowded list for
+// crowded_sort_decode, which keeps the 512- and 1,024-slot register sorts (and their VGPRs)
+// out of this kernel's occupancy.  c4 (1.6M hits, ~100 tries of one (k, record) on each of 12k
+// positions): 5.6k buckets of 65-256 keys and 1.6k of 257-849.  Round 4 ranked the 65-256 ones
+// by counting through LDS (256-thread workgroup per bucket in turn) and sorted the rest with
+// 1024-thread bitonic sorts through LDS: 62 + 66 us.  (One workgroup per bucket left c4's
+// 65,536 workgroups of ~24 keys dispatch-bound: 94 us.)
+constexpr uint32_t kBucketsPerBlock = 4;
+__global__ __launch_bounds__(64 * kBucketsPerBlock) void bucket_sort_decode(
+    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ off, uint32_t nb, unsigned shift, unsigned try_bits,
+    unsigned low_bits, const uint64_t* __restrict__ seq_base, const uint64_t* __restrict__ seq_len, uint32_t n_seq,
+    const uint2* __restrict__ rank_rec, mp_hit* __restrict__ out, unsigned long long* __restrict__ h_out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t b = blockIdx.x * kBucketsPerBlock + (threadIdx.x >> 6);
+    if (b >= nb) return;  // wave-uniform; no barrier in this kernel
+    const uint32_t start = off[b], m = off[b + 1] - start;
+    if (m > kSortCap && lane == 0) flag_overflow(h_out);
+    if (m == 0 || m > kRankCap) return;  // crowded: crowded_sort_decode
+    const SeqRange sr = bucket_seqs(b, shift, low_bits, seq_base, n_seq, lane);
+    if (m <= 64) {
+        const uint64_t key = lane < m ? keys[start + lane] : ~0ull;
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint64_t kj = __shfl(key, (int)j, 64);
+            r += kj < key || (kj == key && j < lane);  // ties: stable
+        }
+        if (lane < m) decode_hit(key, start + r, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
+    } else {
+        static_assert(kRankCap == 256, "4 keys per lane");
+        wave_sort_decode<4>(keys, start, m, lane, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
+    }
+}
+
+// The crowded buckets (kRankCap < keys <= kSortCap) of a mode-1 run.  Up to kWaveSortCap keys:
+// one wave each (wave_sort_decode, 512 or 1,024 register slots).  Larger ones: one 1024-thread
+// workgroup each (persistent over the list), bitonic sort of the bucket padded to a power of two.
 // Wave w holds keys [128 w, 128 w + 128) in registers, two per lane (i and i + 64): every
 // stage with j <= 64 is a register compare or a shuffle, and only the stages with j >= 128
 // (10 of the 66 for 2,048 keys) go through LDS with a barrier each.  (All 66 through LDS,
 // one barrier each: c4's crowded buckets took 109 us.)
-// One crowded bucket b (kRankCap < keys <= kSortCap) sorted and decoded by the whole
+// One crowded bucket b (kWaveSortCap < keys <= kSortCap) sorted and decoded by the whole
 // 1024-thread workgroup (s_k: kSortCap keys of LDS).
 __device__ __forceinline__ void crowded_bucket(uint32_t b, uint64_t* s_k, const uint64_t* __restrict__ keys,
                                                const uint32_t* __restrict__ off, unsigned shift, unsigned try_bits,
@@ -217,7 +281,7 @@ __device__ __forceinline__ void crowded_bucket(uint32_t b, uint64_t* s_k, const 
     const uint32_t lane = threadIdx.x & 63u, base = (threadIdx.x >> 6) * 128u;
     const uint32_t i0 = base + lane, i1 = i0 + 64u;
     const uint32_t start = off[b], m = off[b + 1] - start;
-    uint32_t P = 2 * kRankCap;
+    uint32_t P = kWaveSortCap;
     while (P < m) P <<= 1;
     const bool on = base < P;  // wave-uniform: this wave holds keys of the padded bucket
     uint64_t e0 = i0 < m ? keys[start + i0] : ~0ull, e1 = i1 < m ? keys[start + i1] : ~0ull;
@@ -275,8 +339,25 @@ __global__ __launch_bounds__(1024) void crowded_sort_decode(const uint64_t* __re
     __shared__ uint64_t s_k[kSortCap];
     static_assert(kSortCap == 2 * 1024, "two keys per thread of the 1024-thread workgroup");
     const uint32_t n = crowded[0];
-    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x)  // block-uniform
-        crowded_bucket(crowded[1 + c], s_k, keys, off, shift, try_bits, low_bits, seq_base, seq_len, n_seq, rank_rec, out);
+    // up to kWaveSortCap keys: one wave per bucket, registers only (no barrier in this loop)
+    // list items go round-robin over the workgroups first (item c to workgroup c mod grid), so
+    // that a short list spreads over every CU (c4: 1.6k items, 256 workgroups of 16 waves;
+    // consecutive items per workgroup had filled 102 CUs with 16 sorts each)
+    const uint32_t lane = threadIdx.x & 63u, waves = gridDim.x * (blockDim.x / 64u);
+    for (uint32_t c = (threadIdx.x >> 6) * gridDim.x + blockIdx.x; c < n; c += waves) {  // wave-uniform
+        const uint32_t b = crowded[1 + c], start = off[b], m = off[b + 1] - start;
+        if (m > kWaveSortCap) continue;
+        const SeqRange sr = bucket_seqs(b, shift, low_bits, seq_base, n_seq, lane);
+        if (m <= 512u) wave_sort_decode<8>(keys, start, m, lane, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
+        else wave_sort_decode<16>(keys, start, m, lane, try_bits, low_bits, seq_base, seq_len, sr, rank_rec, out);
+    }
+    static_assert(kWaveSortCap == 1024 && 2 * kRankCap == 512, "8 and 16 keys per lane");
+    // larger: the whole workgroup per bucket
+    for (uint32_t c = blockIdx.x; c < n; c += gridDim.x) {  // block-uniform
+        const uint32_t b = crowded[1 + c];
+        if (off[b + 1] - off[b] > kWaveSortCap)
+            crowded_bucket(b, s_k, keys, off, shift, try_bits, low_bits, seq_base, seq_len, n_seq, rank_rec, out);
+    }
 }
 
 // Order mode 0: pair_kernel left every bucket's keys in its slot (bucket b at b * slot_cap,
@@ -409,7 +490,7 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     const uint32_t cg = crowd_grid ? crowd_grid : (uint32_t)s->n_cu;
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
                        s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits,
-                       g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out, s->d_hcnt, sort_crowded(s));
+                       g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out, s->d_hcnt);
     MP_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(crowded_sort_decode, dim3(cg), dim3(1024), 0, st, s->tmp_hi, off, P.shift, P.try_bits,
                        P.low_bits, g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out,

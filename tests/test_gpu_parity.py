@@ -86,11 +86,12 @@ def test_bundled_search_to_file():
     assert text == "L78833\t75823..76023\tAFM248yg9\t(D17S932)  Chr.17, 63.7 cM\t(-)\n"
 
 
-@pytest.mark.parametrize("bits", [0, 1, 4])
+@pytest.mark.parametrize("bits", [0, 1, 4, 5, 6, 7])
 def test_dense_repeat_order(bits):
     """15,936 hits on an 8 kbp repeat; with 2 forced device-sort buckets they overflow the
-    per-bucket capacity and the rocPRIM fallback orders them, with 16 each bucket holds
-    ~1,000 keys ranked in LDS."""
+    per-bucket capacity and the rocPRIM fallback orders them; with 16 buckets of ~1,000 keys
+    some go to the crowded workgroup sort (over 1,024) and the rest to a wave's 1,024-slot
+    register sort; 32, 64 and 128 buckets take the 1,024- and 256-slot register sorts."""
     case = load_golden("repeat.json.gz")
     eng = _engine(case["params"])
     eng.search_options = dict(sort_bucket_bits=bits)
