@@ -2221,7 +2221,10 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
 // the survivor counter per flush, and those serialise at one address (~11 ns each), so
 // 512 blocks where 2,048 smaller ones spent ~20 us on them at the kernel's end.
 constexpr uint32_t kTailBlock = 1024;
-constexpr uint32_t kTailBuf = 2048;
+#ifndef MP_TAIL_BUF
+#define MP_TAIL_BUF 4096
+#endif
+constexpr uint32_t kTailBuf = MP_TAIL_BUF;
 static_assert(kKeyRef == 0x80000000u, "key references: bucket field 2^31 (ents indices are below)");
 __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32_t& n_sh,
                                            unsigned long long& base_sh) {
@@ -2245,6 +2248,14 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
 #define MP_TAIL_BPC 2
 #endif
 constexpr uint32_t kTailBPC = MP_TAIL_BPC;  // blocks per CU
+// At most this many passes of 1,024 references between two checks of the block's survivor
+// buffer (round 5; a check is two barriers, and a barrier waits for the block's slowest wave:
+// c4's tail spent 67 of its 312 us in the buffer and its barriers, ablation 82).  c4 tail, one
+// check per 1 / 2 / 4 / 8 / 16 passes: 0.315 / 0.298 / 0.283 / 0.271 / 0.264 ms.
+#ifndef MP_TAIL_CHECK
+#define MP_TAIL_CHECK 16
+#endif
+constexpr uint32_t kTailCheck = MP_TAIL_CHECK;
 // kH12: the table has wide key groups (kgrp4), whose key references read the 8-B IUPAC heads
 // kRef16: the references are in the 16-B form (ScanArgs::ref16).
 template <bool kGap = false, bool kH12 = false, bool kRef16 = false>
@@ -2262,7 +2273,8 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     // choice here cost c3's tail 17 us
     const uint2* kref_heads = kH12 ? a.dents12 : a.dents8;
     const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
-    for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride) {  // block-uniform
+    uint32_t it = 0, next_check = 0, period = 1, fill0 = 0;  // buffer checks (block-uniform)
+    for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride, ++it) {  // block-uniform
         const uint64_t i = b + threadIdx.x;
         uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
         if (kRef16) {
@@ -2352,9 +2364,21 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 }
             }
         }
-        __syncthreads();
-        if (s_n >= kTailBuf / 2) tail_flush(a, s_buf, s_n, s_base);  // every thread reads s_n between barriers
-        __syncthreads();
+        // The buffer's fill is read by every thread between two barriers at a check, and the
+        // waves run free between checks.  The next check comes after as many passes as the
+        // buffer's free half holds at the survivor rate since the last one (1..kTailCheck): c4's
+        // ~130 survivors per pass check every 16 passes; a denser table checks every pass, as
+        // before round 5, instead of spilling a burst to one global atomic per survivor.
+        if (it == next_check) {  // block-uniform
+            __syncthreads();
+            const uint32_t f = s_n;
+            const uint32_t rate = (f - fill0 + period - 1u) / period;
+            if (f >= kTailBuf / 4u) tail_flush(a, s_buf, s_n, s_base);  // barriers inside, s_n = 0 after
+            else __syncthreads();  // every thread has read s_n before the next pass appends
+            fill0 = f >= kTailBuf / 4u ? 0u : f;
+            period = max(1u, min(kTailCheck, (kTailBuf / 2u) / max(rate, 1u)));
+            next_check = it + period;
+        }
     }
     tail_flush(a, s_buf, s_n, s_base);
     add_stats(a, ncand, nsurv, lane);

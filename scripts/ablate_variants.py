@@ -145,8 +145,7 @@ VARIANTS = {
     81: [("                if (c.y & kHead8Full) {\n                    first = c.x;  // the bucket's first entry",
           "                ncand += c.y & 1u;  // ablation 81\n                e.count = 0;\n                if (false)\n")],
     82: [("                const uint32_t at = atomicAdd(&s_n, 1u);\n", "                ncand += sv.x & 1u;  // ablation 82\n                continue;\n"),
-         ("        __syncthreads();\n        if (s_n >= kTailBuf / 2)", "        if (false)  // ablation 82\n"),
-         ("        __syncthreads();\n    }\n    tail_flush(a, s_buf, s_n, s_base);", "        if (false)  // ablation 82\n")],
+         ("        if (it == next_check) {  // block-uniform\n", "        if (false)  // ablation 82\n")],
     42: None,  # variant 40 plus per-super-step stamps (below)
     70: [("        end = min(st + chunk, hi);\n        hint = st;\n        claim(lane);\n", "        lo = x;  // ablation 70\n"),
          ("        if (st >= hi) {\n            end = 0;\n            return n_supers;\n",
