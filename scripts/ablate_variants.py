@@ -28,6 +28,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       one super-step per wave left and claims single super-steps there
   71  the key-group field filter of kgrp_pass in branch-free form (round 4, DESIGN 4.2: every
       form computed and selected; 1/8 c3 scan 0.342 -> 0.348 ms)
+  90  64 v_nop per lane per super-step added to scan_kernel (~+8% of c3's VALU instructions):
+      does issue bind the scan?  91: 128 (~+17%)
   80  tail_kernel reading its references (and the sequence tables / exception word they need)
       and nothing more
   81  tail_kernel up to the key's rank word and bucket head (no entries, no fingerprint test)
@@ -146,6 +148,10 @@ VARIANTS = {
           "                ncand += c.y & 1u;  // ablation 81\n                e.count = 0;\n                if (false)\n")],
     82: [("                const uint32_t at = atomicAdd(&s_n, 1u);\n", "                ncand += sv.x & 1u;  // ablation 82\n                continue;\n"),
          ("        if (it == next_check) {  // block-uniform\n", "        if (false)  // ablation 82\n")],
+    90: [("        const uint32_t okm = (kGap ? window_ok_mask(R.iv, g_at) &",
+          "        asm volatile(\".rept 64\\n v_nop\\n .endr\");  // ablation 90\n")],
+    91: [("        const uint32_t okm = (kGap ? window_ok_mask(R.iv, g_at) &",
+          "        asm volatile(\".rept 128\\n v_nop\\n .endr\");  // ablation 91\n")],
     42: None,  # variant 40 plus per-super-step stamps (below)
     70: [("        end = min(st + chunk, hi);\n        hint = st;\n        claim(lane);\n", "        lo = x;  // ablation 70\n"),
          ("        if (st >= hi) {\n            end = 0;\n            return n_supers;\n",
