@@ -436,6 +436,9 @@ def main():
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="diagnostic: every rank on device 0 (rehearses the N-rank path, RCCL included, on a "
                          "one-GPU box); the JSON line is then not the metric")
+    ap.add_argument("--gather", default="ipc", choices=["ipc", "rccl", "host"],
+                    help="N > 1: the per-step hit gather to rank 0 -- ipc: copy-engine puts into rank 0's "
+                         "regions (IpcGather, no kernel on the CUs); rccl: mp_comm_gather_hits; host: gloo")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one search handle: every step waits for the previous one (no run queued ahead)")
     ap.add_argument("--handles", type=int, default=2,
@@ -469,12 +472,16 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = None
+    gmode = args.gather if world > 1 else None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")          # control plane only
-        # data plane: RCCL inside libmerpcr_hip (RCCL refuses two ranks on one device: the
-        # one-GPU rehearsal gathers through gloo on the host instead)
-        comm = None if args.rehearse_one_gpu else native_comm(local)
+        # data plane (--gather): copy-engine puts into rank 0's HBM (default), or RCCL inside
+        # libmerpcr_hip (RCCL refuses two ranks on one device: a one-GPU rehearsal asking for
+        # it gathers through gloo on the host instead)
+        if gmode == "rccl" and args.rehearse_one_gpu:
+            gmode = "host"
+        comm = native_comm(local) if gmode == "rccl" else None
 
     cfg = dict(synth.CONFIGS[args.config])
     total = int(cfg["total"] * args.scale) // 64 * 64
@@ -512,10 +519,34 @@ def main():
         f"range={rng}")
 
     gathered = None
-    last_gloo = [None]  # rehearsal: the host-gathered bytes of the last step
-    if world > 1:
+    last_gloo = [None]  # host gather: the host-gathered bytes of the last step
+    if gmode == "rccl":
         gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)  # rank 0's gather buffer
     shift = len(lens) * rank if weak else 0
+    ipcg = None
+    if gmode == "ipc":
+        # regions of twice the largest rank's hit count (one untimed run to learn it); every
+        # rank must map rank 0's buffers, else the job falls back to RCCL (or the host gather)
+        from merpcr_amd.dist import IpcGather
+        n0 = search.run(rng, stream)
+        every = [None] * world
+        dist.all_gather_object(every, n0)
+        err = None
+        try:
+            ipcg = IpcGather(local, max(4096, 2 * max(every)))
+        except Exception as e:  # noqa: BLE001 (reported, then every rank takes the same fallback)
+            err = f"{type(e).__name__}: {e}"
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+        if any(errs):
+            log(f"[rank {rank}] IPC gather unavailable ({[x for x in errs if x][0]}); falling back")
+            if ipcg is not None:
+                ipcg.close()
+            ipcg = None
+            gmode = "host" if args.rehearse_one_gpu else "rccl"
+            if gmode == "rccl":
+                comm = native_comm(local)
+                gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)
 
     # Steps are pipelined two deep (mp_search_enqueue / mp_search_complete on two search
     # handles over the same resident table and genome): step i+1's kernels are queued before
@@ -540,13 +571,17 @@ def main():
     gdone = [None] * nbuf
     scan_ms = []
 
-    def gather(h):
-        """Every rank's hits of handle h's completed run to rank 0; the job's hit count."""
+    def gather(h, j):
+        """Every rank's hits of handle h's completed run to rank 0; the job's hit count (this
+        rank's under --gather ipc: rank 0 reads the counts after the steps)."""
         nonlocal gathered
         n = h.last_hits()
         if world == 1:
             return n, None
-        if comm is None:  # rehearsal: host gather over gloo
+        if ipcg is not None:  # on the handle's stream: its next run waits for the copy
+            ipcg.put(h, streams[j].cuda_stream)
+            return n, None
+        if comm is None:  # host gather over gloo
             from merpcr_amd.dist import gather_hits as gloo_gather
             mine = h.fetch(n, stream)
             buf_h = torch.from_numpy(np.frombuffer(mine.tobytes() + b"\0" * HIT_BYTES, dtype=np.uint8).copy())
@@ -574,7 +609,7 @@ def main():
         sm = h.last_stats()["scan_ms"]
         if sm >= 0:
             scan_ms.append(sm)
-        n, gdone[j] = gather(h)
+        n, gdone[j] = gather(h, j)
         return n
 
     def run_steps(k):
@@ -617,6 +652,8 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    if ipcg is not None and rank == 0:  # every rank's puts are complete (synchronised before the barrier)
+        nhits = int(sum(ipcg.counts()))
     timed_scan_ms = list(scan_ms)
     if args.pmc_child:  # a counter pass of live_pmc: the counters are all it is for
         for h in handles:
@@ -672,9 +709,15 @@ def main():
     if world > 1 or args.shard_of > 1:
         got = None
         if world > 1 and rank == 0:
-            raw = (gathered[:nhits * HIT_BYTES] if comm is not None else last_gloo[0]).cpu().numpy()
+            if ipcg is not None:
+                raw = ipcg.hits([len(lens) * r for r in range(world)] if weak else None).cpu().numpy()
+            else:
+                raw = (gathered[:nhits * HIT_BYTES] if comm is not None else last_gloo[0]).cpu().numpy()
             got = np.frombuffer(raw.tobytes(), dtype=_native.HIT_DTYPE)
         dist_check = parity_distributed(table, genome, search, rng, got, world, rank, weak, len(lens), stream)
+    if ipcg is not None:  # every rank unmaps before rank 0's buffers go
+        ipcg.close()
+        torch.distributed.barrier()
     if rank != 0:
         if comm is not None:
             comm.close()
@@ -700,6 +743,9 @@ def main():
                 f"W={cfg['W']} N={cfg['N']} M={cfg['M']} I={cfg['I']}")
     if world > 1 and weak:
         workload += f" per rank ({world} contig sets, {tot_bases / 1e9:.3f} Gbp in all)"
+    gather_label = {"ipc": "hit gather: copy-engine puts into rank 0's HBM over xGMI",
+                    "rccl": "RCCL hit gatherv", "host": "hit gather through the host (gloo)"}.get(
+        gmode, f"N > 1 hit gather: --gather {args.gather}")
     from merpcr_amd._build import source_digest
     build = source_digest()
     # roofline.traffic / issue: counters measured now, in child passes of this very command;
@@ -734,8 +780,8 @@ def main():
         "config": {"workload": workload,
                    "sts": n_sts, "records": len(lens), "bases": int(bases), "W": cfg["W"], "N": cfg["N"],
                    "M": cfg["M"], "I": cfg["I"],
-                   "parallelism": (f"contig sets x{world} (one per rank, RCCL hit gatherv)" if weak
-                                   else f"owned (sequence, k) ranges x{world} of one genome (RCCL hit gatherv)")},
+                   "parallelism": (f"contig sets x{world} (one per rank, {gather_label})" if weak
+                                   else f"owned (sequence, k) ranges x{world} of one genome ({gather_label})")},
         "hits": int(tot_hits),
         "hits_per_s": round(tot_hits / t_step, 1),
         "scan_kernel_ms": round(kern_s * 1e3, 3),

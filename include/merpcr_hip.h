@@ -238,6 +238,24 @@ int mp_comm_gather_hits(void* comm, void* search, uint32_t seq_shift, mp_hit* de
                         uint64_t* n_total, void* stream);
 void mp_comm_destroy(void* comm);
 
+/* One node, one process per GPU, no kernel on the CUs: rank 0 exports its gather buffer and
+ * count words once (mp_ipc_handle, MP_IPC_HANDLE_BYTES each, shared out of band), every rank
+ * maps them (mp_ipc_open on its own device; rank 0 may use its pointers directly) and after
+ * each completed run mp_search_put_hits copies the run's hits into its region of that buffer
+ * and the count into its count word, on `stream`, by the copy engines
+ * (hipMemcpyDeviceToDeviceNoCU / host-to-device): a persistent scan holds every CU's LDS, so a
+ * collective's kernels (RCCL's need 37 KiB of LDS) would wait for the scan to end.  Regions
+ * are fixed: rank r owns [r * cap, (r + 1) * cap) entries; a sequence-index shift (contig
+ * shards) is the reader's.  MP_E_CAP: more hits than cap (nothing copied).  Not collective;
+ * completion is the stream's. */
+#define MP_IPC_HANDLE_BYTES 64
+/* The handle names dev_ptr's whole allocation; *offset = dev_ptr - its base.  mp_ipc_open
+ * returns the base as mapped here: add the offset. */
+int mp_ipc_handle(void* dev_ptr, uint8_t* handle64, uint64_t* offset);
+int mp_ipc_open(const uint8_t* handle64, int32_t device, void** base_out);
+int mp_ipc_close(void* dev_ptr);
+int mp_search_put_hits(void* search, mp_hit* dst, uint64_t cap, uint64_t* count_dst, void* stream);
+
 /* ---- FASTA input (replaces FASTALoader.load_file, src/merpcr/io/fasta.py:18-71) --
  * Reads `path` as the reference's text-mode loop does: strict UTF-8, universal
  * newlines, Python str.strip() whitespace, '>' headers (defline = stripped line),

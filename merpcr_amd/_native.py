@@ -38,6 +38,7 @@ EXPORTS = (
     "mp_multi_create", "mp_multi_genome", "mp_multi_put", "mp_multi_seal", "mp_multi_run", "mp_multi_fetch",
     "mp_multi_device_search", "mp_multi_timing", "mp_multi_destroy",
     "mp_comm_unique_id", "mp_comm_create", "mp_comm_gather_hits", "mp_comm_destroy",
+    "mp_ipc_handle", "mp_ipc_open", "mp_ipc_close", "mp_search_put_hits",
     "mp_fasta_load", "mp_fasta_load_parallel", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record_ascii", "mp_fasta_record", "mp_fasta_destroy",
     "mp_fasta_load_device", "mp_fasta_device_info", "mp_fasta_device_record", "mp_fasta_device_read",
     "mp_fasta_device_destroy",
@@ -150,6 +151,10 @@ def _sig(lib):
     lib.mp_comm_gather_hits.argtypes = [P, P, c_uint32, P, c_uint64, u64p, P]
     lib.mp_comm_destroy.argtypes = [P]
     lib.mp_comm_destroy.restype = None
+    lib.mp_ipc_handle.argtypes = [P, P, u64p]
+    lib.mp_ipc_open.argtypes = [P, c_int32, POINTER(c_void_p)]
+    lib.mp_ipc_close.argtypes = [P]
+    lib.mp_search_put_hits.argtypes = [P, P, c_uint64, P, P]
     lib.mp_fasta_load.argtypes = [c_char_p, POINTER(c_void_p)]
     lib.mp_fasta_load_chunked.argtypes = [c_char_p, c_uint64, POINTER(c_void_p)]
     lib.mp_fasta_load_parallel.argtypes = [c_char_p, c_int32, POINTER(c_void_p)]
@@ -408,6 +413,12 @@ class Search:
         """Copy the last run's hits into device memory at dev_ptr (cap entries)."""
         check(lib().mp_search_fetch_device(self._h, c_void_p(dev_ptr), cap, c_void_p(stream or 0)))
 
+    def put_hits(self, dst: int, cap: int, count_dst: int, stream=None):
+        """The last run's hits into dst (cap entries; another rank's buffer mapped by ipc_open
+        on one node) and their count into the u64 at count_dst, by the copy engines on
+        `stream` (mp_search_put_hits)."""
+        check(lib().mp_search_put_hits(self._h, c_void_p(dst), cap, c_void_p(count_dst), c_void_p(stream or 0)))
+
     def device_hits(self) -> int:
         p = c_void_p()
         check(lib().mp_search_device_hits(self._h, ctypes.byref(p)))
@@ -501,6 +512,31 @@ class Multi:
             self.close()
         except Exception:
             pass
+
+
+IPC_HANDLE_BYTES = 64
+
+
+def ipc_handle(dev_ptr: int):
+    """Export the device allocation holding dev_ptr to the other processes of the node
+    (mp_ipc_handle): (handle bytes, dev_ptr's offset in the allocation)."""
+    buf = (ctypes.c_uint8 * IPC_HANDLE_BYTES)()
+    off = c_uint64(0)
+    check(lib().mp_ipc_handle(c_void_p(dev_ptr), buf, ctypes.byref(off)))
+    return bytes(buf), off.value
+
+
+def ipc_open(handle: bytes, device: int) -> int:
+    """Map another process's exported allocation on `device`; returns its base address here
+    (add the exporter's offset)."""
+    b = (ctypes.c_uint8 * IPC_HANDLE_BYTES).from_buffer_copy(handle)
+    p = c_void_p()
+    check(lib().mp_ipc_open(b, device, ctypes.byref(p)))
+    return p.value or 0
+
+
+def ipc_close(dev_ptr: int):
+    check(lib().mp_ipc_close(c_void_p(dev_ptr)))
 
 
 def comm_unique_id() -> bytes:

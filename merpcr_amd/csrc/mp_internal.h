@@ -273,6 +273,8 @@ struct Search {
     unsigned long long* h_cnt = nullptr;
     unsigned long long* d_hcnt = nullptr;   // h_cnt as the device sees it
     hipEvent_t evd = nullptr;               // the run's completion (polled, not slept on)
+    unsigned long long* h_put = nullptr;    // mp_search_put_hits: pinned ring of hit counts in flight
+    uint32_t put_seq = 0;
     bool stage_timing = true;               // events around tail/pair/order too (mp_search_set_stage_timing)
     bool scan_timing = true;                // the scan kernel's own two events (mp_search_set_scan_timing)
     bool dirty = false;                     // counters not known to be zero (an abandoned run): memset first

@@ -470,3 +470,53 @@ MP_EXPORT void mp_comm_destroy(void* comm) {
     if (c->c) ncclCommDestroy(c->c);
     delete c;
 }
+
+// ---- hit gather by the copy engines (one node; include/merpcr_hip.h)
+static_assert(sizeof(hipIpcMemHandle_t) == MP_IPC_HANDLE_BYTES, "IPC handle size");
+
+MP_EXPORT int mp_ipc_handle(void* dev_ptr, uint8_t* handle64, uint64_t* offset) {
+    if (!dev_ptr || !handle64 || !offset) return fail(MP_E_ARG, "mp_ipc_handle: null pointer");
+    // the handle names the whole allocation (a caching allocator's block may hold several
+    // buffers): the importer maps its base and adds dev_ptr's offset in it
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    MP_HIP_CHECK(hipMemGetAddressRange(&base, &size, dev_ptr));
+    *offset = (uint64_t)((const char*)dev_ptr - (const char*)base);
+    hipIpcMemHandle_t h;
+    MP_HIP_CHECK(hipIpcGetMemHandle(&h, dev_ptr));
+    std::memcpy(handle64, &h, sizeof(h));
+    return MP_OK;
+}
+
+MP_EXPORT int mp_ipc_open(const uint8_t* handle64, int32_t device, void** dev_ptr_out) {  // the allocation's base
+    if (!handle64 || !dev_ptr_out) return fail(MP_E_ARG, "mp_ipc_open: null pointer");
+    *dev_ptr_out = nullptr;
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle64, sizeof(h));
+    MP_HIP_CHECK(hipSetDevice(device));
+    MP_HIP_CHECK(hipIpcOpenMemHandle(dev_ptr_out, h, hipIpcMemLazyEnablePeerAccess));
+    return MP_OK;
+}
+
+MP_EXPORT int mp_ipc_close(void* dev_ptr) {
+    if (!dev_ptr) return fail(MP_E_ARG, "mp_ipc_close: null pointer");
+    MP_HIP_CHECK(hipIpcCloseMemHandle(dev_ptr));
+    return MP_OK;
+}
+
+MP_EXPORT int mp_search_put_hits(void* search, mp_hit* dst, uint64_t cap, uint64_t* count_dst, void* stream) {
+    Search* s = (Search*)search;
+    if (!s || !count_dst || (s->n_hits && !dst)) return fail(MP_E_ARG, "mp_search_put_hits: null pointer");
+    if (s->pending) return fail(MP_E_STATE, "mp_search_put_hits: a run is enqueued (mp_search_complete first)");
+    if (s->n_hits > cap) return fail(MP_E_CAP, "mp_search_put_hits: region too small");
+    hipStream_t st = (hipStream_t)stream;
+    MP_HIP_CHECK(hipSetDevice(s->genome->device));
+    constexpr uint32_t kPutRing = 64;  // counts in flight (a handle has at most one put queued)
+    if (!s->h_put) MP_HIP_CHECK(hipHostMalloc((void**)&s->h_put, kPutRing * sizeof(unsigned long long), hipHostMallocDefault));
+    const uint64_t n = s->n_hits;
+    if (n) MP_HIP_CHECK(hipMemcpyAsync(dst, s->out, n * sizeof(mp_hit), hipMemcpyDeviceToDeviceNoCU, st));
+    unsigned long long* c = s->h_put + (s->put_seq++ % kPutRing);
+    *c = n;
+    MP_HIP_CHECK(hipMemcpyAsync(count_dst, c, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    return MP_OK;
+}

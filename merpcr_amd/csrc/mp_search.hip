@@ -2520,6 +2520,7 @@ static void free_search(Search* s) {
     if (s->evt) hipEventDestroy(s->evt);
     if (s->evd) hipEventDestroy(s->evd);
     if (s->h_cnt) hipHostFree(s->h_cnt);
+    if (s->h_put) hipHostFree(s->h_put);
     delete s;
 }
 

@@ -82,6 +82,77 @@ def native_comm(device: int, group=None):
     return Comm(obj[0], world, rank, device)
 
 
+class IpcGather:
+    """Hit gather to rank 0 by the copy engines, for one process per GPU on one node.
+
+    Rank 0 allocates ``world`` fixed regions of ``cap`` hits (the largest any rank asks for)
+    and ``world`` count words in its
+    HBM and exports both (mp_ipc_handle); torch.distributed (any backend: the control plane)
+    carries the handles; every other rank maps them on its own device (mp_ipc_open).  After a
+    completed run, ``put`` copies the run's hits into this rank's region and its count into
+    this rank's word on the given stream (mp_search_put_hits: no kernel on the CUs, no
+    collective, no host synchronisation between ranks).  After the ranks' streams are
+    synchronised and a barrier, rank 0's ``hits()`` is the rank-ordered concatenation (the
+    contig-shard sequence shift applied there, so no rank's own list is modified).
+    Collective to create (every rank), like the RCCL communicator it stands beside."""
+
+    def __init__(self, device: int, cap: int, group=None):
+        import torch
+        import torch.distributed as dist
+        from . import _native
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        caps = [None] * self.world  # one region size for every rank: the largest asked for
+        dist.all_gather_object(caps, int(cap), group=group)
+        self.cap = max(caps)
+        self._opened = []
+        self._buf = self._cnt = None
+        if self.rank == 0:
+            dev = torch.device("cuda", device)
+            self._buf = torch.empty(self.world * self.cap * HIT_BYTES, dtype=torch.uint8, device=dev)
+            self._cnt = torch.zeros(self.world, dtype=torch.int64, device=dev)
+            obj = [(_native.ipc_handle(self._buf.data_ptr()), _native.ipc_handle(self._cnt.data_ptr()))]
+        else:
+            obj = [None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        if self.rank == 0:
+            base, cnt = self._buf.data_ptr(), self._cnt.data_ptr()
+        else:  # each handle maps its whole allocation: add the tensor's offset in it
+            (hb, ob), (hc, oc) = obj[0]
+            mb = _native.ipc_open(hb, device)
+            self._opened.append(mb)
+            mc = _native.ipc_open(hc, device)
+            self._opened.append(mc)
+            base, cnt = mb + ob, mc + oc
+        self.region = base + self.rank * self.cap * HIT_BYTES
+        self.count = cnt + self.rank * 8
+
+    def put(self, search, stream=None):
+        search.put_hits(self.region, self.cap, self.count, stream)
+
+    def hits(self, seq_shifts=None):
+        """Rank 0: the rank-ordered hit bytes (a torch uint8 tensor on its device), rank r's
+        sequence indices plus seq_shifts[r] (contig shards)."""
+        import torch
+        n = self._cnt.cpu().tolist()
+        parts = []
+        for r in range(self.world):
+            part = self._buf[r * self.cap * HIT_BYTES:(r * self.cap + n[r]) * HIT_BYTES].clone()
+            if seq_shifts and seq_shifts[r] and n[r]:
+                # mp_hit = {u64 pos1, u64 pos2, u32 seq, u32 rec}: seq is int32 word 4 of 6
+                part.view(torch.int32).view(n[r], HIT_BYTES // 4)[:, 4] += int(seq_shifts[r])
+            parts.append(part)
+        return torch.cat(parts)
+
+    def counts(self):
+        return self._cnt.cpu().tolist() if self._cnt is not None else None
+
+    def close(self):
+        from . import _native
+        for p in self._opened:
+            _native.ipc_close(p)
+        self._opened = []
+
+
 def gather_hits(local, n_local: int, group=None, dst: int = 0, seq_base: int = 0) -> Optional[object]:
     """Gather per-rank hit byte buffers (torch uint8 tensors) to rank ``dst``.
 

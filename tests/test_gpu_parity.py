@@ -660,6 +660,74 @@ def _two_rank_worker(rank, world, port, sts_text, seqs, q):
     dist.destroy_process_group()
 
 
+def _two_rank_ipc_worker(rank, world, port, sts_text, seqs, q, steps):
+    """One rank of the copy-engine gather (merpcr_amd.dist.IpcGather): `steps` runs of its
+    owned range, each put into rank 0's region on the run's stream, as bench.py does."""
+    import torch
+    import torch.distributed as dist
+    from merpcr_amd import _native
+    from merpcr_amd.dist import IpcGather, shard_ranges
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    eng = MerPCR(wordsize=11, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    data = eng.encode_sequences(seqs)
+    genome = _native.Genome(0, [len(d) for d in data])
+    for i, d in enumerate(data):
+        if len(d):
+            genome.put(i, d)
+    genome.seal()
+    s = _native.Search(eng.device_table(), genome)
+    rng = shard_ranges([len(d) for d in data], world)[rank]
+    n = s.run(rng)
+    g = IpcGather(0, max(64, 2 * n))
+    st = torch.cuda.Stream()
+    for _ in range(steps):
+        s.enqueue(rng, st.cuda_stream)
+        s.complete()
+        g.put(s, st.cuda_stream)
+    st.synchronize()
+    dist.barrier()
+    if rank == 0:
+        q.put((g.counts(), g.hits().cpu().numpy().tobytes()))
+    g.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_ipc_gather_on_one_gpu():
+    """bench.py's default N > 1 gather (copy-engine puts into rank 0's regions, mapped by IPC
+    in the other process): two processes on cuda:0, three pipelined-style steps each; rank 0's
+    rank-ordered regions equal the whole-genome HIP list and the C oracle's."""
+    import socket
+    import torch.multiprocessing as tmp
+    from oracle import c_oracle as C
+    sts_text, seqs = _multi_case(11, 3000, 45)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_two_rank_ipc_worker, args=(r, 2, port, sts_text, seqs, q, 3)) for r in range(2)]
+    for p in procs:
+        p.start()
+    counts, got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    eng = MerPCR(wordsize=11, mismatches=1)
+    with tempfile.TemporaryDirectory() as td:
+        assert _load_sts(eng, sts_text, td)
+    whole = eng.find_hits([FASTARecord(defline=f">m{i}", sequence=x) for i, x in enumerate(seqs)])
+    table = O.load_sts_lines(sts_text.splitlines(True), 11, 240)
+    ref = C.search(table, [np.frombuffer(x.encode(), dtype=np.uint8) for x in seqs], O.params(wordsize=11, mismatches=1), 8)
+    assert len(whole) > 100 and sum(counts) == len(whole) and min(counts) > 0
+    assert got == whole.tobytes() == ref.tobytes()
+    assert all(p.exitcode == 0 for p in procs)
+
+
 def test_two_ranks_on_one_gpu():
     """Two processes on cuda:0, each searching its owned range with the HIP path, gathered
     over torch.distributed (gloo: RCCL does not admit two ranks on one GPU); the gathered
