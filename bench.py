@@ -534,8 +534,13 @@ def main():
         err = None
         try:
             ipcg = IpcGather(local, max(4096, 2 * max(every)))
+            ipcg.put(search, stream)  # a probe put of that run: the copy engines reach rank 0's HBM
+            torch.cuda.synchronize()
         except Exception as e:  # noqa: BLE001 (reported, then every rank takes the same fallback)
             err = f"{type(e).__name__}: {e}"
+        dist.barrier()
+        if err is None and rank == 0 and ipcg.counts() != every:
+            err = f"probe put: rank 0 read counts {ipcg.counts()}, the ranks wrote {every}"
         errs = [None] * world
         dist.all_gather_object(errs, err)
         if any(errs):
