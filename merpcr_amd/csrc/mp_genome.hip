@@ -207,7 +207,7 @@ __global__ void run_dir_kernel(const uint64_t* __restrict__ xr_start, uint64_t n
 static void free_genome(Genome* g) {
     if (!g) return;
     hipFree(g->xr_dir); hipFree(g->d_ucount);
-    hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv); hipFree(g->gwild); hipFree(g->d_base); hipFree(g->d_len);
+    hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv); hipFree(g->gwild); hipFree(g->gpair); hipFree(g->d_base); hipFree(g->d_len);
     hipFree(g->xr_start); hipFree(g->xr_char); hipFree(g->d_counter); hipFree(g->staging);
     delete g;
 }
@@ -289,11 +289,12 @@ static int place(Genome* g) {
     const uint64_t off = g->total;
     const uint64_t w2 = off / 32 + 4, w1 = off / 64 + 4;
     if (off > g->plane_cap || !g->g2) {
-        hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv); hipFree(g->gwild);
-        g->g2 = g->gexc = g->ginv = g->gwild = nullptr;
+        hipFree(g->g2); hipFree(g->gexc); hipFree(g->ginv); hipFree(g->gwild); hipFree(g->gpair);
+        g->g2 = g->gexc = g->ginv = g->gwild = g->gpair = nullptr;
         g->plane_cap = 0;
         if (hipMalloc(&g->g2, w2 * 8) != hipSuccess || hipMalloc(&g->gexc, w1 * 8) != hipSuccess ||
-            hipMalloc(&g->ginv, w1 * 8) != hipSuccess || hipMalloc(&g->gwild, w1 * 8) != hipSuccess)
+            hipMalloc(&g->ginv, w1 * 8) != hipSuccess || hipMalloc(&g->gwild, w1 * 8) != hipSuccess ||
+            hipMalloc(&g->gpair, w1 * 32) != hipSuccess)
             return fail(MP_E_NOMEM, "mp_genome: device allocation failed");
         g->plane_cap = off;
     }
@@ -308,7 +309,8 @@ static int place(Genome* g) {
     }
     if (!g->d_counter && (hipMalloc(&g->d_counter, 64) != hipSuccess || hipMalloc(&g->d_ucount, 64) != hipSuccess))
         return fail(MP_E_NOMEM, "mp_genome: device allocation failed");
-    g->dev_bytes = (g->plane_cap / 32 + 4) * 8 + 3 * (g->plane_cap / 64 + 4) * 8 + g->xr_cap * 9;
+    g->dev_bytes = (g->plane_cap / 32 + 4) * 8 + 3 * (g->plane_cap / 64 + 4) * 8 + (g->plane_cap / 64 + 4) * 32 +
+                   g->xr_cap * 9;
     if (hipMemset(g->d_ucount, 0, 64) != hipSuccess || hipMemset(g->g2, 0, w2 * 8) != hipSuccess ||
         hipMemset(g->gexc, 0xFF, w1 * 8) != hipSuccess || hipMemset(g->ginv, 0xFF, w1 * 8) != hipSuccess ||
         hipMemset(g->gwild, 0, w1 * 8) != hipSuccess)
@@ -379,6 +381,15 @@ MP_EXPORT int mp_genome_put(void* genome, uint32_t seq, uint64_t offset, const u
     return MP_OK;
 }
 
+// Genome::gpair from the planes: block b = {g2[2b], g2[2b + 1], gexc[b], gwild[b]}
+__global__ void interleave_pair_kernel(const uint64_t* __restrict__ g2, const uint64_t* __restrict__ gexc,
+                                       const uint64_t* __restrict__ gwild, uint64_t* __restrict__ out, uint64_t nb) {
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+        reinterpret_cast<ulonglong2*>(out)[2 * b] = make_ulonglong2(g2[2 * b], g2[2 * b + 1]);
+        reinterpret_cast<ulonglong2*>(out)[2 * b + 1] = make_ulonglong2(gexc[b], gwild[b]);
+    }
+}
+
 MP_EXPORT int mp_genome_seal(void* genome, void* stream) {
     Genome* g = (Genome*)genome;
     if (!g) return fail(MP_E_ARG, "mp_genome_seal: null genome");
@@ -395,6 +406,12 @@ MP_EXPORT int mp_genome_seal(void* genome, void* stream) {
     hipLaunchKernelGGL(run_dir_kernel, dim3((uint32_t)((g->n_dir + 255) / 256)), dim3(256), 0, st, g->xr_start,
                        g->n_xr, g->xr_dir, g->n_dir);
     MP_HIP_CHECK(hipGetLastError());
+    {
+        const uint64_t nb = g->total / 64 + 2;  // every block a stretch read can reach (g2 holds total / 32 + 4 words)
+        hipLaunchKernelGGL(interleave_pair_kernel, dim3((uint32_t)std::min<uint64_t>((nb + 255) / 256, 8192)), dim3(256), 0, st,
+                           g->g2, g->gexc, g->gwild, g->gpair, nb);
+        MP_HIP_CHECK(hipGetLastError());
+    }
     unsigned long long nu = 0;
     MP_HIP_CHECK(hipMemcpyAsync(&nu, g->d_ucount, sizeof(nu), hipMemcpyDeviceToHost, st));
     MP_HIP_CHECK(hipStreamSynchronize(st));

@@ -211,6 +211,11 @@ struct Genome {
     uint64_t* g2 = nullptr;
     uint64_t* gexc = nullptr;
     uint64_t* gwild = nullptr;                // 'N' bases (pair check under I = 1: they match any primer base)
+    // The pair check's planes interleaved (round 5, built at seal): per 64-base block b the
+    // 32 B {g2 word 2b, g2 word 2b + 1, gexc word b, gwild word b}, so a survivor's stretch
+    // of ~130 bases is one or two 128-B lines instead of one or two per plane (c4's pair
+    // kernel fetched ~1.6 GB per launch, ~580 B per survivor).
+    uint64_t* gpair = nullptr;
     uint64_t* ginv = nullptr;
     uint64_t* d_base = nullptr;
     uint64_t* d_len = nullptr;
@@ -294,6 +299,25 @@ __device__ __forceinline__ uint64_t ext2(const uint64_t* __restrict__ p, uint64_
     const uint32_t s = (uint32_t)(j & 31) * 2;
     const uint64_t a = p[w];
     const uint64_t b = p[w + 1];
+    return s ? (a << s) | (b >> (64 - s)) : a;
+}
+
+// Genome::gpair words: 2-bit word w, exception / 'N' word e.
+__device__ __forceinline__ uint64_t gp_g2(const uint64_t* __restrict__ p, uint64_t w) { return p[((w >> 1) << 2) | (w & 1)]; }
+__device__ __forceinline__ uint64_t gp_exc(const uint64_t* __restrict__ p, uint64_t e) { return p[(e << 2) | 2]; }
+__device__ __forceinline__ uint64_t gp_wild(const uint64_t* __restrict__ p, uint64_t e) { return p[(e << 2) | 3]; }
+// ext2 / ext1 over Genome::gpair (kPlane 2: gexc, 3: gwild)
+__device__ __forceinline__ uint64_t ext2p(const uint64_t* __restrict__ p, uint64_t j) {
+    const uint64_t w = j >> 5;
+    const uint32_t s = (uint32_t)(j & 31) * 2;
+    const uint64_t a = gp_g2(p, w), b = gp_g2(p, w + 1);
+    return s ? (a << s) | (b >> (64 - s)) : a;
+}
+template <int kPlane>
+__device__ __forceinline__ uint64_t ext1p(const uint64_t* __restrict__ p, uint64_t j) {
+    const uint64_t w = j >> 6;
+    const uint32_t s = (uint32_t)(j & 63);
+    const uint64_t a = p[(w << 2) | kPlane], b = p[((w + 1) << 2) | kPlane];
     return s ? (a << s) | (b >> (64 - s)) : a;
 }
 

@@ -44,6 +44,7 @@ struct ScanArgs {
     const uint64_t* gexc;
     const uint64_t* ginv;
     const uint64_t* gwild;  // 'N' bases: under I = 1 they match every primer base with an IUPAC meaning
+    const uint64_t* gpair;  // the pair check's planes interleaved (Genome::gpair)
     const uint64_t* xr_start;
     const uint8_t* xr_char;
     const uint32_t* xr_dir;
@@ -285,9 +286,9 @@ __device__ __forceinline__ bool primer_ok(const ScanArgs& a, uint64_t gpos, uint
     int mm = 0;
     for (uint32_t c = 0; c < L; c += 32) {
         const int len = (int)min(32u, L - c);
-        const uint64_t G = ext2(a.g2, gpos + c);
-        const uint32_t ex = (uint32_t)(ext1(a.gexc, gpos + c) >> 32);
-        const uint32_t wl = a.I && ex ? (uint32_t)(ext1(a.gwild, gpos + c) >> 32) : 0u;
+        const uint64_t G = ext2p(a.gpair, gpos + c);  // the interleaved planes: one line, not three
+        const uint32_t ex = (uint32_t)(ext1p<2>(a.gpair, gpos + c) >> 32);
+        const uint32_t wl = a.I && ex ? (uint32_t)(ext1p<3>(a.gpair, gpos + c) >> 32) : 0u;
         // chunk 0's planes from the record's pair line (q0) when given
         const uint64_t* P = c == 0 && q0 ? q0 : a.planes + (uint64_t)(pl + (c >> 5)) * 4;
         if (!chunk_ok(a, G, ex, P[0], P[1], P[2], P[3], gpos + c, ch + c, len, c, L, plus, mm, wl)) return false;
@@ -472,7 +473,7 @@ __device__ void pair_check_lanes(const ScanArgs& a, uint4 v, uint32_t batch, int
         fast = keep && r.l2 <= 32u && wl - w0 < (uint64_t)kPW && el - e0 < (uint64_t)kPE;
         if (fast) {
 #pragma unroll
-            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? a.g2[w0 + t] : 0ull;
+            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? gp_g2(a.gpair, w0 + t) : 0ull;
             // exception bits of the stretch [P0l, lastl] (at most 4 words of 64 bases).  Under
             // I = 1 an 'N' matches every primer base with an IUPAC meaning (char_match,
             // engine.py:613-631) -- exactly the positions with an accept-plane bit -- so the
@@ -482,9 +483,9 @@ __device__ void pair_check_lanes(const ScanArgs& a, uint4 v, uint32_t batch, int
 #pragma unroll
             for (int t = 0; t < kPE; ++t) {
                 const bool in = e0 + t <= el;
-                ew[t] = in ? a.gexc[e0 + t] : 0ull;
+                ew[t] = in ? gp_exc(a.gpair, e0 + t) : 0ull;
                 if (a.I) {
-                    const uint64_t wd = in ? a.gwild[e0 + t] : 0ull;
+                    const uint64_t wd = in ? gp_wild(a.gpair, e0 + t) : 0ull;
                     ew[t] &= ~wd;
                     pst[(kPW + t) * MP_PBATCH + lane] = wd;
                 } else {
@@ -3138,7 +3139,7 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         }
         ScanArgs& a = *reinterpret_cast<ScanArgs*>(s->pend_args);
         a = ScanArgs{};
-        a.g2 = g->g2; a.gexc = g->gexc; a.ginv = g->ginv; a.gwild = g->gwild;
+        a.g2 = g->g2; a.gexc = g->gexc; a.ginv = g->ginv; a.gwild = g->gwild; a.gpair = g->gpair;
         a.xr_start = g->xr_start; a.xr_char = g->xr_char; a.xr_dir = g->xr_dir; a.n_xr = g->n_xr;
         a.has_u = g->has_u ? 1 : 0;
         a.seq_base = g->d_base; a.seq_len = g->d_len;
