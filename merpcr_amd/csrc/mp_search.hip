@@ -2240,6 +2240,13 @@ __device__ __forceinline__ void tail_flush(const ScanArgs& a, uint4* buf, uint32
     __syncthreads();
 }
 
+// The seed key of a 16-B key reference v (ref16_make: the window at the seed in v.z, v.w).
+template <bool kGap>
+__device__ __forceinline__ uint32_t ref16_key(const ScanArgs& a, const uint4& v) {
+    const uint32_t W = (uint32_t)a.W;
+    return kGap ? gap_key(v.w, a.gap_at, a.gap_len) >> (32u - 2u * W) : v.w >> (32u - 2u * W);
+}
+
 // kGap: the references of a gapped seed scan (split tables): the key is the gapped one, and a
 // window whose gap matches the record exactly is left to the contiguous seed's scan.
 // One reference per thread.  (Round 4 measured two and four per thread with their head loads
@@ -2257,6 +2264,10 @@ constexpr uint32_t kTailBPC = MP_TAIL_BPC;  // blocks per CU
 #define MP_TAIL_CHECK 16
 #endif
 constexpr uint32_t kTailCheck = MP_TAIL_CHECK;
+#ifndef MP_TAIL_PREFETCH
+#define MP_TAIL_PREFETCH 1
+#endif
+constexpr bool kTailPrefetch = MP_TAIL_PREFETCH != 0;  // the next pass's 16-B reference and rank word in flight
 // kH12: the table has wide key groups (kgrp4), whose key references read the 8-B IUPAC heads
 // kRef16: the references are in the 16-B form (ScanArgs::ref16).
 template <bool kGap = false, bool kH12 = false, bool kRef16 = false>
@@ -2275,13 +2286,31 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     const uint2* kref_heads = kH12 ? a.dents12 : a.dents8;
     const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
     uint32_t it = 0, next_check = 0, period = 1, fill0 = 0;  // buffer checks (block-uniform)
+    // 16-B references: the next pass's reference is loaded at the top of this pass, so its
+    // latency hides behind this pass's dependent loads (rank word, head, entries)
+    // and the reference's rank word is loaded at the end of the pass before (one dependent
+    // load fewer on each pass's chain)
+    uint4 vnext = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+    uint2 rwnext = make_uint2(0u, 0u);
+    if (kRef16 && kTailPrefetch && (uint64_t)blockIdx.x * kTailBlock + threadIdx.x < n_refs) {
+        vnext = a.tails[(uint64_t)blockIdx.x * kTailBlock + threadIdx.x];
+        if (!(vnext.x == 0xFFFFFFFFu && vnext.y == 0xFFFFFFFFu)) rwnext = a.rk[ref16_key<kGap>(a, vnext) >> 5];
+    }
     for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride, ++it) {  // block-uniform
         const uint64_t i = b + threadIdx.x;
         uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
+        uint2 rwpre = make_uint2(0u, 0u);  // the rank word of v, loaded the pass before
         if (kRef16) {
             // 16-B key reference (ref16_make) -> the 32-B form's fields: the bases left from the
             // sequence tables, the window's exception bits from the genome when flagged
-            if (i < n_refs) v = a.tails[i];
+            if constexpr (kTailPrefetch) {
+                v = vnext;
+                rwpre = rwnext;
+                vnext = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+                if (i + stride < n_refs) vnext = a.tails[i + stride];
+            } else if (i < n_refs) {
+                v = a.tails[i];
+            }
             if (!(v.x == 0xFFFFFFFFu && v.y == 0xFFFFFFFFu)) {
                 const uint64_t gp = (uint64_t)v.x | ((uint64_t)(v.y & 0xFFu) << 32);
                 const uint32_t seq = v.y >> 9;
@@ -2305,7 +2334,7 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 const uint32_t W = (uint32_t)a.W;
                 const uint32_t h = kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
                                         : (uint32_t)(Gs >> (64u - 2u * W));
-                const uint2 rw = a.rk[h >> 5];
+                const uint2 rw = (kRef16 && kTailPrefetch) ? rwpre : a.rk[h >> 5];
                 const uint2 c = kref_heads[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
                 if (c.y & kHead8Full) {
                     first = c.x;  // the bucket's first entry
@@ -2365,6 +2394,8 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 }
             }
         }
+        if (kRef16 && kTailPrefetch && !(vnext.x == 0xFFFFFFFFu && vnext.y == 0xFFFFFFFFu))
+            rwnext = a.rk[ref16_key<kGap>(a, vnext) >> 5];
         // The buffer's fill is read by every thread between two barriers at a check, and the
         // waves run free between checks.  The next check comes after as many passes as the
         // buffer's free half holds at the survivor rate since the last one (1..kTailCheck): c4's
