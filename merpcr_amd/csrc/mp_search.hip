@@ -1364,7 +1364,11 @@ __device__ __forceinline__ uint32_t lds_probe32(const uint32_t* __restrict__ lds
                     static_assert(kLdsFilterLog2 - 5 <= 2 * (int)kGapW8At && kShw + 5 <= 2 * kGapW8At,
                                   "word index inside the ungapped bases, second bit below them");
                     const uint32_t wv = lds[x >> (37 - kLdsFilterLog2)];
-                    const uint32_t b1 = (((x & 0xFFFF0000u) | ((x << (2 * kGapW8Len)) & 0xFFFFu)) >> (32 - kLdsFilterLog2)) & 31u;
+                    // g's bits 16..12 are x's bit 16 and bits 9..6: ubfe reads only the offset's low
+                    // five bits, so the bit-field insert of the two shifts is the whole index
+                    // (three instructions where the masked assembly of g took four)
+                    static_assert(kLdsFilterLog2 == 20 && kGapW8Len == 3, "b1 = x16 ++ x9..6");
+                    const uint32_t b1 = ((x >> 6) & 15u) | ((x >> 12) & ~15u);
                     uint32_t on = __builtin_amdgcn_ubfe(wv, b1, 1u);
                     if constexpr (kK >= 2) on &= __builtin_amdgcn_ubfe(wv, (x >> (kShw - 2 * kGapW8Len)) & 31u, 1u);
                     static_assert(kK <= 2, "the W = 8 gapped form takes one or two bits per key");
