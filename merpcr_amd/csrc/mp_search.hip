@@ -411,6 +411,7 @@ __device__ __forceinline__ void stage_try_hit(const ScanArgs& a, HitStage& S, in
 // words (I = 1) and the four primer-2 accept planes, [slot][survivor] in the wave's LDS.
 // At M=50 and primers of <= 25 bases every survivor fits (the tries span <= 125 bases).
 constexpr int kPW = 6, kPE = 4, kPSlots = kPW + kPE + 4;
+static_assert(kPW + 1 < 2 * kPE, "staged 2-bit words lie in the staged 64-base blocks");
 static_assert(MP_PBATCH <= 64, "pair-check batch is one survivor per lane");
 
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int j) { return (uint32_t)__builtin_amdgcn_readlane((int)v, j); }
@@ -472,26 +473,38 @@ __device__ void pair_check_lanes(const ScanArgs& a, uint4 v, uint32_t batch, int
         const uint64_t wl = (lastl >> 5) + 1, el = (lastl >> 6) + 1;  // last words any try reads
         fast = keep && r.l2 <= 32u && wl - w0 < (uint64_t)kPW && el - e0 < (uint64_t)kPE;
         if (fast) {
-#pragma unroll
-            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? gp_g2(a.gpair, w0 + t) : 0ull;
             // exception bits of the stretch [P0l, lastl] (at most 4 words of 64 bases).  Under
             // I = 1 an 'N' matches every primer base with an IUPAC meaning (char_match,
             // engine.py:613-631) -- exactly the positions with an accept-plane bit -- so the
             // lane-parallel tries take 'N' as a wildcard from the staged 'N' words, and only
             // the other exception characters make a stretch unclean
             uint64_t ew[kPE];
+            // whole 32-B gpair blocks e0..el, two 16-B loads each: 2-bit words 2b, 2b+1, then the
+            // exception and 'N' words (word w0 is in block e0).  Round 5: one 16-B load per two
+            // words instead of one 8-B load per word (up to 14 loads per lane -> 8): c4 pair
+            // 0.387 -> 0.342 ms, c3 0.079 -> 0.074 ms (`gpurun_out/pblk_*`)
+            uint64_t g2w[2 * kPE];
+            const ulonglong2* gq = reinterpret_cast<const ulonglong2*>(a.gpair);
 #pragma unroll
             for (int t = 0; t < kPE; ++t) {
-                const bool in = e0 + t <= el;
-                ew[t] = in ? gp_exc(a.gpair, e0 + t) : 0ull;
+                ulonglong2 q0 = make_ulonglong2(0ull, 0ull), q1 = q0;
+                if (e0 + t <= el) {
+                    q0 = gq[2 * (e0 + t)];
+                    q1 = gq[2 * (e0 + t) + 1];
+                }
+                g2w[2 * t] = q0.x;
+                g2w[2 * t + 1] = q0.y;
+                ew[t] = q1.x;
                 if (a.I) {
-                    const uint64_t wd = in ? gp_wild(a.gpair, e0 + t) : 0ull;
-                    ew[t] &= ~wd;
-                    pst[(kPW + t) * MP_PBATCH + lane] = wd;
+                    ew[t] &= ~q1.y;
+                    pst[(kPW + t) * MP_PBATCH + lane] = q1.y;
                 } else {
                     pst[(kPW + t) * MP_PBATCH + lane] = ew[t];
                 }
             }
+            const bool odd = (w0 & 1u) != 0u;
+#pragma unroll
+            for (int t = 0; t < kPW; ++t) pst[t * MP_PBATCH + lane] = w0 + t <= wl ? (odd ? g2w[t + 1] : g2w[t]) : 0ull;
             const uint32_t f0 = (uint32_t)(P0l & 63), f1 = (uint32_t)(lastl - (e0 << 6));  // stretch bits in word order
             uint64_t any = 0;
 #pragma unroll
