@@ -482,13 +482,15 @@ __device__ void pair_check_lanes(const ScanArgs& a, uint4 v, uint32_t batch, int
             // whole 32-B gpair blocks e0..el, two 16-B loads each: 2-bit words 2b, 2b+1, then the
             // exception and 'N' words (word w0 is in block e0).  Round 5: one 16-B load per two
             // words instead of one 8-B load per word (up to 14 loads per lane -> 8): c4 pair
-            // 0.387 -> 0.342 ms, c3 0.079 -> 0.074 ms (`gpurun_out/pblk_*`)
+            // 0.387 -> 0.342 ms, c3 0.079 -> 0.074 ms (`gpurun_out/pblk_*`).  Block el holds
+            // no stretch base, only (when wl is its first word) a try's last 2-bit word and
+            // its 'N' bits: loaded only then, c4 pair 0.342 -> 0.336 ms (`gpurun_out/pv_*`)
             uint64_t g2w[2 * kPE];
             const ulonglong2* gq = reinterpret_cast<const ulonglong2*>(a.gpair);
 #pragma unroll
             for (int t = 0; t < kPE; ++t) {
                 ulonglong2 q0 = make_ulonglong2(0ull, 0ull), q1 = q0;
-                if (e0 + t <= el) {
+                if (e0 + t <= (wl >> 1)) {  // up to the block of the last 2-bit word a try reads
                     q0 = gq[2 * (e0 + t)];
                     q1 = gq[2 * (e0 + t) + 1];
                 }
