@@ -144,11 +144,13 @@ def live_pmc(argv, kernel_regex: str, timeout_s: float = 150.0):
             out = os.path.join(td, name)
             cmd = [prof, "--pmc", *counters, "--kernel-include-regex", kernel_regex, "-d", out, "-o", "run",
                    "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), *child]
+            t_pass = time.time()
             try:
                 res = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, cwd=td,
                                      env=dict(os.environ, TMPDIR=td))
             except subprocess.TimeoutExpired:
                 return None, f"pass {name}: rocprofv3 timed out after {timeout_s:.0f} s"
+            log(f"live counters: pass {name} took {time.time() - t_pass:.1f} s")
             if res.returncode:
                 return None, f"pass {name}: rocprofv3 exit {res.returncode}: {res.stderr[-300:]}"
             files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
@@ -156,11 +158,52 @@ def live_pmc(argv, kernel_regex: str, timeout_s: float = 150.0):
                 return None, f"pass {name}: no counter CSV"
             for f in files:
                 ctr.update(pmc_counters(f))
+        # the scan stage's own duration: a kernel-trace pass (no counters) of the same child, one
+        # handle so that no kernel of another step runs beside a scan (isolated dispatches)
+        out = os.path.join(td, "trace")
+        cmd = [prof, "--kernel-trace", "--kernel-include-regex", kernel_regex, "-d", out, "-o", "run",
+               "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__), *child,
+               "--no-pipeline", "--steps", str(TRACE_STEPS)]
+        t_pass = time.time()
+        try:
+            res = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, cwd=td,
+                                 env=dict(os.environ, TMPDIR=td))
+        except subprocess.TimeoutExpired:
+            return None, f"pass trace: rocprofv3 timed out after {timeout_s:.0f} s"
+        log(f"live counters: pass trace took {time.time() - t_pass:.1f} s")
+        if res.returncode:
+            return None, f"pass trace: rocprofv3 exit {res.returncode}: {res.stderr[-300:]}"
+        files = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
+        if not files:
+            return None, "pass trace: no kernel-trace CSV"
+        ctr.update(trace_stage_ns(files[0]))
     missing = [c for _, cs in PMC_PASSES for c in cs if c not in ctr]
     if missing:
         return None, f"counters missing from the passes: {missing}"
-    return ctr, (f"live: {len(PMC_PASSES)} rocprofv3 --pmc passes of this bench command (--pmc-child: same build, "
-                 f"workload and options), kernels /{kernel_regex}/, counters per search step")
+    return ctr, (f"live: {len(PMC_PASSES)} rocprofv3 --pmc passes and one --kernel-trace pass of this bench command "
+                 f"(--pmc-child: same build, workload and options), kernels /{kernel_regex}/, per search step")
+
+
+TRACE_STEPS = 8
+
+
+def trace_stage_ns(csv_path: str) -> dict:
+    """The scan stage's duration per search step from a rocprofv3 kernel-trace CSV: each kernel
+    form's dispatches averaged (the first dispatch of each form, a cold start, left out when
+    there are more), the forms of a step summed (a split W 7..9 table scans two or three
+    forms one after another).  The forms' dispatch counts and medians are kept beside it."""
+    import collections
+    import csv
+    dur = collections.defaultdict(list)
+    for r in csv.DictReader(open(csv_path)):
+        dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    total, forms = 0.0, {}
+    for name, v in dur.items():
+        use = v[1:] if len(v) > 1 else v
+        total += sum(use) / len(use)
+        forms[name] = {"dispatches": len(v), "mean_ns": round(sum(use) / len(use), 1),
+                       "median_ns": float(np.median(use))}
+    return {"_trace_stage_ns": total, "_trace_forms": forms}
 
 
 def issue_bound(pmc: dict, dur_ns=None):
@@ -730,9 +773,8 @@ def main():
         return
     bases = float(sum(lens))          # one rank's genome (= the whole job's at N=1 or strong)
     t_step = elapsed / args.steps
-    kern_s = float(np.mean(scan_ms)) / 1e3
+    kern_ev_s = float(np.mean(scan_ms)) / 1e3  # HIP events on the scan's launch stream
     alg_bytes = BYTES_PER_BASE * st["windows"] + BYTES_PER_HIT * search.last_hits()  # rank 0's scan launch
-    achieved = alg_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
     # the scan stage's kernels (events around all of them): a split W 7..9 table scans its two
     # exact seeds with scan_kernel (plus dense_kernel over the records they cannot carry)
     sp = table.split()
@@ -768,6 +810,14 @@ def main():
             if prof is not None:
                 pmc, pmc_src = prof, f"profiles/{tag}_pmc.json (committed profile of this build)"
                 traffic = prof["hbm_traffic_bytes_per_launch"]
+    # roofline time: the scan stage's isolated dispatches in the kernel-trace pass (rocprofv3's own
+    # clock, no event between kernels); the HIP events when no trace ran (N > 1, shard, --no-pmc)
+    trace_ns = (pmc or {}).get("_trace_stage_ns") or (pmc or {}).get("avg_duration_ns_trace")
+    kern_s = trace_ns / 1e9 if trace_ns else kern_ev_s
+    kern_src = ("rocprofv3 --kernel-trace pass of this command: mean isolated dispatch of each scan form, "
+                "forms of a step summed" if (pmc or {}).get("_trace_stage_ns")
+                else ("avg_duration_ns_trace of the committed profile" if trace_ns else "HIP events (no trace pass)"))
+    achieved = alg_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
     out = {
         "metric": METRIC,
         "value": round(tot_bases / max(args.shard_of, 1) / t_step / 1e9, 4),
@@ -790,6 +840,8 @@ def main():
         "hits": int(tot_hits),
         "hits_per_s": round(tot_hits / t_step, 1),
         "scan_kernel_ms": round(kern_s * 1e3, 3),
+        "scan_kernel_ms_source": kern_src,
+        "scan_kernel_ms_events": round(kern_ev_s * 1e3, 3),
         "tail_kernel_ms": round(float(np.mean(tail_ms)), 3),
         "pair_kernel_ms": round(float(np.mean(pair_ms)), 3),
         "order_ms": round(float(np.mean(order_ms)), 3),
@@ -804,6 +856,9 @@ def main():
                      "traffic_null_reason": None if traffic else why,
                      "kernel": scan_label,
                      "alg_bytes_per_launch": int(alg_bytes),
+                     "time_ms": round(kern_s * 1e3, 4),
+                     "time_source": kern_src,
+                     "trace_forms": (pmc or {}).get("_trace_forms"),
                      "issue": (dict(issue_bound(pmc, kern_s * 1e9), source=pmc_src) if pmc else None)},
         "build": build,
         "setup_s": round(setup_s, 2),

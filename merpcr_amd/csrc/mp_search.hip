@@ -786,6 +786,12 @@ static_assert(sizeof(WaveLds) <= 2048, "per-wave LDS beside the 128 KiB prefilte
 
 // The current super-step as the wave holds it: lane L owns bases [base + 32L,
 // base + 32L + 64) as two 2-bit words and one ambiguity word.
+// A lane's 32 (+32) ambiguity bits from the two plane words around its first base: sh = 32
+// when that base is in the second half of the first word.
+__device__ __forceinline__ uint64_t inv_join(uint64_t v0, uint64_t v1, uint32_t sh) {
+    return (v0 << sh) | ((v1 >> (63 - sh)) >> 1);
+}
+
 struct SuperRegs {
     uint64_t w0, w1, iv;
     uint32_t base;
@@ -1718,19 +1724,33 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         pf_sbase = a.seq_base[pf.seq];
         pf_n = (uint32_t)a.seq_len[pf.seq];
     };
-    auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& iv) {
+    // The prefetch keeps the two raw ambiguity words; they are joined where the super-step
+    // starts.  Joining them at the prefetch (round 5) put a vmcnt wait for the ambiguity load
+    // -- and, counters being in order, for every level-2 probe issued before it -- right
+    // after the issue: the "prefetch" of that plane was a synchronous HBM round trip per
+    // super-step.
+    auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& v0, uint64_t& v1) {
         const uint64_t j = pf_sbase + pf.p_al + (x - pf.super0) * kSuper + (uint64_t)lane * kLanePos;
         w0 = a.g2[j >> 5];
         w1 = a.g2[(j >> 5) + 1];
-        const uint64_t v0 = a.ginv[j >> 6];
-        const uint64_t v1 = a.ginv[(j >> 6) + 1];
-        const uint32_t sh = (uint32_t)(j & 32);  // branch-free: both loads always issue
-        iv = (v0 << sh) | ((v1 >> (63 - sh)) >> 1);
+        v0 = a.ginv[j >> 6];  // branch-free: both loads always issue
+        v1 = a.ginv[(j >> 6) + 1];
     };
-    uint64_t nw0 = 0, nw1 = 0, niv = 0;
+    uint64_t nw0 = 0, nw1 = 0, nv0 = 0, nv1 = 0;
+    // The next super-step's words, issued after this step's level-2 probes.  They are issued
+    // on every path -- a scan's last super-step reloads its own words, a dense super-step's
+    // later rounds the same addresses -- so that they are the youngest loads wherever the
+    // probes are consumed: the compiler then waits vmcnt(2) there, and the HBM round trip
+    // runs under the rest of the super-step.  (A conditional issue merges with a path that
+    // has no such loads, and the merged wait is vmcnt(0).)
+    auto prefetch = [&](uint64_t nx, uint64_t cur) {
+        const uint64_t x = nx < n_supers ? nx : cur;
+        locate(x);
+        words(x, nw0, nw1, nv0, nv1);
+    };
     if (ss < n_supers) {
         locate(ss);
-        words(ss, nw0, nw1, niv);
+        words(ss, nw0, nw1, nv0, nv1);
     }
     while (ss < n_supers) {
         const SeqSpan sp = pf;
@@ -1739,11 +1759,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
         SuperRegs R;
         R.w0 = nw0;
         R.w1 = nw1;
-        R.iv = niv;
         R.base = sp.p_al + (uint32_t)(ss - sp.super0) * kSuper;
         R.seq = sp.seq;
         R.owned = (a.g_lo == 0 || sbase + R.base >= a.g_lo + 65536u) && sbase + R.base + kSuper <= a.g_hi;
         const uint32_t pb = R.base + (uint32_t)lane * kLanePos;
+        R.iv = inv_join(nv0, nv1, (uint32_t)((sbase + pb) & 32u));
         const uint32_t d0 = (uint32_t)(R.w0 >> 32), d1 = (uint32_t)R.w0, d2 = (uint32_t)(R.w1 >> 32);
         // a gapped seed's windows: both of its pieces clean
         const uint32_t okm = (kGap ? window_ok_mask(R.iv, g_at) &
@@ -1766,7 +1786,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
             const uint32_t c = (uint32_t)__popc(rem);
             const uint32_t incl = wave_incl_scan(c, lane);
             const uint32_t tot = rl32(incl, 63);
-            bool first = true;
             uint32_t r0 = 0;
             do {  // rounds of kSeedQR positives (one round unless the super-step is dense)
                 {
@@ -1840,13 +1859,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                         }
                     }
                 }
-                if (first) {  // the next super-step's words, issued after this step's probes
-                    first = false;
-                    if (nx < n_supers) {
-                        locate(nx);
-                        words(nx, nw0, nw1, niv);
-                    }
-                }
+                prefetch(nx, ss);  // after this round's probes (every round: see prefetch)
                 wave_sync();  // every list entry is in registers before the seeds overwrite it
                 if constexpr (kRkf != 0) {
                     // the few seeds that pass the key groups (c3: 4% of seeds) leave as key
@@ -1912,16 +1925,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                 wave_sync();
                 r0 += kSeedQR;
             } while (r0 < tot);
-            (void)first;
             ss = nx;
             continue;
         }
         uint32_t hits = probe32<kMode>(a, s_lf, d0, d1, d2, shw, okm, [&] {
-            // prefetch the next super-step's words (issued after this step's probes)
-            if (nx < n_supers) {
-                locate(nx);
-                words(nx, nw0, nw1, niv);
-            }
+            prefetch(nx, ss);  // the next super-step's words (issued after this step's probes)
         });
         // publish this super-step's seed hits: per-lane masks + prefix of their counts
         const uint32_t c = (uint32_t)__popc(hits);
@@ -2095,28 +2103,27 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         pf_sbase = a.seq_base[pf.seq];
         pf_n = (uint32_t)a.seq_len[pf.seq];
     };
-    auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& iv) {
+    auto words = [&](uint64_t x, uint64_t& w0, uint64_t& w1, uint64_t& v0, uint64_t& v1) {  // as scan_kernel's
         const uint64_t j = pf_sbase + pf.p_al + (x - pf.super0) * kSuper + (uint64_t)lane * kLanePos;
         w0 = a.g2[j >> 5];
         w1 = a.g2[(j >> 5) + 1];
-        const uint64_t v0 = a.ginv[j >> 6];
-        const uint64_t v1 = a.ginv[(j >> 6) + 1];
-        const uint32_t sh = (uint32_t)(j & 32);
-        iv = (v0 << sh) | ((v1 >> (63 - sh)) >> 1);
+        v0 = a.ginv[j >> 6];
+        v1 = a.ginv[(j >> 6) + 1];
     };
-    uint64_t nw0 = 0, nw1 = 0, niv = 0;
+    uint64_t nw0 = 0, nw1 = 0, nv0 = 0, nv1 = 0;
     if (ss < n_supers) {
         locate(ss);
-        words(ss, nw0, nw1, niv);
+        words(ss, nw0, nw1, nv0, nv1);
     }
     while (ss < n_supers) {
         const SeqSpan sp = pf;
         const uint64_t sbase = pf_sbase;
         const uint32_t n = pf_n;
-        const uint64_t w0 = nw0, w1 = nw1, iv = niv;
+        const uint64_t w0 = nw0, w1 = nw1;
         const uint32_t base = sp.p_al + (uint32_t)(ss - sp.super0) * kSuper;
         const bool owned = (a.g_lo == 0 || sbase + base >= a.g_lo + 65536u) && sbase + base + kSuper <= a.g_hi;
         const uint32_t pb = base + (uint32_t)lane * kLanePos;
+        const uint64_t iv = inv_join(nv0, nv1, (uint32_t)((sbase + pb) & 32u));
         const uint32_t d0 = (uint32_t)(w0 >> 32), d1 = (uint32_t)w0, d2 = (uint32_t)(w1 >> 32);
         const uint32_t okm = window_ok_mask(iv, W) &
                              span_bits(sp, pb);
@@ -2129,7 +2136,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
         (void)stride;
         if (nx < n_supers) {  // next super-step's words, in flight during this one
             locate(nx);
-            words(nx, nw0, nw1, niv);
+            words(nx, nw0, nw1, nv0, nv1);
         }
         uint32_t escm = 0;
 #pragma unroll 1

@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0", help="0 = product, n = MP_ABLATE=n, NAME=VAL[+...] = defines, opt:name=val[,...] = search options")
+    ap.add_argument("--variants", default="0", help="0 = product, n = MP_ABLATE=n, NAME=VAL[+...] = defines, opt:name=val[,...] = search options, lib:path = a prebuilt library")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--steps", type=int, default=3)
@@ -36,6 +36,9 @@ def main():
         # 0 = product; n = MP_ABLATE=n; nt = non-temporal genome
         # stream; NAME=VAL[+NAME=VAL...] = those defines
         flags = None
+        if v.startswith("lib:"):  # a library built beforehand (e.g. an earlier build's variant), path from the repo root
+            libs[v] = os.path.join(ROOT, v[4:])
+            continue
         if v == "0" or v.startswith("opt:"):
             defs = ()
         elif v == "atomopt":  # the compiler's atomic optimizer back on for mp_search.hip

@@ -57,12 +57,11 @@ _T_ENTRY = "    zero_sort_counts(a);\n    // stage the seed prefilter in LDS (on
 _T_STAGED = "    const int lane = threadIdx.x & 63;\n    const int w = threadIdx.x >> 6;\n    const uint64_t stride = (uint64_t)gridDim.x * kWaves;"
 _T_END = "    close_chunked(a.surv, a.surv_cap, lane, C);\n    if (a.ref16) close_chunked<1, kTC>"
 _T_TAIL = "MP_EXPORT int mp_search_set_stage_timing(void* search, int32_t on) {"
-_WORDS = ("        w0 = a.g2[j >> 5];\n        w1 = a.g2[(j >> 5) + 1];\n        const uint64_t v0 = a.ginv[j >> 6];\n"
-          "        const uint64_t v1 = a.ginv[(j >> 6) + 1];\n        const uint32_t sh = (uint32_t)(j & 32);  // branch-free")
+_WORDS = ("        w0 = a.g2[j >> 5];\n        w1 = a.g2[(j >> 5) + 1];\n        v0 = a.ginv[j >> 6];  // branch-free: both loads always issue\n"
+          "        v1 = a.ginv[(j >> 6) + 1];\n")
 _WORDS_NT = ("        w0 = __builtin_nontemporal_load(&a.g2[j >> 5]);\n        w1 = __builtin_nontemporal_load(&a.g2[(j >> 5) + 1]);\n"
-             "        const uint64_t v0 = __builtin_nontemporal_load(&a.ginv[j >> 6]);\n"
-             "        const uint64_t v1 = __builtin_nontemporal_load(&a.ginv[(j >> 6) + 1]);\n"
-             "        const uint32_t sh = (uint32_t)(j & 32);  // branch-free")
+             "        v0 = __builtin_nontemporal_load(&a.ginv[j >> 6]);\n"
+             "        v1 = __builtin_nontemporal_load(&a.ginv[(j >> 6) + 1]);\n")
 _T_GLOBAL = ("}  // namespace mp\n\nusing namespace mp;\n\nMP_EXPORT int mp_search_set_stage_timing")
 
 _STEAL = """    __device__ __forceinline__ bool steal(uint64_t n_supers) {  // ablation 70
@@ -114,16 +113,16 @@ _KGRP_BF = """    if (!kGap && !a.kgrp_wild) {  // ablation 71: every field form
 VARIANTS = {
     1: [(_L1, "            if constexpr (kMode == 1) {  // ablation 1\n"
               "                ncand += (uint32_t)__popc(rem);\n"
-              "                if (nx < n_supers) { locate(nx); words(nx, nw0, nw1, niv); }\n"
+              "                prefetch(nx, ss);\n"
               "                ss = nx;\n                continue;\n            }\n")],
-    2: [(_L2, "                if (first) { first = false; if (nx < n_supers) { locate(nx); words(nx, nw0, nw1, niv); } }\n"
+    2: [(_L2, "                prefetch(nx, ss);\n"
               "                ncand += (uint32_t)L.rq.r[lane] & 1u;  // ablation 2\n"
               "                wave_sync();\n                r0 += kSeedQR;\n                continue;\n")],
     3: [(_L3, "                for (int q = 0; q < kP; ++q) ncand += rw[q].x & 1u;  // ablation 3\n"
               "                r0 += kSeedQR;\n                continue;\n")],
     5: [(_PROBE, "            if constexpr (kMode == 1) {  // ablation 5\n"
                  "                ncand += (uint32_t)__popc(okm ^ d0 ^ d1 ^ d2);\n"
-                 "                if (nx < n_supers) { locate(nx); words(nx, nw0, nw1, niv); }\n"
+                 "                prefetch(nx, ss);\n"
                  "                ss = nx;\n                continue;\n            }\n")],
     30: [(_LOOP, "    ss = n_supers;  // ablation 30\n")],
     31: [(_LOOP, "    ss = n_supers;  // ablation 31\n"), (_STAGE, "    if (false)  // ablation 31\n")],
@@ -164,7 +163,7 @@ VARIANTS = {
 
 
 VARIANTS[42] = VARIANTS[40] + [
-    ("            (void)first;\n            ss = nx;\n            continue;",
+    ("            ss = nx;\n            continue;\n        }\n        uint32_t hits = probe32",
      "            if ((threadIdx.x & 63) == 0 && n_ss <= 32 && blockIdx.x * kWaves + (threadIdx.x >> 6) < 8192)  // ablation 42\n"
      "                g_ss_times[(blockIdx.x * kWaves + (threadIdx.x >> 6)) * 32 + n_ss - 1] = wall_clock64();\n"),
     ("struct SuperSched {", "__device__ unsigned long long g_ss_times[8192 * 32];  // ablation 42\n"),

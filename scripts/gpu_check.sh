@@ -14,7 +14,7 @@ tail -3 gpurun_out/${TAG}_gputest.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
     || { echo "smoke failed rc=$?"; tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -2 gpurun_out/${TAG}_smoke.log
-timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 \
+timeout -k 10 700 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 \
     || { echo "bench failed rc=$?"; tail -20 gpurun_out/${TAG}_bench.log; exit 1; }
 tail -1 gpurun_out/${TAG}_bench.log
 # the N-rank path with no outside launcher: bench.py --gpus 2 starts torch.distributed.run itself
