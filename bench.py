@@ -566,6 +566,7 @@ def main():
     if gmode == "rccl":
         gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)  # rank 0's gather buffer
     shift = len(lens) * rank if weak else 0
+    nbuf = 1 if args.no_pipeline else max(2, args.handles)
     ipcg = None
     if gmode == "ipc":
         # regions of twice the largest rank's hit count (one untimed run to learn it); every
@@ -576,7 +577,7 @@ def main():
         dist.all_gather_object(every, n0)
         err = None
         try:
-            ipcg = IpcGather(local, max(4096, 2 * max(every)))
+            ipcg = IpcGather(local, max(4096, 2 * max(every)), slots=nbuf)  # a region slot per handle
             ipcg.put(search, stream)  # a probe put of that run: the copy engines reach rank 0's HBM
             torch.cuda.synchronize()
         except Exception as e:  # noqa: BLE001 (reported, then every rank takes the same fallback)
@@ -601,14 +602,13 @@ def main():
     # the host waits for step i, so the host turnaround between runs is off the GPU's path.
     # With N > 1 each completed step's RCCL gather runs on a stream of its own, and the
     # handle's next run waits (on the device) for its gather to have sent the hits.
-    nbuf = 1 if args.no_pipeline else max(2, args.handles)
     handles = [search] + [_native.Search(table, genome) for _ in range(nbuf - 1)]
     if args.opts:
         kw = {}
         for item in args.opts.split(","):
             k, val = item.split("=")
-            kw[k] = val if k in ("tails", "sort") else (val.lower() in ("1", "true") if k in (
-                "defer", "dense", "rank_filter", "split") else int(val))
+            kw[k] = val if k in ("tails", "sort", "generic") else (val.lower() in ("1", "true") if k in (
+                "defer", "dense", "rank_filter", "split", "ref32") else int(val))
         for h in handles:
             h.set_options(**kw)
     # one stream per handle (--one-stream: all on the default stream): step i+1's scan may then
@@ -626,8 +626,8 @@ def main():
         n = h.last_hits()
         if world == 1:
             return n, None
-        if ipcg is not None:  # on the handle's stream: its next run waits for the copy
-            ipcg.put(h, streams[j].cuda_stream)
+        if ipcg is not None:  # on the handle's stream, into the handle's own region slot
+            ipcg.put(h, streams[j].cuda_stream, slot=j)
             return n, None
         if comm is None:  # host gather over gloo
             from merpcr_amd.dist import gather_hits as gloo_gather
@@ -700,8 +700,11 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    if ipcg is not None and rank == 0:  # every rank's puts are complete (synchronised before the barrier)
-        nhits = int(sum(ipcg.counts()))
+    if ipcg is not None:  # every rank's puts are complete (synchronised before the barrier)
+        if ipcg.settle():  # a put did not fit its region: regrown, every slot put again (untimed)
+            log(f"[rank {rank}] IPC gather regions regrown to {ipcg.cap} hits")
+        if rank == 0:
+            nhits = int(sum(ipcg.counts((args.steps - 1) % nbuf)))
     timed_scan_ms = list(scan_ms)
     if args.pmc_child:  # a counter pass of live_pmc: the counters are all it is for
         for h in handles:
@@ -756,6 +759,10 @@ def main():
     dist_check = None
     if world > 1 or args.shard_of > 1:
         got = None
+        if ipcg is not None:  # collective: the untimed steps' puts (slot 0) may need a regrow too
+            torch.cuda.synchronize()
+            torch.distributed.barrier()
+            ipcg.settle()
         if world > 1 and rank == 0:
             if ipcg is not None:
                 raw = ipcg.hits([len(lens) * r for r in range(world)] if weak else None).cpu().numpy()

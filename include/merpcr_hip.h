@@ -23,7 +23,10 @@
 extern "C" {
 #endif
 
-#define MP_ABI_VERSION 2  /* 2: mp_search_options without fuse_tails; mp_table_layout */
+#define MP_ABI_VERSION 3  /* 2: mp_search_options without fuse_tails; mp_table_layout.
+                             3: mp_table_create_ex, mp_search_options form/tuning fields (no
+                             environment switches), mp_search_put_hits reports the need,
+                             mp_multi_set_gather */
 
 #define MP_OK 0
 #define MP_E_ARG (-1)     /* bad argument (maps to ValueError) */
@@ -100,6 +103,22 @@ int mp_table_split(void* table, uint32_t* seed_tables, uint32_t* rest_records);
 #define MP_LAYOUT_SPLIT 32u    /* split seeds (mp_table_split) */
 #define MP_LAYOUT_HASHED 64u   /* hashed presence filter + open-addressed slots (W >= 14) */
 int mp_table_layout(void* table, uint32_t* flags);
+/* Layout choices of a table build.  Every field zero = the library's own choice (what
+ * mp_table_create makes); the others exist for A/B runs and for tests that drive each layout
+ * against the oracle.  No layout choice is read from the process environment. */
+typedef struct mp_table_options {
+    int32_t lds_k;   /* W 11..13: prefilter bits per key, 1..3; 0 = from the key count */
+    int32_t no_h12;  /* 1: IUPAC-after-seed tables keep the 16-B heads, not the 8-B IUPAC heads */
+    int32_t kgrp4;   /* wide I = 1 key groups: 0 = when the pass-rate estimate favours them,
+                        1 = never, -1 = whenever the table can carry them */
+    int32_t no_split;/* 1: W 7..9 tables are not split into exact-seed sub-tables */
+} mp_table_options;
+int mp_table_create_ex(const mp_params* params, int32_t device, uint32_t n_rec,
+                       const uint32_t* key, const uint32_t* hash_off,
+                       const uint64_t* pcr_size,
+                       const uint8_t* primer1, const uint64_t* p1_off,
+                       const uint8_t* primer2, const uint64_t* p2_off,
+                       const mp_table_options* options, void** table_out);
 void mp_table_destroy(void* table);
 
 /* ---- genome (replaces the per-record sequence strings that search() walks,
@@ -158,7 +177,15 @@ typedef struct mp_search_options {
                                    filtered rank groups' primer-base filter */
     int32_t no_split;           /* 1: W 7..9 tables keep the dense scan, not the split seeds
                                    (two exact-seed scans, see mp_internal.h kSplitSeed) */
+    int32_t generic_forms;      /* MP_GENERIC_* bits: the run-time-shape kernel forms in place of
+                                   the constant-shape ones (A/B; the hit lists are identical) */
+    int32_t ref32;              /* 1: 32-B bucket-tail key references where 16-B ones fit */
+    int32_t sched_short;        /* super-steps per scheduler claim in short scans; 0 = 4 */
+    int32_t crowd_grid;         /* workgroups of the crowded-bucket sort; 0 = one per CU */
 } mp_search_options;
+#define MP_GENERIC_FIX 1u   /* key-group scans of W = 11 with W, F and N as run-time values */
+#define MP_GENERIC_GAP 2u   /* the gapped W = 8 split seed with its shape as run-time values */
+#define MP_GENERIC_PAIR 4u  /* pair_kernel with I, N and X as run-time values */
 /* Replace the handle's options (reallocating the lists to the given capacities). */
 int mp_search_set_options(void* search, const mp_search_options* opt);
 /* Per-stage timing (tail, pair and order events; default on).  Off, a run records only the
@@ -205,10 +232,10 @@ void mp_search_destroy(void* search);
  * One process, several devices: the genome's (sequence, k) space is split into owned
  * ranges of equal base count, one per device (contiguous, in device order); each device
  * packs only the bases its range reads and searches it in a host thread of its own; the
- * sorted per-device lists are gathered into devices[0] by one grouped ncclSend/ncclRecv
- * over RCCL (xGMI).  Their concatenation is exactly the single-device hit list.
- * tables[i] must have been created on devices[i] from the same records.  A device listed
- * twice (tests on one GPU) is gathered by device copies: RCCL admits one rank per device. */
+ * sorted per-device lists are gathered into devices[0] by the copy engines over xGMI
+ * (mp_multi_set_gather).  Their concatenation is exactly the single-device hit list.
+ * tables[i] must have been created on devices[i] from the same records.  A device may be
+ * listed twice (tests on one GPU): the gather is the same peer copy. */
 int mp_multi_create(uint32_t n_dev, const int32_t* devices, void* const* tables, void** multi_out);
 /* (Re)lay out the sequence set on every device and split it into owned ranges. */
 int mp_multi_genome(void* multi, uint32_t n_seq, const uint64_t* seq_len);
@@ -217,6 +244,14 @@ int mp_multi_put(void* multi, uint32_t seq, const uint8_t* host_bytes, uint64_t 
 int mp_multi_seal(void* multi);
 /* Search every device's owned range and gather: *n_hits = all hits, in output order. */
 int mp_multi_run(void* multi, uint64_t* n_hits);
+/* The gather's data plane.  MP_GATHER_COPY (default): the copy engines move each device's
+ * sorted list into devices[0] (hipMemcpyPeerAsync on devices[0]'s stream, peer access enabled
+ * once; no kernel on the CUs), for distinct and repeated devices alike.  MP_GATHER_RCCL: one
+ * grouped ncclSend/ncclRecv gatherv (ncclCommInitAll at the first such run; distinct devices
+ * only). */
+#define MP_GATHER_COPY 0
+#define MP_GATHER_RCCL 1
+int mp_multi_set_gather(void* multi, int32_t mode);
 int mp_multi_fetch(void* multi, mp_hit* out, uint64_t cap);
 /* Device i's search handle (borrowed: stats, timings), its owned range and the last
  * gather's duration on devices[0]'s stream. */
@@ -246,15 +281,18 @@ void mp_comm_destroy(void* comm);
  * (hipMemcpyDeviceToDeviceNoCU / host-to-device): a persistent scan holds every CU's LDS, so a
  * collective's kernels (RCCL's need 37 KiB of LDS) would wait for the scan to end.  Regions
  * are fixed: rank r owns [r * cap, (r + 1) * cap) entries; a sequence-index shift (contig
- * shards) is the reader's.  MP_E_CAP: more hits than cap (nothing copied).  Not collective;
- * completion is the stream's. */
+ * shards) is the reader's.  *n_hits (may be NULL) = the run's hit count, always: on MP_E_CAP
+ * (more hits than cap, nothing copied) it is the region size a regrow needs.  Not collective;
+ * completion is the stream's.  The handle's next mp_search_enqueue, on any stream, waits on the
+ * device for the put to have read the hit list; a handle's puts must stay on one stream. */
 #define MP_IPC_HANDLE_BYTES 64
 /* The handle names dev_ptr's whole allocation; *offset = dev_ptr - its base.  mp_ipc_open
  * returns the base as mapped here: add the offset. */
 int mp_ipc_handle(void* dev_ptr, uint8_t* handle64, uint64_t* offset);
 int mp_ipc_open(const uint8_t* handle64, int32_t device, void** base_out);
 int mp_ipc_close(void* dev_ptr);
-int mp_search_put_hits(void* search, mp_hit* dst, uint64_t cap, uint64_t* count_dst, void* stream);
+int mp_search_put_hits(void* search, mp_hit* dst, uint64_t cap, uint64_t* count_dst, uint64_t* n_hits,
+                       void* stream);
 
 /* ---- FASTA input (replaces FASTALoader.load_file, src/merpcr/io/fasta.py:18-71) --
  * Reads `path` as the reference's text-mode loop does: strict UTF-8, universal

@@ -29,14 +29,14 @@ MP_STS_OK, MP_STS_BAD_LINE, MP_STS_PYTHON = 0, 1, 2
 # every symbol include/merpcr_hip.h declares
 EXPORTS = (
     "mp_abi_version", "mp_last_error", "mp_device_count",
-    "mp_table_create", "mp_table_stats", "mp_table_split", "mp_table_layout", "mp_table_destroy",
+    "mp_table_create", "mp_table_create_ex", "mp_table_stats", "mp_table_split", "mp_table_layout", "mp_table_destroy",
     "mp_genome_create", "mp_genome_put", "mp_genome_put_device", "mp_genome_seal",
     "mp_genome_stats", "mp_genome_download", "mp_genome_reset", "mp_genome_destroy",
     "mp_search_create", "mp_search_set_options", "mp_search_set_stage_timing", "mp_search_set_scan_timing", "mp_search_run",
     "mp_search_enqueue", "mp_search_complete", "mp_search_fetch", "mp_search_fetch_device", "mp_search_device_hits",
     "mp_search_last_stats", "mp_search_regrowths", "mp_search_dev_bytes", "mp_search_survivors", "mp_search_timing", "mp_search_destroy",
     "mp_multi_create", "mp_multi_genome", "mp_multi_put", "mp_multi_seal", "mp_multi_run", "mp_multi_fetch",
-    "mp_multi_device_search", "mp_multi_timing", "mp_multi_destroy",
+    "mp_multi_set_gather", "mp_multi_device_search", "mp_multi_timing", "mp_multi_destroy",
     "mp_comm_unique_id", "mp_comm_create", "mp_comm_gather_hits", "mp_comm_destroy",
     "mp_ipc_handle", "mp_ipc_open", "mp_ipc_close", "mp_search_put_hits",
     "mp_fasta_load", "mp_fasta_load_parallel", "mp_fasta_load_chunked", "mp_fasta_info", "mp_fasta_record_ascii", "mp_fasta_record", "mp_fasta_destroy",
@@ -65,7 +65,17 @@ class MPSearchOptions(ctypes.Structure):
     _fields_ = [("tails", c_int32), ("no_defer", c_int32), ("no_dense", c_int32), ("sort", c_int32),
                 ("sort_bucket_bits", c_int32), ("pair_blocks_per_cu", c_int32),
                 ("hit_cap", c_uint64), ("surv_cap", c_uint64), ("tail_cap", c_uint64),
-                ("no_rank_filter", c_int32), ("no_split", c_int32)]
+                ("no_rank_filter", c_int32), ("no_split", c_int32),
+                ("generic_forms", c_int32), ("ref32", c_int32), ("sched_short", c_int32), ("crowd_grid", c_int32)]
+
+
+class MPTableOptions(ctypes.Structure):
+    _fields_ = [("lds_k", c_int32), ("no_h12", c_int32), ("kgrp4", c_int32), ("no_split", c_int32)]
+
+
+ABI_VERSION = 3
+MP_GENERIC = {"fix": 1, "gap": 2, "pair": 4}
+MP_GATHER = {"copy": 0, "rccl": 1}
 
 
 HIT_DTYPE = np.dtype([("pos1", "<u8"), ("pos2", "<u8"), ("seq", "<u4"), ("rec", "<u4")])
@@ -105,6 +115,8 @@ def _sig(lib):
     lib.mp_device_count.argtypes = [POINTER(c_int32)]
     lib.mp_table_create.argtypes = [POINTER(MPParams), c_int32, c_uint32, P, P, P, P, P, P, P,
                                     POINTER(c_void_p)]
+    lib.mp_table_create_ex.argtypes = [POINTER(MPParams), c_int32, c_uint32, P, P, P, P, P, P, P,
+                                       POINTER(MPTableOptions), POINTER(c_void_p)]
     lib.mp_table_stats.argtypes = [P, u64p, u64p, u64p]
     lib.mp_table_split.argtypes = [P, POINTER(c_uint32), POINTER(c_uint32)]
     lib.mp_table_layout.argtypes = [P, POINTER(c_uint32)]
@@ -141,6 +153,7 @@ def _sig(lib):
     lib.mp_multi_put.argtypes = [P, c_uint32, P, c_uint64]
     lib.mp_multi_seal.argtypes = [P]
     lib.mp_multi_run.argtypes = [P, u64p]
+    lib.mp_multi_set_gather.argtypes = [P, c_int32]
     lib.mp_multi_fetch.argtypes = [P, P, c_uint64]
     lib.mp_multi_device_search.argtypes = [P, c_uint32, POINTER(c_void_p), POINTER(MPRange), POINTER(c_float)]
     lib.mp_multi_timing.argtypes = [P, POINTER(c_float), POINTER(c_float)]
@@ -154,7 +167,7 @@ def _sig(lib):
     lib.mp_ipc_handle.argtypes = [P, P, u64p]
     lib.mp_ipc_open.argtypes = [P, c_int32, POINTER(c_void_p)]
     lib.mp_ipc_close.argtypes = [P]
-    lib.mp_search_put_hits.argtypes = [P, P, c_uint64, P, P]
+    lib.mp_search_put_hits.argtypes = [P, P, c_uint64, P, u64p, P]
     lib.mp_fasta_load.argtypes = [c_char_p, POINTER(c_void_p)]
     lib.mp_fasta_load_chunked.argtypes = [c_char_p, c_uint64, POINTER(c_void_p)]
     lib.mp_fasta_load_parallel.argtypes = [c_char_p, c_int32, POINTER(c_void_p)]
@@ -213,7 +226,8 @@ def lib():
         _share_hip_runtime()
         l = ctypes.CDLL(LIB_PATH)
         _sig(l)
-        if l.mp_abi_version() != 2:
+        # MERPCR_LIB (A/B runs against an earlier build) admits the previous ABI as well
+        if l.mp_abi_version() != ABI_VERSION and not (os.environ.get("MERPCR_LIB") and l.mp_abi_version() == 2):
             raise RuntimeError("libmerpcr_hip ABI version mismatch")
         _lib = l
     return _lib
@@ -242,7 +256,11 @@ def ptr(a: np.ndarray) -> c_void_p:
 class Table:
     """Device seed table (owns the native handle)."""
 
-    def __init__(self, params: MPParams, device: int, key, hash_off, pcr_size, p1, p1_off, p2, p2_off):
+    def __init__(self, params: MPParams, device: int, key, hash_off, pcr_size, p1, p1_off, p2, p2_off,
+                 lds_k: int = 0, h12: bool = True, kgrp4: str = "auto", split: bool = True):
+        """Layout choices (mp_table_create_ex; the defaults are the library's own): lds_k 1..3 bits
+        per key in the W 11..13 prefilter, h12 False keeps the 16-B IUPAC heads, kgrp4 "never" /
+        "always" for the wide I = 1 key groups, split False keeps W 7..9 tables unsplit."""
         self._h = c_void_p()
         self.n_rec = len(key)
         key = np.ascontiguousarray(key, dtype=np.uint32)
@@ -253,9 +271,16 @@ class Table:
         p1_off = np.ascontiguousarray(p1_off, dtype=np.uint64)
         p2_off = np.ascontiguousarray(p2_off, dtype=np.uint64)
         self.params = params
-        check(lib().mp_table_create(ctypes.byref(params), device, self.n_rec, ptr(key), ptr(hash_off),
-                                    ptr(pcr_size), ptr(p1), ptr(p1_off), ptr(p2), ptr(p2_off),
-                                    ctypes.byref(self._h)))
+        opt = MPTableOptions(int(lds_k), 0 if h12 else 1, {"auto": 0, "never": 1, "always": -1}[kgrp4],
+                             0 if split else 1)
+        if not callable(lib().mp_table_create_ex):  # an ABI 2 library under MERPCR_LIB (A/B runs)
+            check(lib().mp_table_create(ctypes.byref(params), device, self.n_rec, ptr(key), ptr(hash_off),
+                                        ptr(pcr_size), ptr(p1), ptr(p1_off), ptr(p2), ptr(p2_off),
+                                        ctypes.byref(self._h)))
+            return
+        check(lib().mp_table_create_ex(ctypes.byref(params), device, self.n_rec, ptr(key), ptr(hash_off),
+                                       ptr(pcr_size), ptr(p1), ptr(p1_off), ptr(p2), ptr(p2_off),
+                                       ctypes.byref(opt), ctypes.byref(self._h)))
 
     def stats(self):
         a, b, c = c_uint64(), c_uint64(), c_uint64()
@@ -350,12 +375,20 @@ class Search:
         check(lib().mp_search_create(table._h, genome._h, ctypes.byref(self._h)))
 
     def set_options(self, tails="auto", defer=True, dense=True, sort="auto", sort_bucket_bits=0,
-                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True, split=True):
-        """Kernel-path selection and initial list capacities (mp_search_set_options);
-        the defaults are the library's automatic choices."""
+                    pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True, split=True,
+                    generic=(), ref32=False, sched_short=0, crowd_grid=0):
+        """Kernel-path selection, initial list capacities and tuning (mp_search_set_options);
+        the defaults are the library's automatic choices.  generic: names of MP_GENERIC ("fix",
+        "gap", "pair": the run-time-shape kernel forms, for A/B runs)."""
+        if isinstance(generic, str):
+            generic = [g for g in generic.split("+") if g]
+        gbits = 0
+        for g in generic:
+            gbits |= MP_GENERIC[g]
         o = MPSearchOptions(MP_TAILS[tails], 0 if defer else 1, 0 if dense else 1, MP_SORT[sort],
                             sort_bucket_bits, pair_blocks_per_cu, hit_cap, surv_cap, tail_cap,
-                            0 if rank_filter else 1, 0 if split else 1)
+                            0 if rank_filter else 1, 0 if split else 1, gbits, 1 if ref32 else 0,
+                            int(sched_short), int(crowd_grid))
         check(lib().mp_search_set_options(self._h, ctypes.byref(o)))
 
     def set_stage_timing(self, on: bool):
@@ -413,11 +446,20 @@ class Search:
         """Copy the last run's hits into device memory at dev_ptr (cap entries)."""
         check(lib().mp_search_fetch_device(self._h, c_void_p(dev_ptr), cap, c_void_p(stream or 0)))
 
-    def put_hits(self, dst: int, cap: int, count_dst: int, stream=None):
+    def put_hits(self, dst: int, cap: int, count_dst: int, stream=None) -> int:
         """The last run's hits into dst (cap entries; another rank's buffer mapped by ipc_open
         on one node) and their count into the u64 at count_dst, by the copy engines on
-        `stream` (mp_search_put_hits)."""
-        check(lib().mp_search_put_hits(self._h, c_void_p(dst), cap, c_void_p(count_dst), c_void_p(stream or 0)))
+        `stream` (mp_search_put_hits).  Returns the count; more than cap raises NativeError
+        (code MP_E_CAP, nothing copied) whose ``need`` is the count."""
+        n = c_uint64(0)
+        rc = lib().mp_search_put_hits(self._h, c_void_p(dst), cap, c_void_p(count_dst), ctypes.byref(n),
+                                      c_void_p(stream or 0))
+        if rc == MP_E_CAP:
+            e = NativeError(rc, lib().mp_last_error().decode(errors="replace"))
+            e.need = n.value
+            raise e
+        check(rc)
+        return n.value
 
     def device_hits(self) -> int:
         p = c_void_p()
@@ -458,7 +500,7 @@ class _Borrowed(Search):
 
 class Multi:
     """One process, several devices (mp_multi_*): owned ranges of one sequence set, one per
-    device, searched in parallel and gathered into devices[0] over RCCL."""
+    device, searched in parallel and gathered into devices[0] by the copy engines (xGMI)."""
 
     def __init__(self, devices, tables):
         self.devices = [int(d) for d in devices]
@@ -479,6 +521,10 @@ class Multi:
 
     def seal(self):
         check(lib().mp_multi_seal(self._h))
+
+    def set_gather(self, mode: str):
+        """"copy" (default: peer copies by the copy engines) or "rccl" (distinct devices)."""
+        check(lib().mp_multi_set_gather(self._h, MP_GATHER[mode]))
 
     def run(self) -> int:
         n = c_uint64(0)

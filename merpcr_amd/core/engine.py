@@ -254,6 +254,9 @@ class MerPCR:
         # kernel-path selection of the device search (tests; _native.Search.set_options
         # keywords), and the genome/search handles kept across search() calls
         self.search_options: dict = {}
+        # layout choices of the device seed table (tests and A/B runs; _native.Table keywords:
+        # lds_k, h12, kgrp4, split); empty = the library's own
+        self.table_options: dict = {}
         self._dev_genome = None
         self._dev_search = None
         self._dev_search_key = None
@@ -514,9 +517,14 @@ class MerPCR:
     def _record_keys(self, recs) -> np.ndarray:
         """Each record's seed key: the one it is filed under in sts_table.  The reference finds a
         record only through its load-time bucket (engine.py:265-279, 483-486), whatever its
-        primer holds after an edit in place, and takes hash_offset from the record itself.  A
-        record the caller put in sts_records alone is keyed by its primer as the loader would
-        have keyed it."""
+        primer holds after an edit in place, and takes hash_offset from the record itself.
+
+        Deliberate extension, not reference parity: the device table is built from sts_records,
+        so a record the caller put in sts_records alone (never filed in sts_table) is keyed by
+        its primer as the loader would have keyed it and IS searched, where the reference, which
+        walks only sts_table's buckets (engine.py:483-486), would never report it; conversely a
+        record filed in sts_table alone is not searched here.  Both need the caller to edit the
+        engine's internal containers by hand; the loaders keep the two in step."""
         filed = {}
         for h, lst in self.sts_table.items():
             for r in lst:
@@ -547,9 +555,10 @@ class MerPCR:
         """The seed table resident on this engine's GPU (rebuilt when stale)."""
         from .. import _native
         sig = (self._records_sig(), self._n_records(), self.wordsize, self.margin,
-               self.mismatches, self.three_prime_match, self.iupac_mode, self.device)
+               self.mismatches, self.three_prime_match, self.iupac_mode, self.device,
+               tuple(sorted(self.table_options.items())))
         if self._dev_table is None or self._dev_table_sig != sig:
-            self._dev_table = _native.Table(self._params(), self.device, *self._table_arrays())
+            self._dev_table = _native.Table(self._params(), self.device, *self._table_arrays(), **self.table_options)
             self._dev_table_sig = sig
             self._extra_tables = {}
         return self._dev_table
@@ -577,7 +586,7 @@ class MerPCR:
                 out.append(first)
                 continue
             if d not in self._extra_tables:
-                self._extra_tables[d] = _native.Table(self._params(), d, *self._table_arrays())
+                self._extra_tables[d] = _native.Table(self._params(), d, *self._table_arrays(), **self.table_options)
             out.append(self._extra_tables[d])
         return out
 

@@ -68,6 +68,7 @@ constexpr int kHashedFilterLog2 = 27;               // 16 MiB hashed filter for 
 constexpr int kDirectFilterMaxW = 13;               // 4^13 bits = 8 MiB direct bitmap
 constexpr int kBlock = 1024;                        // threads per scan workgroup (one per CU)
 constexpr int kWaves = kBlock / 64;
+constexpr uint32_t kPutRing = 64;  // mp_search_put_hits: pinned count slots in flight per handle
 constexpr int kLanePos = 32;                        // consecutive window positions per lane
 constexpr uint32_t kSuper = 64 * kLanePos;          // positions per wave super-step
 constexpr int kBlocksPerCU = 1;                     // persistent grid: resident workgroups per CU
@@ -132,6 +133,7 @@ struct SeqSpan {           // per-sequence work description for one search run
 // ---------------------------------------------------------------- handles
 struct Table {
     mp_params prm{};
+    mp_table_options topt{};  // layout choices of the build (all zero = automatic)
     int device = 0;
     uint32_t n_rec = 0;
     uint64_t n_keys = 0, max_bucket = 0, dev_bytes = 0;
@@ -269,7 +271,6 @@ struct Search {
     mp_search_options opt{};     // kernel-path selection (all zero = automatic)
     uint32_t pair_per_cu = 0;    // resident pair_kernel blocks per CU (occupancy query at create)
     uint32_t dense_per_cu = 0;   // resident dense_kernel blocks per CU
-    uint32_t sched_short = 4;    // super-steps per claim in short scans (MP_SCHUNK_SHORT, tuning)
     size_t dense_lds = 0;        // dense_kernel dynamic LDS bytes
     uint64_t n_regrowths = 0;    // list regrowths over the handle's life (tests)
     std::vector<SeqSpan> last_spans;        // spans on the device (a rerun of the same range uploads nothing)
@@ -279,6 +280,9 @@ struct Search {
     unsigned long long* d_hcnt = nullptr;   // h_cnt as the device sees it
     hipEvent_t evd = nullptr;               // the run's completion (polled, not slept on)
     unsigned long long* h_put = nullptr;    // mp_search_put_hits: pinned ring of hit counts in flight
+    hipEvent_t* put_ev = nullptr;           // per ring slot (kPutRing): its count's copy has run (slot reuse)
+    hipEvent_t put_done = nullptr;          // the last put has read the hit list (next enqueue waits)
+    bool put_wait = false;
     uint32_t put_seq = 0;
     bool stage_timing = true;               // events around tail/pair/order too (mp_search_set_stage_timing)
     bool scan_timing = true;                // the scan kernel's own two events (mp_search_set_scan_timing)

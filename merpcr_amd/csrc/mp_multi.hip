@@ -1,5 +1,5 @@
 // Multi-GPU search: one genome's (sequence, k) space split into owned ranges, one range
-// per device, and the per-device sorted hit lists gathered over RCCL (xGMI) into one list.
+// per device, and the per-device sorted hit lists gathered into one list over xGMI.
 //
 // every window position is independent and owned ranges are contiguous in
 // (sequence, k), so the rank-ordered concatenation of the per-device sorted lists is the
@@ -12,9 +12,10 @@
 // Two forms:
 //   * mp_multi_*: one process drives several devices: a host thread per device for the
 //     pack, the searches enqueued and completed from the calling thread (they run
-//     concurrently), then one grouped ncclSend/ncclRecv gatherv into devices[0]
-//     (ncclCommInitAll over distinct devices; a repeated device -- tests on one GPU --
-//     is gathered by device copies instead, as RCCL admits one rank per device).
+//     concurrently), then the copy engines move every device's list into devices[0]
+//     (hipMemcpyPeerAsync on devices[0]'s stream; a repeated device -- tests on one GPU --
+//     takes the very same copies).  A grouped ncclSend/ncclRecv gatherv stays behind
+//     mp_multi_set_gather(MP_GATHER_RCCL), distinct devices only.
 //   * mp_comm_*: one process per GPU (torchrun / MPI style): the caller shares the RCCL
 //     unique id out of band; every rank's last search result is gathered to rank 0.
 #include <rccl/rccl.h>
@@ -49,7 +50,9 @@ struct Multi {
     std::vector<Genome*> gen;
     std::vector<Search*> srch;
     std::vector<hipStream_t> st;
-    std::vector<ncclComm_t> comm;   // empty when a device repeats
+    std::vector<ncclComm_t> comm;   // MP_GATHER_RCCL only (made at its first run)
+    int gather = MP_GATHER_COPY;
+    bool distinct = false;          // no device listed twice
     std::vector<mp_range> rng;      // owned range per device
     std::vector<std::vector<std::pair<uint64_t, uint64_t>>> need;  // per device, per sequence: bases packed
     std::vector<uint64_t> counts;
@@ -193,13 +196,17 @@ MP_EXPORT int mp_multi_create(uint32_t n_dev, const int32_t* devices, void* cons
     if (!rc) {
         std::vector<int> sorted(m->dev);
         std::sort(sorted.begin(), sorted.end());
-        const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-        if (distinct) {
-            m->comm.resize(n_dev);
-            const ncclResult_t r = ncclCommInitAll(m->comm.data(), (int)n_dev, m->dev.data());
-            if (r != ncclSuccess) {
-                m->comm.clear();
-                rc = fail(MP_E_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+        m->distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+        // the gather's copies run on devices[0]'s stream and read the other devices' lists:
+        // direct xGMI reads need peer access from devices[0] (without it HIP stages the copy)
+        (void)hipSetDevice(m->dev[0]);
+        for (uint32_t d = 1; d < n_dev; ++d) {
+            int can = 0;
+            if (m->dev[d] != m->dev[0] && hipDeviceCanAccessPeer(&can, m->dev[0], m->dev[d]) == hipSuccess && can) {
+                const hipError_t e = hipDeviceEnablePeerAccess(m->dev[d], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    rc = fail(MP_E_HIP, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+                (void)hipGetLastError();  // an "already enabled" error is not sticky for later calls
             }
         }
     }
@@ -208,6 +215,24 @@ MP_EXPORT int mp_multi_create(uint32_t n_dev, const int32_t* devices, void* cons
         return rc;
     }
     *out = m;
+    return MP_OK;
+}
+
+MP_EXPORT int mp_multi_set_gather(void* multi, int32_t mode) {
+    Multi* m = (Multi*)multi;
+    if (!m) return fail(MP_E_ARG, "mp_multi_set_gather: null multi");
+    if (mode != MP_GATHER_COPY && mode != MP_GATHER_RCCL) return fail(MP_E_ARG, "mp_multi_set_gather: unknown mode");
+    if (mode == MP_GATHER_RCCL && !m->distinct)
+        return fail(MP_E_ARG, "mp_multi_set_gather: RCCL admits one rank per device (a device is listed twice)");
+    if (mode == MP_GATHER_RCCL && m->comm.empty()) {
+        m->comm.resize(m->dev.size());
+        const ncclResult_t r = ncclCommInitAll(m->comm.data(), (int)m->dev.size(), m->dev.data());
+        if (r != ncclSuccess) {
+            m->comm.clear();
+            return fail(MP_E_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+        }
+    }
+    m->gather = mode;
     return MP_OK;
 }
 
@@ -278,7 +303,7 @@ MP_EXPORT int mp_multi_run(void* multi, uint64_t* n_hits) {
     }
     MP_HIP_CHECK(hipEventRecord(m->e0, m->st[0]));
     uint64_t off = 0;
-    if (!m->comm.empty()) {
+    if (m->gather == MP_GATHER_RCCL) {
         // gatherv over RCCL: devices[0] receives every device's sorted list at its offset
         MP_NCCL_CHECK(ncclGroupStart());
         for (uint32_t d = 0; d < nd; ++d) {
@@ -299,7 +324,10 @@ MP_EXPORT int mp_multi_run(void* multi, uint64_t* n_hits) {
         MP_HIP_CHECK(hipSetDevice(m->dev[0]));
         for (uint32_t d = 1; d < nd; ++d) MP_HIP_CHECK(hipStreamWaitEvent(m->st[0], m->sent[d], 0));
     } else {
-        for (uint32_t d = 0; d < nd; ++d) {  // a repeated device: peer / local copies
+        // the copy engines, one peer copy per device on devices[0]'s stream (xGMI between
+        // distinct devices, a local copy for a repeated one): every run was completed above,
+        // so each list is final; no kernel on the CUs
+        for (uint32_t d = 0; d < nd; ++d) {
             const size_t bytes = m->counts[d] * sizeof(mp_hit);
             if (bytes)
                 MP_HIP_CHECK(hipMemcpyPeerAsync(m->all + off, m->dev[0], m->srch[d]->out, m->dev[d], bytes, m->st[0]));
@@ -504,19 +532,34 @@ MP_EXPORT int mp_ipc_close(void* dev_ptr) {
     return MP_OK;
 }
 
-MP_EXPORT int mp_search_put_hits(void* search, mp_hit* dst, uint64_t cap, uint64_t* count_dst, void* stream) {
+// The count travels from a pinned ring slot (kPutRing per handle); a slot is reused only after
+// the copy that read it has run (its event), and the handle's next run waits on the device for
+// the hit copy (put_done, taken by mp_search_enqueue on whatever stream that run uses).
+MP_EXPORT int mp_search_put_hits(void* search, mp_hit* dst, uint64_t cap, uint64_t* count_dst, uint64_t* n_hits,
+                                 void* stream) {
     Search* s = (Search*)search;
+    if (n_hits) *n_hits = s ? s->n_hits : 0;
     if (!s || !count_dst || (s->n_hits && !dst)) return fail(MP_E_ARG, "mp_search_put_hits: null pointer");
     if (s->pending) return fail(MP_E_STATE, "mp_search_put_hits: a run is enqueued (mp_search_complete first)");
-    if (s->n_hits > cap) return fail(MP_E_CAP, "mp_search_put_hits: region too small");
+    if (s->n_hits > cap) return fail(MP_E_CAP, "mp_search_put_hits: region too small (*n_hits = the need)");
     hipStream_t st = (hipStream_t)stream;
     MP_HIP_CHECK(hipSetDevice(s->genome->device));
-    constexpr uint32_t kPutRing = 64;  // counts in flight (a handle has at most one put queued)
-    if (!s->h_put) MP_HIP_CHECK(hipHostMalloc((void**)&s->h_put, kPutRing * sizeof(unsigned long long), hipHostMallocDefault));
+    if (!s->h_put) {
+        MP_HIP_CHECK(hipHostMalloc((void**)&s->h_put, kPutRing * sizeof(unsigned long long), hipHostMallocDefault));
+        s->put_ev = new hipEvent_t[kPutRing]();
+        for (uint32_t i = 0; i < kPutRing; ++i)
+            MP_HIP_CHECK(hipEventCreateWithFlags(&s->put_ev[i], hipEventDisableTiming));
+        MP_HIP_CHECK(hipEventCreateWithFlags(&s->put_done, hipEventDisableTiming));
+    }
     const uint64_t n = s->n_hits;
     if (n) MP_HIP_CHECK(hipMemcpyAsync(dst, s->out, n * sizeof(mp_hit), hipMemcpyDeviceToDeviceNoCU, st));
-    unsigned long long* c = s->h_put + (s->put_seq++ % kPutRing);
+    MP_HIP_CHECK(hipEventRecord(s->put_done, st));
+    s->put_wait = true;
+    const uint32_t k = s->put_seq++ % kPutRing;
+    if (s->put_seq > kPutRing) MP_HIP_CHECK(hipEventSynchronize(s->put_ev[k]));  // kPutRing puts ago: long done
+    unsigned long long* c = s->h_put + k;
     *c = n;
     MP_HIP_CHECK(hipMemcpyAsync(count_dst, c, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    MP_HIP_CHECK(hipEventRecord(s->put_ev[k], st));
     return MP_OK;
 }

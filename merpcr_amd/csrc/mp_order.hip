@@ -482,12 +482,8 @@ int sort_hits_device(Search* s, hipStream_t st, int mode, bool finish) {
     hipLaunchKernelGGL(bucket_scatter, dim3(grid), dim3(256), 0, st, s->tmp_lo, sort_region_counts(s),
                        s->cap / kHitRegions, P.shift, cursor, s->tmp_hi);
     MP_HIP_CHECK(hipGetLastError());
-    // crowded buckets: MP_CROWD_GRID workgroups (tuning; default one per CU)
-    static const uint32_t crowd_grid = [] {
-        const char* e = std::getenv("MP_CROWD_GRID");
-        return e ? (uint32_t)std::max(1, std::atoi(e)) : 0u;
-    }();
-    const uint32_t cg = crowd_grid ? crowd_grid : (uint32_t)s->n_cu;
+    // crowded buckets: mp_search_options.crowd_grid workgroups (tuning; default one per CU)
+    const uint32_t cg = s->opt.crowd_grid ? (uint32_t)s->opt.crowd_grid : (uint32_t)s->n_cu;
     hipLaunchKernelGGL(bucket_sort_decode, dim3((P.nb + kBucketsPerBlock - 1) / kBucketsPerBlock), dim3(256), 0, st,
                        s->tmp_hi, off, P.nb, P.shift, P.try_bits, P.low_bits,
                        g->d_base, g->d_len, g->n_seq, s->table->rank_rec, s->out, s->d_hcnt);

@@ -2579,6 +2579,12 @@ static void free_search(Search* s) {
     if (s->evd) hipEventDestroy(s->evd);
     if (s->h_cnt) hipHostFree(s->h_cnt);
     if (s->h_put) hipHostFree(s->h_put);
+    if (s->put_ev) {
+        for (uint32_t i = 0; i < kPutRing; ++i)
+            if (s->put_ev[i]) hipEventDestroy(s->put_ev[i]);
+        delete[] s->put_ev;
+    }
+    if (s->put_done) hipEventDestroy(s->put_done);
     delete s;
 }
 
@@ -2644,7 +2650,9 @@ MP_EXPORT int mp_search_set_options(void* search, const mp_search_options* opt) 
     if (s->pending) return fail(MP_E_STATE, "mp_search_set_options: a run is enqueued");
     if (opt->tails < MP_TAILS_AUTO || opt->tails > MP_TAILS_KERNEL || opt->sort < MP_SORT_AUTO ||
         opt->sort > MP_SORT_SCATTER || opt->sort_bucket_bits < 0 || opt->sort_bucket_bits > 16 ||
-        opt->pair_blocks_per_cu < 0)
+        opt->pair_blocks_per_cu < 0 || opt->generic_forms < 0 ||
+        opt->generic_forms > (int32_t)(MP_GENERIC_FIX | MP_GENERIC_GAP | MP_GENERIC_PAIR) || opt->ref32 < 0 ||
+        opt->ref32 > 1 || opt->sched_short < 0 || opt->sched_short > 64 || opt->crowd_grid < 0)
         return fail(MP_E_ARG, "mp_search_set_options: option out of range");
     MP_HIP_CHECK(hipSetDevice(s->genome->device));
     s->opt = *opt;
@@ -2682,7 +2690,6 @@ MP_EXPORT int mp_search_create(void* table, void* genome, void** out) {
                                   (const void*)dense_kernel<2, 0>, (const void*)dense_kernel<-1, 0>})
                 (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s->dense_lds);
         occ = 0;
-        if (const char* e = std::getenv("MP_SCHUNK_SHORT")) s->sched_short = (uint32_t)std::max(1, std::atoi(e));
         s->dense_per_cu = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dense_kernel<1, 2>, kDenseBlock, s->dense_lds) ==
                                hipSuccess && occ > 0) ? (uint32_t)occ : 1u;
         if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess ||
@@ -2808,7 +2815,8 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
             return fail(MP_E_STATE, "gapped seed table without key groups");
         // c5's shape (W = 8, N = 1) with its gap as constants; other W 7..9 shapes from the table
         const bool w8 = t->gap_at == kGapW8At && t->gap_len == kGapW8Len && t->gap_post == kGapW8Post && a.N == 1 &&
-                        t->kgrp_F == kGapW8Len + kGapW8Post && a.W == (int)kSplitSeed && !std::getenv("MP_GAP_GENERIC");
+                        t->kgrp_F == kGapW8Len + kGapW8Post && a.W == (int)kSplitSeed &&
+                        !(s->opt.generic_forms & MP_GENERIC_GAP);
         if (w8 && t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true, kGapW8>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (w8) hipLaunchKernelGGL((scan_kernel<1, false, 1, true, false, true, kGapW8>), dim3(grid), dim3(kBlock), 0, st, a);
         else if (t->lds_k == 2) hipLaunchKernelGGL((scan_kernel<1, false, 2, true, false, true, 1>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -2831,8 +2839,8 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
     const bool rkf4 = scan_uses_kgrp4(s, t, a);
     // the I = 0 key-group scan with its shape as constants (kFix: W = 11, F = 6, N <= 1)
     const int fix = (a.W == (int)kFixW && a.I == 0 && !t->kgrp_wild && t->kgrp_F == kFixF && a.N <= 1 &&
-                     !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
-    const int fix4 = (a.W == (int)kFixW && a.N <= 2 && !std::getenv("MP_FIX_GENERIC")) ? a.N + 1 : 0;
+                     !(s->opt.generic_forms & MP_GENERIC_FIX)) ? a.N + 1 : 0;
+    const int fix4 = (a.W == (int)kFixW && a.N <= 2 && !(s->opt.generic_forms & MP_GENERIC_FIX)) ? a.N + 1 : 0;
     // the forms below that leave key references (kRkf 1 and 2)
     // (16-B references only for the wide key groups: c4 leaves ~16M, whose traffic they halve;
     // c3's 5.5M took 12 us longer in tail_kernel, which looks up the bases left per reference)
@@ -2968,7 +2976,7 @@ static int enqueue_kernels(Search* s, const ScanArgs& a, uint64_t tiles, hipStre
     const uint32_t pair_per_cu = s->opt.pair_blocks_per_cu ? std::min(s->pair_per_cu, (uint32_t)s->opt.pair_blocks_per_cu)
                                                            : s->pair_per_cu;
     const dim3 pg((uint32_t)s->n_cu * pair_per_cu);
-    const bool pgen = std::getenv("MP_PAIR_GENERIC") != nullptr;
+    const bool pgen = (s->opt.generic_forms & MP_GENERIC_PAIR) != 0;
     if (!pgen && a.I == 0 && a.N == 0 && a.X == 1) hipLaunchKernelGGL((pair_kernel<0, 0, 1>), pg, dim3(kPairBlock), 0, st, a);
     else if (!pgen && a.I == 0 && a.N == 1 && a.X == 1) hipLaunchKernelGGL((pair_kernel<0, 1, 1>), pg, dim3(kPairBlock), 0, st, a);
     else if (!pgen && a.I == 1 && a.N == 2 && a.X == 1) hipLaunchKernelGGL((pair_kernel<1, 2, 1>), pg, dim3(kPairBlock), 0, st, a);
@@ -3117,6 +3125,10 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
     if (!g->sealed) return fail(MP_E_STATE, "mp_search_run: genome not sealed (call mp_genome_seal)");
     hipStream_t st = (hipStream_t)stream;
     MP_HIP_CHECK(hipSetDevice(g->device));
+    if (s->put_wait) {  // a put of the last run's hits may still be reading them (any stream)
+        MP_HIP_CHECK(hipStreamWaitEvent(st, s->put_done, 0));
+        s->put_wait = false;
+    }
     mp_range r{0, g->n_seq, 0, 0};
     if (range) r = *range;
     if (r.seq_begin > r.seq_end || r.seq_end > g->n_seq)
@@ -3209,13 +3221,13 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         a.M = t->prm.margin; a.N = t->prm.mismatches;
         a.X = t->prm.three_prime_match; a.I = t->prm.iupac_mode;
         a.g_lo = g_lo; a.g_hi = g_hi;
-        a.sched_short = s->sched_short;
+        a.sched_short = s->opt.sched_short ? (uint32_t)s->opt.sched_short : (uint32_t)MP_SCHUNK_SHORT;
         // the scan grid's static bucket-tail slots (launch_scan's grid; a dense scan has none,
         // and its run launches no tail pass)
         a.tail_static = (uint64_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU) *
                         kWaves * kStaticRefs;
         // 16-B key references need the position in 40 bits and the sequence in 23 (ref16_make)
-        a.ref16 = (g->total < (1ull << 40) && g->n_seq + 1u < (1u << 23) && !std::getenv("MP_REF32")) ? 1u : 0u;
+        a.ref16 = (g->total < (1ull << 40) && g->n_seq + 1u < (1u << 23) && !s->opt.ref32) ? 1u : 0u;
         // keys over 64 bits, or a forced rocPRIM sort: mode 2
         const int mode = run_order_mode(s);
         s->pend_mode = mode;

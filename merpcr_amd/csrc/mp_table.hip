@@ -109,9 +109,10 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                        const uint32_t* hash_off, const uint64_t* pcr_size, const uint8_t* primer1,
                        const uint64_t* p1_off, const uint8_t* primer2, const uint64_t* p2_off,
                        const uint32_t* rec_map, uint32_t gap_at, uint32_t gap_len, uint32_t gap_post,
-                       Table** table_out) {
+                       const mp_table_options& topt, Table** table_out) {
     Table* t = new Table();
     t->prm = p;
+    t->topt = topt;
     t->device = device;
     t->n_rec = n_rec;
     t->gap_at = gap_at;
@@ -168,9 +169,9 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         std::vector<uint32_t> lfilt(kLdsFilterWords, 0);
         const bool blocked = !t->lds_exact && t->filt_direct;  // W 11..13: lds_block_mask
         t->lds_k = blocked && nb > kLdsK2Keys ? 2 : 1;
-        // MP_LDS_K=1..3 forces the bits per key (the level-1 A/B of DESIGN 4.2; the scan
-        // launches k = 3 only on its key-group and 16-B-head paths)
-        if (const char* e = std::getenv("MP_LDS_K"); e && blocked) t->lds_k = std::min(3, std::max(1, std::atoi(e)));
+        // mp_table_options.lds_k 1..3 forces the bits per key (the level-1 A/B of DESIGN 4.2; the
+        // scan launches k = 3 only on its key-group and 16-B-head paths)
+        if (topt.lds_k && blocked) t->lds_k = std::min(3, std::max(1, (int)topt.lds_k));
         for (uint32_t b = 0; b < nb; ++b) {
             const uint32_t idx = lds_bit(bkey[b], W, t->lds_exact);
             if (blocked) {
@@ -442,10 +443,10 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
             }
             // 16-B heads when they make the deferring drain possible (full heads under 5%) and
             // the 8-B heads do not (c4: 10% IUPAC primer bases); held in the 8-B IUPAC form when
-            // that keeps full heads under 5% too (MP_NO_H12=1: the 16-B form, for A/B runs)
+            // that keeps full heads under 5% too (mp_table_options.no_h12: the 16-B form, A/B)
             t->h16 = W >= 10 && n_full16 * 20 < (uint64_t)nb && n_full8 * 20 >= (uint64_t)nb;
             t->h12 = t->h16 && n_full12 * 20 < (uint64_t)nb;
-            if (const char* e = std::getenv("MP_NO_H12"); e && std::atoi(e)) t->h12 = 0;
+            if (topt.no_h12) t->h12 = 0;
             if (t->h16 && !t->h12) dents16.resize(std::max<uint32_t>(nb, 1));
             std::vector<uint2> dents12;
             if (t->h12) dents12.resize(std::max<uint32_t>(nb, 1));
@@ -591,10 +592,9 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
                 // present key of its group) always passes.  Taken when fewer than a quarter of
                 // a random window's seeds would pass (c4: ~0.12 with the keys without a field
                 // counted, against ~0.30 for the 8-B fields)
-                // MP_NO_KGRP4 (A/B runs and tests): 1 = never, -1 = whenever the table can
-                // carry them (the pass-rate estimate skipped)
-                const char* no4 = std::getenv("MP_NO_KGRP4");
-                const int no4v = no4 ? std::atoi(no4) : 0;
+                // mp_table_options.kgrp4 (A/B runs and tests): 1 = never, -1 = whenever the
+                // table can carry them (the pass-rate estimate skipped)
+                const int no4v = topt.kgrp4;
                 if (!t->kgrp_wild && t->h12 && t->defer_full && no4v <= 0) {
                     const uint32_t F4 = kKgrp4F;
                     const uint64_t seedm = sp_lt((int)W);
@@ -765,7 +765,7 @@ static int build_split(Table* t, uint32_t n_rec, const uint32_t* key, const uint
     const mp_params& p = t->prm;
     const uint32_t W = (uint32_t)p.wordsize;
     if (W < 7 || W > 9 || p.iupac_mode != 0 || p.mismatches > 1 || n_rec == 0) return MP_OK;
-    if (const char* e = std::getenv("MP_NO_SPLIT"); e && std::atoi(e)) return MP_OK;
+    if (t->topt.no_split) return MP_OK;
     const uint32_t S = split_span(W), A = kSplitSeed - W;  // span of the cut stretch, bases of A (= of B)
     const uint32_t need = p.mismatches ? S + split_post(W) : kSplitSeed;
     auto code = [](uint8_t c) -> int {
@@ -815,7 +815,7 @@ static int build_split(Table* t, uint32_t n_rec, const uint32_t* key, const uint
         q.wordsize = (int32_t)w;
         return build_table(q, t->device, (uint32_t)s.key.size(), s.key.data(), s.hoff.data(), s.size.data(),
                            s.b1.data(), s.o1.data(), s.b2.data(), s.o2.data(), s.map.data(), gap_at, gap_len,
-                           gap_post, out);
+                           gap_post, t->topt, out);
     };
     int rc = MP_OK;
     {
@@ -842,7 +842,19 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
                               const uint64_t* pcr_size, const uint8_t* primer1,
                               const uint64_t* p1_off, const uint8_t* primer2,
                               const uint64_t* p2_off, void** table_out) {
+    return mp_table_create_ex(prm, device, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off, nullptr,
+                              table_out);
+}
+
+MP_EXPORT int mp_table_create_ex(const mp_params* prm, int32_t device, uint32_t n_rec,
+                                 const uint32_t* key, const uint32_t* hash_off,
+                                 const uint64_t* pcr_size, const uint8_t* primer1,
+                                 const uint64_t* p1_off, const uint8_t* primer2,
+                                 const uint64_t* p2_off, const mp_table_options* options, void** table_out) {
     if (!prm || !table_out) return fail(MP_E_ARG, "mp_table_create: null pointer");
+    const mp_table_options topt = options ? *options : mp_table_options{};
+    if (topt.lds_k < 0 || topt.lds_k > 3 || topt.kgrp4 < -1 || topt.kgrp4 > 1)
+        return fail(MP_E_ARG, "mp_table_create_ex: option out of range");
     *table_out = nullptr;
     const mp_params& p = *prm;
     if (p.wordsize < 3 || p.wordsize > 16) return fail(MP_E_ARG, "Word size must be between 3 and 16");
@@ -855,7 +867,8 @@ MP_EXPORT int mp_table_create(const mp_params* prm, int32_t device, uint32_t n_r
     if (n_rec && (!key || !hash_off || !pcr_size || !primer1 || !p1_off || !primer2 || !p2_off))
         return fail(MP_E_ARG, "mp_table_create: null record array");
     Table* t = nullptr;
-    int rc = build_table(p, device, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off, nullptr, 0, 0, 0, &t);
+    int rc = build_table(p, device, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off, nullptr, 0, 0, 0,
+                         topt, &t);
     if (rc) return rc;
     rc = build_split(t, n_rec, key, hash_off, pcr_size, primer1, p1_off, primer2, p2_off);
     if (rc) {

@@ -85,66 +85,127 @@ def native_comm(device: int, group=None):
 class IpcGather:
     """Hit gather to rank 0 by the copy engines, for one process per GPU on one node.
 
-    Rank 0 allocates ``world`` fixed regions of ``cap`` hits (the largest any rank asks for)
-    and ``world`` count words in its
-    HBM and exports both (mp_ipc_handle); torch.distributed (any backend: the control plane)
-    carries the handles; every other rank maps them on its own device (mp_ipc_open).  After a
-    completed run, ``put`` copies the run's hits into this rank's region and its count into
-    this rank's word on the given stream (mp_search_put_hits: no kernel on the CUs, no
-    collective, no host synchronisation between ranks).  After the ranks' streams are
-    synchronised and a barrier, rank 0's ``hits()`` is the rank-ordered concatenation (the
-    contig-shard sequence shift applied there, so no rank's own list is modified).
-    Collective to create (every rank), like the RCCL communicator it stands beside."""
+    Rank 0 allocates ``slots`` x ``world`` fixed regions of ``cap`` hits (the largest any rank
+    asks for) and as many count words in its HBM and exports both (mp_ipc_handle);
+    torch.distributed (any backend: the control plane) carries the handles; every other rank
+    maps them on its own device (mp_ipc_open).  After a completed run, ``put`` copies the run's
+    hits into this rank's region of the given slot and its count into the slot's word, on the
+    given stream (mp_search_put_hits: no kernel on the CUs, no collective, no host
+    synchronisation between ranks).  Pipelined search handles each put into a slot of their
+    own, so no two streams of a rank ever write one region.  A run with more hits than ``cap``
+    is not copied; ``settle`` (collective, after the ranks' streams are synchronised) then
+    regrows every region to twice the largest need and every rank puts each slot's last run
+    again.  Rank 0's ``hits(slot)`` is then the rank-ordered concatenation (the contig-shard
+    sequence shift applied there, so no rank's own list is modified).  Collective to create
+    (every rank), like the RCCL communicator it stands beside; a failure to export or to map
+    raises on every rank, after the handles' broadcast."""
 
-    def __init__(self, device: int, cap: int, group=None):
-        import torch
+    def __init__(self, device: int, cap: int, group=None, slots: int = 1):
         import torch.distributed as dist
-        from . import _native
+        self.device, self.group, self.slots = device, group, max(1, int(slots))
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         caps = [None] * self.world  # one region size for every rank: the largest asked for
         dist.all_gather_object(caps, int(cap), group=group)
         self.cap = max(caps)
         self._opened = []
         self._buf = self._cnt = None
+        self._last = {}   # slot -> (search, stream) of this rank's last put there
+        self._need = 0    # the largest count a put of this rank could not copy (0: none)
+        self.regrowths = 0
+        self._map()
+
+    def _map(self):
+        """Rank 0 allocates and exports; the others map.  An export failure travels in the
+        broadcast itself, so every rank leaves the collective before raising it."""
+        import torch
+        import torch.distributed as dist
+        from . import _native
         if self.rank == 0:
-            dev = torch.device("cuda", device)
-            self._buf = torch.empty(self.world * self.cap * HIT_BYTES, dtype=torch.uint8, device=dev)
-            self._cnt = torch.zeros(self.world, dtype=torch.int64, device=dev)
-            obj = [(_native.ipc_handle(self._buf.data_ptr()), _native.ipc_handle(self._cnt.data_ptr()))]
+            try:
+                dev = torch.device("cuda", self.device)
+                n = self.slots * self.world
+                self._buf = torch.empty(n * self.cap * HIT_BYTES, dtype=torch.uint8, device=dev)
+                self._cnt = torch.zeros(n, dtype=torch.int64, device=dev)
+                obj = [("ok", (_native.ipc_handle(self._buf.data_ptr()), _native.ipc_handle(self._cnt.data_ptr())))]
+            except Exception as e:  # noqa: BLE001 -- re-raised on every rank below
+                obj = [("err", f"rank 0 could not export its gather buffers: {type(e).__name__}: {e}")]
         else:
             obj = [None]
-        dist.broadcast_object_list(obj, src=0, group=group)
+        dist.broadcast_object_list(obj, src=0, group=self.group)
+        kind, payload = obj[0]
+        if kind == "err":
+            raise RuntimeError(payload)
         if self.rank == 0:
-            base, cnt = self._buf.data_ptr(), self._cnt.data_ptr()
+            self._base, self._cbase = self._buf.data_ptr(), self._cnt.data_ptr()
         else:  # each handle maps its whole allocation: add the tensor's offset in it
-            (hb, ob), (hc, oc) = obj[0]
-            mb = _native.ipc_open(hb, device)
+            (hb, ob), (hc, oc) = payload
+            mb = _native.ipc_open(hb, self.device)
             self._opened.append(mb)
-            mc = _native.ipc_open(hc, device)
+            mc = _native.ipc_open(hc, self.device)
             self._opened.append(mc)
-            base, cnt = mb + ob, mc + oc
-        self.region = base + self.rank * self.cap * HIT_BYTES
-        self.count = cnt + self.rank * 8
+            self._base, self._cbase = mb + ob, mc + oc
 
-    def put(self, search, stream=None):
-        search.put_hits(self.region, self.cap, self.count, stream)
+    def _region(self, slot: int):
+        i = slot * self.world + self.rank
+        return self._base + i * self.cap * HIT_BYTES, self._cbase + i * 8
 
-    def hits(self, seq_shifts=None):
-        """Rank 0: the rank-ordered hit bytes (a torch uint8 tensor on its device), rank r's
-        sequence indices plus seq_shifts[r] (contig shards)."""
+    def put(self, search, stream=None, slot: int = 0) -> bool:
+        """This rank's last run of `search` into its region of `slot`.  False: more hits than
+        the region holds (nothing copied; ``settle`` regrows and puts it again)."""
+        from . import _native
+        self._last[slot] = (search, stream)
+        region, count = self._region(slot)
+        try:
+            search.put_hits(region, self.cap, count, stream)
+        except _native.NativeError as e:
+            if e.code != _native.MP_E_CAP:
+                raise
+            self._need = max(self._need, e.need)
+            return False
+        return True
+
+    def settle(self) -> bool:
+        """Collective, after every rank synchronised the streams of its puts: if any rank's put
+        did not fit, regrow the regions to twice the largest need and put every slot's last run
+        again (the handles must still hold those runs).  True when a regrow happened."""
         import torch
-        n = self._cnt.cpu().tolist()
+        import torch.distributed as dist
+        needs = [None] * self.world
+        dist.all_gather_object(needs, int(self._need), group=self.group)
+        if max(needs) <= self.cap:
+            return False
+        self.close()                                # every rank unmaps the old buffers ...
+        dist.barrier(group=self.group)              # ... before rank 0 frees them
+        self._buf = self._cnt = None
+        self.cap = 2 * max(needs)
+        self._need = 0
+        self._map()
+        for slot, (search, stream) in sorted(self._last.items()):
+            self.put(search, stream, slot)
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+        self.regrowths += 1
+        return True
+
+    def hits(self, seq_shifts=None, slot: int = 0):
+        """Rank 0: the rank-ordered hit bytes of `slot` (a torch uint8 tensor on its device),
+        rank r's sequence indices plus seq_shifts[r] (contig shards)."""
+        import torch
+        n = self.counts(slot)
         parts = []
         for r in range(self.world):
-            part = self._buf[r * self.cap * HIT_BYTES:(r * self.cap + n[r]) * HIT_BYTES].clone()
+            at = (slot * self.world + r) * self.cap
+            part = self._buf[at * HIT_BYTES:(at + n[r]) * HIT_BYTES].clone()
             if seq_shifts and seq_shifts[r] and n[r]:
                 # mp_hit = {u64 pos1, u64 pos2, u32 seq, u32 rec}: seq is int32 word 4 of 6
                 part.view(torch.int32).view(n[r], HIT_BYTES // 4)[:, 4] += int(seq_shifts[r])
             parts.append(part)
         return torch.cat(parts)
 
-    def counts(self):
-        return self._cnt.cpu().tolist() if self._cnt is not None else None
+    def counts(self, slot: int = 0):
+        if self._cnt is None:
+            return None
+        return self._cnt[slot * self.world:(slot + 1) * self.world].cpu().tolist()
 
     def close(self):
         from . import _native

@@ -98,7 +98,7 @@ def main():
             kw = {}
             for item in v[4:].split(","):
                 k, val = item.split("=")
-                kw[k] = val if k in ("tails", "sort") else int(val)
+                kw[k] = val if k in ("tails", "sort", "generic") else int(val)
             s.set_options(**kw)
         from merpcr_amd.dist import shard_ranges
         rng = shard_ranges(lens, args.shard_of)[0] if args.shard_of > 1 else None

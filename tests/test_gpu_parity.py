@@ -573,8 +573,9 @@ def test_sharded_ranges_all_paths(W, n_sts, opts):
 @pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0, 0]])
 def test_multi_device_engine_matches_single(devices):
     """MerPCR(devices=[...]) / CLI --gpus: owned ranges over the devices, each packing only
-    its share of the genome, gathered into devices[0]; identical to one device.  (One GPU
-    here: a repeated device takes the device-copy gather, RCCL admitting one rank per GPU.)"""
+    its share of the genome, gathered into devices[0] by the copy engines (hipMemcpyPeerAsync
+    on devices[0]'s stream); identical to one device.  A repeated device (one GPU here) takes
+    the same gather code as distinct devices do (mp_multi_run has one copy path)."""
     sts_text, seqs = _multi_case(11, 6000, 41)
     recs = [FASTARecord(defline=f">m{i}", sequence=s) for i, s in enumerate(seqs)]
     single = MerPCR(wordsize=11, mismatches=1)
@@ -590,8 +591,9 @@ def test_multi_device_engine_matches_single(devices):
 
 
 def test_multi_rccl_gather_one_device():
-    """mp_multi over one device: the RCCL communicator path (ncclCommInitAll, grouped
-    ncclSend/ncclRecv to itself) gathers the hit list."""
+    """mp_multi over one device with the gather switched to RCCL (mp_multi_set_gather:
+    ncclCommInitAll, grouped ncclSend/ncclRecv to itself) gathers the hit list; a repeated
+    device refuses it (RCCL admits one rank per device)."""
     from merpcr_amd import _native
     sts_text, seqs = _multi_case(11, 3000, 43)
     eng = MerPCR(wordsize=11, mismatches=1)
@@ -600,6 +602,7 @@ def test_multi_rccl_gather_one_device():
     data = eng.encode_sequences(seqs)
     exp = eng.find_hits([FASTARecord(defline=f">m{i}", sequence=s) for i, s in enumerate(seqs)])
     m = _native.Multi([0], [eng.device_table()])
+    m.set_gather("rccl")
     m.genome([len(d) for d in data])
     for i, d in enumerate(data):
         if len(d):
@@ -608,6 +611,10 @@ def test_multi_rccl_gather_one_device():
     got = m.fetch(m.run())
     assert len(exp) > 100 and got.tobytes() == exp.tobytes()
     m.close()
+    rep = _native.Multi([0, 0], [eng.device_table(), eng.device_table()])
+    with pytest.raises(ValueError):
+        rep.set_gather("rccl")
+    rep.close()
 
 
 def test_comm_gather_single_rank():
@@ -660,9 +667,11 @@ def _two_rank_worker(rank, world, port, sts_text, seqs, q):
     dist.destroy_process_group()
 
 
-def _two_rank_ipc_worker(rank, world, port, sts_text, seqs, q, steps):
+def _two_rank_ipc_worker(rank, world, port, sts_text, seqs, q, steps, cap0=0):
     """One rank of the copy-engine gather (merpcr_amd.dist.IpcGather): `steps` runs of its
-    owned range, each put into rank 0's region on the run's stream, as bench.py does."""
+    owned range on two pipelined handles, each put into rank 0's region slot of its handle on
+    the run's stream, as bench.py does.  cap0 > 0: regions of cap0 hits, too small, so every
+    put fails with MP_E_CAP and settle() must regrow them."""
     import torch
     import torch.distributed as dist
     from merpcr_amd import _native
@@ -679,28 +688,35 @@ def _two_rank_ipc_worker(rank, world, port, sts_text, seqs, q, steps):
         if len(d):
             genome.put(i, d)
     genome.seal()
-    s = _native.Search(eng.device_table(), genome)
+    hs = [_native.Search(eng.device_table(), genome) for _ in range(2)]
     rng = shard_ranges([len(d) for d in data], world)[rank]
-    n = s.run(rng)
-    g = IpcGather(0, max(64, 2 * n))
-    st = torch.cuda.Stream()
-    for _ in range(steps):
-        s.enqueue(rng, st.cuda_stream)
-        s.complete()
-        g.put(s, st.cuda_stream)
-    st.synchronize()
+    n = hs[0].run(rng)
+    g = IpcGather(0, cap0 or max(64, 2 * n), slots=2)
+    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    fits = []
+    for i in range(steps):
+        j = i % 2
+        hs[j].enqueue(rng, sts[j].cuda_stream)
+        hs[j].complete()
+        fits.append(g.put(hs[j], sts[j].cuda_stream, slot=j))
+    torch.cuda.synchronize()
     dist.barrier()
+    grown = g.settle()
+    last = (steps - 1) % 2
     if rank == 0:
-        q.put((g.counts(), g.hits().cpu().numpy().tobytes()))
+        q.put((g.counts(last), g.hits(slot=last).cpu().numpy().tobytes(), grown, fits, g.cap))
     g.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_ranks_ipc_gather_on_one_gpu():
+@pytest.mark.parametrize("cap0", [0, 8])
+def test_two_ranks_ipc_gather_on_one_gpu(cap0):
     """bench.py's default N > 1 gather (copy-engine puts into rank 0's regions, mapped by IPC
-    in the other process): two processes on cuda:0, three pipelined-style steps each; rank 0's
-    rank-ordered regions equal the whole-genome HIP list and the C oracle's."""
+    in the other process): two processes on cuda:0, three steps each on two pipelined handles
+    with a region slot each; rank 0's rank-ordered regions equal the whole-genome HIP list and
+    the C oracle's.  cap0 = 8: every put overflows (MP_E_CAP, nothing copied) and the
+    collective settle() regrows the regions and puts each slot's last run again."""
     import socket
     import torch.multiprocessing as tmp
     from oracle import c_oracle as C
@@ -711,10 +727,10 @@ def test_two_ranks_ipc_gather_on_one_gpu():
     s.close()
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_two_rank_ipc_worker, args=(r, 2, port, sts_text, seqs, q, 3)) for r in range(2)]
+    procs = [ctx.Process(target=_two_rank_ipc_worker, args=(r, 2, port, sts_text, seqs, q, 3, cap0)) for r in range(2)]
     for p in procs:
         p.start()
-    counts, got = q.get(timeout=240)
+    counts, got, grown, fits, cap = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
     eng = MerPCR(wordsize=11, mismatches=1)
@@ -726,6 +742,10 @@ def test_two_ranks_ipc_gather_on_one_gpu():
     assert len(whole) > 100 and sum(counts) == len(whole) and min(counts) > 0
     assert got == whole.tobytes() == ref.tobytes()
     assert all(p.exitcode == 0 for p in procs)
+    if cap0:
+        assert grown and not any(fits) and cap >= max(counts), (grown, fits, cap, counts)
+    else:
+        assert not grown and all(fits)
 
 
 def test_two_ranks_on_one_gpu():
@@ -806,12 +826,12 @@ def test_iupac_wide_key_groups_with_genome_ambiguity():
 
 @pytest.mark.parametrize("W,N,iupac,n_sts", [(11, 2, 0.1, 30000), (11, 2, 0.1, 100000), (11, 1, 0.3, 30000),
                                              (12, 2, 0.1, 40000), (13, 2, 0.1, 40000), (13, 2, 0.2, 40000)])
-def test_wide_key_groups_vs_rank_heads(W, N, iupac, n_sts, monkeypatch):
+def test_wide_key_groups_vs_rank_heads(W, N, iupac, n_sts):
     """The I = 1 scan through the wide key groups (kgrp4, the default for c4-shaped tables)
-    and through the rank words and 8-B IUPAC heads (MP_NO_KGRP4=1, read when the table is
-    built) give the C oracle's hit list byte for byte: primers with IUPAC bases after the
+    and through the rank words and 8-B IUPAC heads (table option kgrp4="never") give the C
+    oracle's hit list byte for byte: primers with IUPAC bases after the
     seed, short primers (fields past the primer's end), multi-record keys, groups with more
-    than three present keys, N runs and planted amplicons.  MP_NO_KGRP4=-1 builds the wide key
+    than three present keys, N runs and planted amplicons.  kgrp4="always" builds the wide key
     groups whenever the table can carry them (the pass-rate estimate skipped); a table that
     takes the I = 1 8-B fields instead (kgrp_wild) is checked on that path in both runs.
     100k STS at W = 11 (c4's table): ~6% of the groups hold four or more keys and ~2% of the
@@ -836,9 +856,9 @@ def test_wide_key_groups_vs_rank_heads(W, N, iupac, n_sts, monkeypatch):
     ref = C.search(table, [g], O.params(**prm), 8)
     assert len(ref) > 100
     lays = []
-    for no4 in ("-1", "1"):
-        monkeypatch.setenv("MP_NO_KGRP4", no4)
+    for no4 in ("always", "never"):
         eng = MerPCR(**prm)
+        eng.table_options = {"kgrp4": no4}
         with tempfile.TemporaryDirectory() as td:
             assert _load_sts(eng, sts.text(), td)
         hits = eng.find_hits([FASTARecord(defline=">chrK", sequence=seq)])

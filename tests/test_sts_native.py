@@ -218,7 +218,9 @@ def test_primer_edit_in_place_keeps_load_time_key(tmp_path):
     after = eng._table_arrays()
     assert after[0].tolist() == before
     assert after[1].tolist()[0] == r0.hash_offset
-    # a record the caller adds to sts_records alone is keyed as the loader would key it
+    # a record the caller adds to sts_records alone is keyed as the loader would key it (a
+    # deliberate extension, engine._record_keys: the reference, walking only sts_table, would
+    # never report it -- this pins the engine's behaviour, it is not a parity claim)
     from merpcr_amd.core.models import STSRecord
     extra = STSRecord(id="C", primer1="TTTTAAAACCCCG", primer2="ACGTACGTAC", pcr_size=100, alias="",
                       offset=3, hash_offset=0, direct="+")
