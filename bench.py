@@ -176,7 +176,7 @@ def live_pmc(argv, kernel_regex: str, timeout_s: float = 150.0):
         files = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
         if not files:
             return None, "pass trace: no kernel-trace CSV"
-        ctr.update(trace_stage_ns(files[0]))
+        ctr.update(trace_stage_ns(files[0], kernel_regex))
     missing = [c for _, cs in PMC_PASSES for c in cs if c not in ctr]
     if missing:
         return None, f"counters missing from the passes: {missing}"
@@ -187,16 +187,19 @@ def live_pmc(argv, kernel_regex: str, timeout_s: float = 150.0):
 TRACE_STEPS = 8
 
 
-def trace_stage_ns(csv_path: str) -> dict:
-    """The scan stage's duration per search step from a rocprofv3 kernel-trace CSV: each kernel
-    form's dispatches averaged (the first dispatch of each form, a cold start, left out when
-    there are more), the forms of a step summed (a split W 7..9 table scans two or three
+def trace_stage_ns(csv_path: str, kernel_regex: str) -> dict:
+    """The scan stage's duration per search step from a rocprofv3 kernel-trace CSV (the trace
+    holds every kernel of the process; the stage's are those matching kernel_regex): each
+    kernel form's dispatches averaged (the first dispatch of each form, a cold start, left out
+    when there are more), the forms of a step summed (a split W 7..9 table scans two or three
     forms one after another).  The forms' dispatch counts and medians are kept beside it."""
     import collections
     import csv
+    import re
     dur = collections.defaultdict(list)
     for r in csv.DictReader(open(csv_path)):
-        dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        if re.search(kernel_regex, r["Kernel_Name"]):
+            dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     total, forms = 0.0, {}
     for name, v in dur.items():
         use = v[1:] if len(v) > 1 else v

@@ -1671,7 +1671,11 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     const uint32_t g_at = kGC ? kGapW8At : a.gap_at, g_len = kGC ? kGapW8Len : a.gap_len;
     const uint32_t g_post = kGC ? kGapW8Post : a.gap_post;
     __shared__ uint32_t s_lf[kLdsFilterWords];
-    __shared__ WaveLds s_wl[kWaves];
+    // the per-wave lists: the key-group forms (kRkf) use only the offset list rq.q (680 B per
+    // wave of the 2,040): 21 KB of the CU's LDS stay free beside the scan block, for a later
+    // step's bucket-tail or order blocks to run on the same CU
+    constexpr uint32_t kWlBytes = kRkf ? (uint32_t)((kSeedQR * sizeof(uint16_t) + 15u) & ~15u) : (uint32_t)sizeof(WaveLds);
+    __shared__ __attribute__((aligned(16))) uint8_t s_wl_raw[kWaves * kWlBytes];
 
     zero_sort_counts(a);
     // stage the seed prefilter in LDS (once per persistent workgroup): all eight 16-B loads of
@@ -1694,7 +1698,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     const uint64_t n_supers = a.spans[a.n_spans].super0;
     const uint32_t W = kFix ? kFixW : (uint32_t)a.W;
     const uint32_t shw = 32u - 2u * W;
-    WaveLds& L = s_wl[w];
+    WaveLds& L = *reinterpret_cast<WaveLds*>(s_wl_raw + (uint32_t)w * kWlBytes);
     uint32_t ncand = 0;
     SurvChunk C{0, kChunkNone, 0u};
     // the wave's first kStaticRefs bucket-tail slots are its own, [gwave * kStaticRefs, + kStaticRefs):
@@ -2247,7 +2251,10 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
 // 1024-thread blocks, two per CU: each block's survivors leave with one returning atomic on
 // the survivor counter per flush, and those serialise at one address (~11 ns each), so
 // 512 blocks where 2,048 smaller ones spent ~20 us on them at the kernel's end.
-constexpr uint32_t kTailBlock = 1024;
+#ifndef MP_TAIL_BLOCK
+#define MP_TAIL_BLOCK 1024
+#endif
+constexpr uint32_t kTailBlock = MP_TAIL_BLOCK;
 #ifndef MP_TAIL_BUF
 #define MP_TAIL_BUF 4096
 #endif

@@ -53,3 +53,24 @@ def test_mismatch_exits_before_any_gpu_work():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_trace_stage_time_filters_the_scan_forms(tmp_path):
+    """roofline's time: the kernel-trace pass holds every kernel of the child process; only the
+    scan stage's forms count, each averaged without its first (cold) dispatch, forms summed."""
+    import csv
+    import bench
+    p = tmp_path / "kernel_trace.csv"
+    with open(p, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        for i, d in enumerate([9000, 2000, 2200]):
+            w.writerow(["void mp::scan_kernel<1, false>(mp::ScanArgs)", 10 * i, 10 * i + d])
+        for d in [5000, 700, 900]:
+            w.writerow(["void mp::scan_kernel<1, false, 8>(mp::ScanArgs)", 0, d])
+        w.writerow(["void at::native::vectorized_elementwise_kernel<4>", 0, 10 ** 9])
+        w.writerow(["void mp::tail_kernel<false>(mp::ScanArgs)", 0, 10 ** 6])
+    got = bench.trace_stage_ns(str(p), "scan_kernel|dense_kernel")
+    assert got["_trace_stage_ns"] == 2100 + 800
+    assert sorted(got["_trace_forms"]) == ["void mp::scan_kernel<1, false, 8>(mp::ScanArgs)",
+                                           "void mp::scan_kernel<1, false>(mp::ScanArgs)"]
