@@ -2319,40 +2319,28 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
     const uint2* kref_heads = kH12 ? a.dents12 : a.dents8;
     const uint64_t stride = (uint64_t)gridDim.x * kTailBlock;
     uint32_t it = 0, next_check = 0, period = 1, fill0 = 0;  // buffer checks (block-uniform)
-    // 16-B references, software-pipelined two deep (round 6): at the top of pass p the
-    // reference of pass p + 1 (vnext) and the rank word of pass p's (rwnext) have landed; pass p
-    // issues its head, the rank word of pass p + 1, the reference of pass p + 2 (vnext2) and its
-    // own sequence tables in one batch, so a pass whose bucket head is compact costs one round
-    // trip.  Round 5 chained reference -> tables -> rank word -> head: three.
-    uint4 vnext = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), vnext2 = vnext;
+    // 16-B references: the next pass's reference is loaded at the top of this pass, so its
+    // latency hides behind this pass's dependent loads (rank word, head, entries)
+    // and the reference's rank word is loaded at the end of the pass before (one dependent
+    // load fewer on each pass's chain)
+    uint4 vnext = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
     uint2 rwnext = make_uint2(0u, 0u);
-    if (kRef16 && kTailPrefetch) {
-        const uint64_t i0 = (uint64_t)blockIdx.x * kTailBlock + threadIdx.x;
-        if (i0 < n_refs) vnext = a.tails[i0];
-        if (i0 + stride < n_refs) vnext2 = a.tails[i0 + stride];
-        rwnext = a.rk[ref16_key<kGap>(a, vnext) >> 5];  // a padding reference reads word 0, unused
+    if (kRef16 && kTailPrefetch && (uint64_t)blockIdx.x * kTailBlock + threadIdx.x < n_refs) {
+        vnext = a.tails[(uint64_t)blockIdx.x * kTailBlock + threadIdx.x];
+        if (!(vnext.x == 0xFFFFFFFFu && vnext.y == 0xFFFFFFFFu)) rwnext = a.rk[ref16_key<kGap>(a, vnext) >> 5];
     }
     for (uint64_t b = (uint64_t)blockIdx.x * kTailBlock; b < n_refs; b += stride, ++it) {  // block-uniform
         const uint64_t i = b + threadIdx.x;
         uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u), w = make_uint4(0u, 0u, 0u, 0u);
         uint2 rwpre = make_uint2(0u, 0u);  // the rank word of v, loaded the pass before
-        uint2 cpre = make_uint2(0u, 0u);   // v's bucket head, issued beside the sequence-table loads
         if (kRef16) {
             // 16-B key reference (ref16_make) -> the 32-B form's fields: the bases left from the
             // sequence tables, the window's exception bits from the genome when flagged
             if constexpr (kTailPrefetch) {
-                // Every load of the batch is issued on every path (clamped index; a padding
-                // reference's head and rank word are read and ignored): a conditional issue would
-                // make the compiler's merged wait vmcnt(0), and counters retire in order.
                 v = vnext;
                 rwpre = rwnext;
-                const uint32_t h = ref16_key<kGap>(a, v);
-                cpre = kref_heads[rwpre.y + (uint32_t)__popc(rwpre.x & ((1u << (h & 31u)) - 1u))];
-                vnext = vnext2;
-                rwnext = a.rk[ref16_key<kGap>(a, vnext) >> 5];
-                const bool more = i + 2 * stride < n_refs;
-                vnext2 = a.tails[more ? i + 2 * stride : 0u];
-                if (!more) vnext2 = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+                vnext = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+                if (i + stride < n_refs) vnext = a.tails[i + stride];
             } else if (i < n_refs) {
                 v = a.tails[i];
             }
@@ -2379,13 +2367,8 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 const uint32_t W = (uint32_t)a.W;
                 const uint32_t h = kGap ? gap_key((uint32_t)(Gs >> 32), a.gap_at, a.gap_len) >> (32u - 2u * W)
                                         : (uint32_t)(Gs >> (64u - 2u * W));
-                uint2 c;
-                if constexpr (kRef16 && kTailPrefetch) {
-                    c = cpre;
-                } else {
-                    const uint2 rw = a.rk[h >> 5];
-                    c = kref_heads[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
-                }
+                const uint2 rw = (kRef16 && kTailPrefetch) ? rwpre : a.rk[h >> 5];
+                const uint2 c = kref_heads[rw.y + (uint32_t)__popc(rw.x & ((1u << (h & 31u)) - 1u))];
                 if (c.y & kHead8Full) {
                     first = c.x;  // the bucket's first entry
                     if (c.y & kHead8Filt) {  // none of the bucket's records within N on bases W..W+F-1: done
@@ -2444,6 +2427,8 @@ __global__ __launch_bounds__(kTailBlock) void tail_kernel(ScanArgs a) {
                 }
             }
         }
+        if (kRef16 && kTailPrefetch && !(vnext.x == 0xFFFFFFFFu && vnext.y == 0xFFFFFFFFu))
+            rwnext = a.rk[ref16_key<kGap>(a, vnext) >> 5];
         // The buffer's fill is read by every thread between two barriers at a check, and the
         // waves run free between checks.  The next check comes after as many passes as the
         // buffer's free half holds at the survivor rate since the last one (1..kTailCheck): c4's
@@ -2827,9 +2812,6 @@ static void launch_fixed4(int fix, uint32_t grid, hipStream_t st, const ScanArgs
     else hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2, 0, 3>), dim3(grid), dim3(kBlock), 0, st, a);
 }
 
-#ifndef MP_REF16_ALL
-#define MP_REF16_ALL 0
-#endif
 // *ref16: the run's key references are in the 16-B form (the key-group scans; a0.ref16 says
 // whether the genome allows it), as the tail pass must read them.
 static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t tiles, hipStream_t st, bool* tail,
@@ -2839,8 +2821,7 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
     *tail = false;
     *ref16 = 0;
     if (t->gap_len) {  // gapped seed: the key-group path, every passing seed deferred to tail_kernel
-        a.ref16 = MP_REF16_ALL ? a0.ref16 : 0u;  // (see keyref below)
-        *ref16 = a.ref16;
+        a.ref16 = 0u;  // (32-B references: see keyref below)
         if (!(t->filt_direct && !t->lds_exact && t->kgrp_F >= 2 && a.W >= 11 && a.W <= 13 && a.defer_full))
             return fail(MP_E_STATE, "gapped seed table without key groups");
         // c5's shape (W = 8, N = 1) with its gap as constants; other W 7..9 shapes from the table
@@ -2874,7 +2855,7 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
     // the forms below that leave key references (kRkf 1 and 2)
     // (16-B references only for the wide key groups: c4 leaves ~16M, whose traffic they halve;
     // c3's 5.5M took 12 us longer in tail_kernel, which looks up the bases left per reference)
-    const bool keyref = !dense && !inl && !t->lds_exact && (rkf4 || (MP_REF16_ALL && rkf)) && (t->lds_k == 1 || t->lds_k == 2);
+    const bool keyref = !dense && !inl && !t->lds_exact && rkf4 && (t->lds_k == 1 || t->lds_k == 2);
     a.ref16 = keyref ? a0.ref16 : 0u;
     *ref16 = a.ref16;
     if (dense) {
