@@ -31,7 +31,6 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-CHAIN_SHORT_MS = 0.15  # the calibration run's tail + pair + order under this: the deeper pipeline
 METRIC = "genome bases scanned/sec (Gbp/s) + STS hits/sec, W=11 N=1, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip parameters)
 BYTES_PER_BASE = 0.375       # 2-bit plane + 1-bit ambiguity plane, read once
@@ -488,16 +487,15 @@ def main():
                          "regions (IpcGather, no kernel on the CUs); rccl: mp_comm_gather_hits; host: gloo")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one search handle: every step waits for the previous one (no run queued ahead)")
-    ap.add_argument("--handles", type=int, default=0,
-                    help="search handles of the pipeline (0: chosen from a calibration run, see --depth)")
+    ap.add_argument("--handles", type=int, default=2,
+                    help="search handles of the pipeline")
     ap.add_argument("--streams", type=int, default=0,
                     help="streams the handles are dealt onto round-robin (0: one per handle); with fewer "
                          "streams than handles a stream runs step i's tail/pair/order then step i+streams' scan")
-    ap.add_argument("--depth", type=int, default=0,
+    ap.add_argument("--depth", type=int, default=1,
                     help="steps enqueued ahead of the one the host completes (1: step i+1 is enqueued before "
-                         "the host waits for step i); at most handles - 1.  0 (with --handles 0 and --streams 0): "
-                         f"2 steps ahead on 4 handles over 2 streams when a calibration run's tail + pair + "
-                         f"order take under {CHAIN_SHORT_MS} ms, else 1 ahead on 2 handles")
+                         "the host waits for step i); at most handles - 1.  Diagnostic: 2 or more can start a "
+                         "scan while another scan's blocks still wait for CUs (DESIGN 5.1, round 6)")
     ap.add_argument("--one-stream", action="store_true",
                     help="pipelined handles share one stream (no kernel of step i+1 overlaps step i)")
     ap.add_argument("--shard-of", type=int, default=0,
@@ -578,31 +576,14 @@ def main():
     if gmode == "rccl":
         gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)  # rank 0's gather buffer
     shift = len(lens) * rank if weak else 0
-    # Pipeline shape from one calibration run with every stage timed (untimed, before the warmup).
-    # A stream runs step i's scan then its tail, pair and order kernels; the persistent scan holds
-    # every CU, so the next step's scan (on the other stream) takes the CUs as soon as they free
-    # and both steps' chains run after it (profiles/r06d_timeline_*.txt).  With 2 handles the
-    # host enqueues step i+2 only after it completed step i, which leaves the GPU idle between
-    # the chains and the next scan; 4 handles over the same 2 streams, 2 steps ahead, queue that
-    # scan behind its stream's chain instead (1/8 c3 0.309-0.313 -> 0.299-0.301 ms, c2 0.150 ->
-    # 0.143-0.144 ms).  With a long chain (c4: 0.76 ms) that scan then starts block by block
-    # beside the other stream's chain, and a persistent scan whose blocks start late ends late:
-    # c4 2.68 -> 3.75 ms (profiles/r06e_pipeline_depth_ab.json).  Hence the threshold.
-    search.set_stage_timing(True)
-    search.run(rng, stream)
-    cal = search.last_stats()
-    chain_ms = sum(max(0.0, cal[k]) for k in ("tail_ms", "pair_ms", "order_ms"))
-    auto = args.handles <= 0 and args.depth <= 0 and args.streams <= 0 and not args.one_stream
-    short = chain_ms < CHAIN_SHORT_MS
-    if args.no_pipeline:
-        nbuf = 1
-    elif args.handles > 0:
-        nbuf = max(2, args.handles)
-    else:
-        nbuf = 4 if auto and short else 2
-    if auto and short and nbuf == 4:
-        args.streams, args.depth = 2, 2
-    args.depth = max(1, args.depth)
+    # Pipeline: 2 handles on 2 streams, step i+1 enqueued before the host completes step i.  The
+    # host's completion of step i-1 then stands between step i's scan and step i+1's, so a scan
+    # never becomes runnable while another scan's blocks still wait for CUs.  Deeper pipelines
+    # (--handles 4 --streams 2 --depth 2) fill the ~13 us the host leaves between a stream's
+    # chain and its next scan (1/8 c3 0.31 -> 0.30 ms), but let two scans run at once, each on
+    # part of the CUs, and a persistent scan whose blocks start late ends late: c4 2.68 -> 3.75
+    # ms, and the default c3 bench once 2.05 -> 4.03 ms.
+    nbuf = 1 if args.no_pipeline else max(2, args.handles)
     ipcg = None
     if gmode == "ipc":
         # regions of twice the largest rank's hit count (one untimed run to learn it); every
@@ -654,8 +635,7 @@ def main():
         torch.cuda.current_stream() if args.one_stream else torch.cuda.Stream(device=dev) for _ in range(nstr - 1)]
     streams = [own[j % nstr] for j in range(nbuf)]  # handle j's stream
     depth = max(1, min(args.depth, nbuf - 1)) if nbuf > 1 else 1
-    log(f"[rank {rank}] pipeline: {nbuf} handles on {nstr} streams, {depth} step(s) ahead "
-        f"(calibration run: tail + pair + order {chain_ms:.3f} ms)")
+    log(f"[rank {rank}] pipeline: {nbuf} handles on {nstr} streams, {depth} step(s) ahead")
     gstream = torch.cuda.Stream(device=dev) if comm is not None else None
     gdone = [None] * nbuf
     scan_ms = []
@@ -920,8 +900,6 @@ def main():
         "pipeline": (f"{nbuf} search handles on {'one stream' if args.one_stream else f'{nstr} streams'}: step i+{depth} "
                      f"enqueued before the host waits for step i (mp_search_enqueue/complete)"
                      if nbuf > 1 else "none: each step waits for the previous"),
-        "pipeline_calibration": {"chain_ms": round(chain_ms, 4), "short_chain_below_ms": CHAIN_SHORT_MS,
-                                 "note": "tail + pair + order of one untimed staged run before the warmup"},
         "scan_timing": ("HIP events around the scan kernel on its launch stream in every timed step"
                         if scan_in_timed else
                         "HIP events around the scan kernel on its launch stream in 3 untimed steps after the "
