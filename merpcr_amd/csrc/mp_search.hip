@@ -1596,35 +1596,60 @@ constexpr uint32_t kSChunkShort = 128;
 // super-steps at ~11 us each and waves 0-3 did 60 at ~5 us; with fixed chunks of 4 and one
 // chunk claimed ahead the young waves ended 20 us after the old ones and the last wave 47 us
 // after the first.
+// Round 6: a block's first chunks are claimed, not assigned.  Thread 0 claims kW chunks for its
+// waves with one atomic on the group's counter while the block stages its LDS (block_claim); the
+// waves then claim on as before.  Round 5 gave each wave a static first chunk at lo + (its index
+// in the group) x chunk: a block that started late (another kernel holding its CU) still owned
+// that chunk, and the scan could not end before the late block had done it -- with two scans
+// sharing the CUs a step took twice as long.  Now a late block takes only what is
+// left, and its waves find nothing and leave when the group's range is gone.  Start-up cost: one
+// more returning atomic per block (32 per group counter), under the LDS staging.
+__device__ __forceinline__ bool sched_dynamic(uint64_t n_supers, int kW) {
+    return n_supers >= (uint64_t)gridDim.x * (uint32_t)kW * MP_SCHED_MIN;
+}
+__device__ __forceinline__ uint32_t sched_chunk(uint64_t n_supers, int kW, uint32_t short_chunk) {
+    return n_supers < (uint64_t)gridDim.x * (uint32_t)kW * kSChunkShort ? short_chunk : kSChunk;
+}
+// thread 0 of the block: the group-relative position of the block's kW first chunks
+__device__ __forceinline__ uint32_t block_claim(unsigned long long* counters, uint32_t sched_base, uint64_t n_supers,
+                                                int kW, uint32_t short_chunk) {
+    const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;
+    unsigned int* ctr = reinterpret_cast<unsigned int*>(counters + sched_base + (blockIdx.x % g) * kStatStride);
+    return atomicAdd(ctr, (uint32_t)kW * sched_chunk(n_supers, kW, short_chunk));
+}
+
 struct SuperSched {  // 32-bit state (super-step indices < 2^32): it lives beside the scan's registers
     uint32_t lo, hi, nw, end;  // XCD group range, waves of the group, end of the current chunk
-    uint32_t S;                // end of the static first chunks: dynamic positions count from here
+    uint32_t S;                // where claimed positions count from (the group's lo)
     uint32_t pending, psize;   // lane 0: position claimed for the next chunk, and its size
     uint32_t stride;           // 0: dynamic; else the static round-robin stride
     uint32_t chunk;            // largest claim
     uint32_t young;            // the SIMD's two youngest waves (w >= kW / 2) claim half
     uint32_t hint;             // start of this wave's last chunk (the guided size's estimate)
     unsigned int* ctr;
+    // first_pos: the block's claim (block_claim, shared through LDS; unused for static-order scans)
     __device__ __forceinline__ uint64_t first(unsigned long long* counters, uint32_t sched_base, uint64_t n_supers, int w,
-                                              int kW, int lane, uint32_t short_chunk) {
+                                              int kW, int lane, uint32_t short_chunk, uint32_t first_pos) {
         // short scans (under 64 super-steps per wave, e.g. c2) keep the static order: their
         // per-wave totals average out and the claims would only add latency
         const uint32_t waves = gridDim.x * (uint32_t)kW;
-        if (n_supers < (uint64_t)waves * MP_SCHED_MIN) {
+        if (!sched_dynamic(n_supers, kW)) {
             stride = waves;
             return (uint64_t)blockIdx.x * (uint64_t)kW + (uint64_t)w;
         }
         stride = 0;
-        chunk = n_supers < (uint64_t)waves * kSChunkShort ? short_chunk : kSChunk;
+        chunk = sched_chunk(n_supers, kW, short_chunk);
         const uint32_t g = gridDim.x < 8u ? gridDim.x : 8u;  // groups: one per XCD, fewer on small grids
         const uint32_t x = blockIdx.x % g;
         ctr = reinterpret_cast<unsigned int*>(counters + sched_base + x * kStatStride);
         lo = (uint32_t)(n_supers * x / g);
         hi = (uint32_t)(n_supers * (x + 1) / g);
         nw = ((gridDim.x - x + g - 1u) / g) * (uint32_t)kW;
-        S = min(lo + nw * chunk, hi);
+        S = lo;
         young = (uint32_t)w >= (uint32_t)kW / 2u;
-        const uint32_t st = lo + ((blockIdx.x / g) * (uint32_t)kW + (uint32_t)w) * chunk;
+        // positions past the range: the sum saturates instead of wrapping (a very late block)
+        const uint64_t st64 = (uint64_t)lo + first_pos + (uint64_t)w * chunk;
+        const uint32_t st = st64 < hi ? (uint32_t)st64 : hi;
         end = min(st + chunk, hi);
         hint = st;
         claim(lane);
@@ -1678,6 +1703,10 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t s_wl_raw[kWaves * kWlBytes];
 
     zero_sort_counts(a);
+    const uint64_t n_supers = a.spans[a.n_spans].super0;
+    __shared__ uint32_t s_first;  // the block's first chunks (block_claim), issued before the staging loads
+    if (threadIdx.x == 0 && sched_dynamic(n_supers, kWaves))
+        s_first = block_claim(a.counters, a.sched_base, n_supers, kWaves, a.sched_short);
     // stage the seed prefilter in LDS (once per persistent workgroup): all eight 16-B loads of
     // a thread in flight before the first LDS store (one L2 round trip, not eight)
     {
@@ -1695,7 +1724,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const uint64_t stride = (uint64_t)gridDim.x * kWaves;
-    const uint64_t n_supers = a.spans[a.n_spans].super0;
     const uint32_t W = kFix ? kFixW : (uint32_t)a.W;
     const uint32_t shw = 32u - 2u * W;
     WaveLds& L = *reinterpret_cast<WaveLds*>(s_wl_raw + (uint32_t)w * kWlBytes);
@@ -1715,7 +1743,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
                        kTC - kStaticRefs, 0u};
 
     SuperSched sch;
-    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kWaves, lane, a.sched_short);
+    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kWaves, lane, a.sched_short, s_first);
     // span of the super-step being prefetched, cached in registers (wave-uniform): the
     // common path of the prefetch issues only the four plane loads, no waits
     SeqSpan pf{};
@@ -2073,6 +2101,10 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     uint32_t* s_esc = reinterpret_cast<uint32_t*>(s_grp + ngrp);
     uint32_t* s_sum = s_esc + ngrp;  // dsum_mode: 16-bit summary per key, two per word
     zero_sort_counts(a);
+    const uint64_t n_supers = a.spans[a.n_spans].super0;
+    __shared__ uint32_t s_first;  // the block's first chunks (block_claim, as scan_kernel's)
+    if (threadIdx.x == 0 && sched_dynamic(n_supers, kDenseWaves))
+        s_first = block_claim(a.counters, a.sched_base, n_supers, kDenseWaves, a.sched_short);
     for (uint32_t i = threadIdx.x; i < ngrp; i += kDenseBlock) {
         s_grp[i] = a.dgrp[i];
         s_esc[i] = a.dgesc[i];
@@ -2087,7 +2119,6 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const uint64_t stride = (uint64_t)gridDim.x * kDenseWaves;
-    const uint64_t n_supers = a.spans[a.n_spans].super0;
     const uint32_t shw = 32u - 2u * W;
     const uint32_t fmask = a.dense_M;
     const uint32_t N = (uint32_t)a.N;
@@ -2096,7 +2127,7 @@ __global__ __launch_bounds__(kDenseBlock) void dense_kernel(ScanArgs a) {
     SurvChunk C{0, kChunkNone, 0u};
 
     SuperSched sch;
-    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kDenseWaves, lane, a.sched_short);
+    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kDenseWaves, lane, a.sched_short, s_first);
     SeqSpan pf{};
     pf.super0 = 1;
     uint64_t pf_end = 0, pf_sbase = 0;

@@ -131,7 +131,7 @@ VARIANTS = {
          (_T_END, "    const uint64_t wt2 = wall_clock64();  // ablation 40\n"),
          ("        const uint64_t nx = sch.next(ss, n_supers, lane);\n        (void)stride;\n        if constexpr (kMode == 1) {",
           "        ++n_ss;  // ablation 40\n"),
-         ("    SuperSched sch;\n    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kWaves, lane, a.sched_short);",
+         ("    SuperSched sch;\n    uint64_t ss = sch.first(a.counters, a.sched_base, n_supers, w, kWaves, lane, a.sched_short, s_first);",
           "    uint32_t n_ss = 0;  // ablation 40\n"),
          ("    // candidate statistics\n    add_stats(a, ncand, lane == 0 ? C.total : 0u, lane);\n}\n",
           "    if ((threadIdx.x & 63) == 0 && blockIdx.x * kWaves + (threadIdx.x >> 6) < 8192)  // ablation 40\n"
