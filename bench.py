@@ -487,15 +487,14 @@ def main():
                          "regions (IpcGather, no kernel on the CUs); rccl: mp_comm_gather_hits; host: gloo")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one search handle: every step waits for the previous one (no run queued ahead)")
-    ap.add_argument("--handles", type=int, default=2,
+    ap.add_argument("--handles", type=int, default=4,
                     help="search handles of the pipeline")
-    ap.add_argument("--streams", type=int, default=0,
+    ap.add_argument("--streams", type=int, default=2,
                     help="streams the handles are dealt onto round-robin (0: one per handle); with fewer "
                          "streams than handles a stream runs step i's tail/pair/order then step i+streams' scan")
-    ap.add_argument("--depth", type=int, default=1,
+    ap.add_argument("--depth", type=int, default=2,
                     help="steps enqueued ahead of the one the host completes (1: step i+1 is enqueued before "
-                         "the host waits for step i); at most handles - 1.  Diagnostic: 2 or more can start a "
-                         "scan while another scan's blocks still wait for CUs (DESIGN 5.1, round 6)")
+                         "the host waits for step i); at most handles - 1")
     ap.add_argument("--one-stream", action="store_true",
                     help="pipelined handles share one stream (no kernel of step i+1 overlaps step i)")
     ap.add_argument("--shard-of", type=int, default=0,
@@ -576,13 +575,13 @@ def main():
     if gmode == "rccl":
         gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)  # rank 0's gather buffer
     shift = len(lens) * rank if weak else 0
-    # Pipeline: 2 handles on 2 streams, step i+1 enqueued before the host completes step i.  The
-    # host's completion of step i-1 then stands between step i's scan and step i+1's, so a scan
-    # never becomes runnable while another scan's blocks still wait for CUs.  Deeper pipelines
-    # (--handles 4 --streams 2 --depth 2) fill the ~13 us the host leaves between a stream's
-    # chain and its next scan (1/8 c3 0.31 -> 0.30 ms), but let two scans run at once, each on
-    # part of the CUs, and a persistent scan whose blocks start late ends late: c4 2.68 -> 3.75
-    # ms, and the default c3 bench once 2.05 -> 4.03 ms.
+    # Pipeline: 4 handles dealt onto 2 streams, step i+2 enqueued before the host completes step
+    # i.  A stream runs step i's scan and then its tail, pair and order kernels, and the next step's
+    # scan (on the other stream) takes the CUs as the scan's blocks leave, so both steps' chains
+    # run after it; with 2 handles the host enqueued step i+2 only after completing step i, which
+    # left ~13 us of idle GPU between the chains and the next scan.  Queued two ahead, that scan
+    # waits behind its stream's chain instead: 1/8 c3 0.303-0.306 -> 0.294-0.295 ms, c2 0.148-0.150
+    # -> 0.143-0.144 ms, c3 / c4 / c5 unchanged (profiles/r06j_pipeline_ab.json).
     nbuf = 1 if args.no_pipeline else max(2, args.handles)
     ipcg = None
     if gmode == "ipc":

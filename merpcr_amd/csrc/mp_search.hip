@@ -1600,10 +1600,10 @@ constexpr uint32_t kSChunkShort = 128;
 // waves with one atomic on the group's counter while the block stages its LDS (block_claim); the
 // waves then claim on as before.  Round 5 gave each wave a static first chunk at lo + (its index
 // in the group) x chunk: a block that started late (another kernel holding its CU) still owned
-// that chunk, and the scan could not end before the late block had done it -- with two scans
-// sharing the CUs a step took twice as long.  Now a late block takes only what is
-// left, and its waves find nothing and leave when the group's range is gone.  Start-up cost: one
-// more returning atomic per block (32 per group counter), under the LDS staging.
+// that chunk, and the scan could not end before the late block had done it.  Now a late block
+// takes only what is left, and its waves find nothing and leave when the group's range is gone.
+// Start-up cost: one more returning atomic per block (32 per group counter), under the LDS
+// staging; same-box step times unchanged (profiles/r06i_sched_ab.json).
 __device__ __forceinline__ bool sched_dynamic(uint64_t n_supers, int kW) {
     return n_supers >= (uint64_t)gridDim.x * (uint32_t)kW * MP_SCHED_MIN;
 }
