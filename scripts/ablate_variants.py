@@ -159,6 +159,7 @@ VARIANTS = {
          ("};\n\n// kRkf: 0 the rank queue", _STEAL)],
     71: [("    if (!((rw.x >> bit) & 1u)) return false;  // the key is absent\n    if constexpr (kGap != 0) {", _KGRP_BF)],
     55: [(_LPHIT, "            if (hit && t < -1000000) // ablation 55\n")],
+    54: [(_P1, "    if (false)  // ablation 54\n")],
 }
 
 
