@@ -34,6 +34,10 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       and nothing more
   81  tail_kernel up to the key's rank word and bucket head (no entries, no fingerprint test)
   82  tail_kernel with survivors counted, not stored: no LDS buffer, no barriers, no flushes
+  7   level 2 without level 1's LDS reads: each window's level-1 bit is a hash of its W-mer
+      (1/8 of windows pass, about the prefilter's 12% on c3), so the key-group probes, the field
+      test and the references run as in the product on a like number of positives
+  8   variant 5 with the static round-robin order (no claims): the genome stream alone
   60  scan_kernel's genome-plane loads non-temporal (the stream kept out of L2's working set:
       the c4 level-2 tables, rank words + 16-B heads, are ~4.1 MB against a 4 MB L2)
 """
@@ -158,10 +162,17 @@ VARIANTS = {
           "            st = S + (uint32_t)__builtin_amdgcn_readfirstlane((int)pending);\n        }\n"),
          ("};\n\n// kRkf: 0 the rank queue", _STEAL)],
     71: [("    if (!((rw.x >> bit) & 1u)) return false;  // the key is absent\n    if constexpr (kGap != 0) {", _KGRP_BF)],
+    7: [("                if constexpr (kGap != 0) x = gap_key(x, gap_at, gap_len);\n                const uint32_t wv = lds[x >> (37 - kLdsFilterLog2)];\n",
+         "                if constexpr (kGap != 0) x = gap_key(x, gap_at, gap_len);\n"
+         "                const uint32_t wv = ((x ^ (x >> 13)) & 7u) == 0u ? ~0u : 0u;  // ablation 7\n", "replace")],
     55: [(_LPHIT, "            if (hit && t < -1000000) // ablation 55\n")],
     54: [(_P1, "    if (false)  // ablation 54\n")],
 }
 
+
+VARIANTS[8] = VARIANTS[5] + [
+    ("        if (!sched_dynamic(n_supers, kW)) {\n            stride = waves;", "        if (true) {  // ablation 8\n            stride = waves;", "replace"),
+]
 
 VARIANTS[42] = VARIANTS[40] + [
     ("            ss = nx;\n            continue;\n        }\n        uint32_t hits = probe32",
