@@ -489,9 +489,11 @@ def main():
                     help="one search handle: every step waits for the previous one (no run queued ahead)")
     ap.add_argument("--handles", type=int, default=4,
                     help="search handles of the pipeline")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=0,
                     help="streams the handles are dealt onto round-robin (0: one per handle); with fewer "
-                         "streams than handles a stream runs step i's tail/pair/order then step i+streams' scan")
+                         "streams than handles a stream runs step i's tail/pair/order then step i+streams' scan "
+                         "(round 6, same box: one per handle 1/8 c3 0.293-0.295 ms against 0.301-0.305 on 2 "
+                         "streams, c4 2.649-2.654 against 2.692; profiles/r06n_streams_ab.json)")
     ap.add_argument("--depth", type=int, default=2,
                     help="steps enqueued ahead of the one the host completes (1: step i+1 is enqueued before "
                          "the host waits for step i); at most handles - 1")
@@ -575,13 +577,15 @@ def main():
     if gmode == "rccl":
         gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)  # rank 0's gather buffer
     shift = len(lens) * rank if weak else 0
-    # Pipeline: 4 handles dealt onto 2 streams, step i+2 enqueued before the host completes step
-    # i.  A stream runs step i's scan and then its tail, pair and order kernels, and the next step's
-    # scan (on the other stream) takes the CUs as the scan's blocks leave, so both steps' chains
-    # run after it; with 2 handles the host enqueued step i+2 only after completing step i, which
-    # left ~13 us of idle GPU between the chains and the next scan.  Queued two ahead, that scan
-    # waits behind its stream's chain instead: 1/8 c3 0.303-0.306 -> 0.294-0.295 ms, c2 0.148-0.150
-    # -> 0.143-0.144 ms, c3 / c4 / c5 unchanged (profiles/r06j_pipeline_ab.json).
+    # Pipeline: 4 handles, each on its own stream, step i+2 enqueued before the host completes
+    # step i.  Step i+1's scan takes the CUs as step i's scan blocks leave, so step i's chain
+    # (tail, pair, order) runs after it; with 2 handles the host enqueued step i+2 only after
+    # completing step i, which left ~13 us of idle GPU between the chains and the next scan
+    # (1/8 c3 0.303-0.306 -> 0.294-0.295 ms queued two ahead, profiles/r06j_pipeline_ab.json).
+    # With the 4 handles on 2 streams step i+2's scan still queued behind step i's chain; on
+    # their own streams it starts on the CUs the latency-bound chains leave idle: 1/8 c3
+    # 0.301-0.305 -> 0.293-0.295 ms, c4 2.692 -> 2.649-2.654 ms, c3 2.046-2.051 -> 2.028-2.043
+    # (profiles/r06n_streams_ab.json).
     nbuf = 1 if args.no_pipeline else max(2, args.handles)
     ipcg = None
     if gmode == "ipc":
