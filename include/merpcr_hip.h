@@ -182,6 +182,8 @@ typedef struct mp_search_options {
     int32_t ref32;              /* 1: 32-B bucket-tail key references where 16-B ones fit */
     int32_t sched_short;        /* super-steps per scheduler claim in short scans; 0 = 4 */
     int32_t crowd_grid;         /* workgroups of the crowded-bucket sort; 0 = one per CU */
+    int32_t scan_grid;          /* scan_kernel workgroups; 0 = one per CU.  Fewer leave CUs free
+                                   for another pipelined run's post-scan kernels */
 } mp_search_options;
 #define MP_GENERIC_FIX 1u   /* key-group scans of W = 11 with W, F and N as run-time values */
 #define MP_GENERIC_GAP 2u   /* the gapped W = 8 split seed with its shape as run-time values */

@@ -66,7 +66,8 @@ class MPSearchOptions(ctypes.Structure):
                 ("sort_bucket_bits", c_int32), ("pair_blocks_per_cu", c_int32),
                 ("hit_cap", c_uint64), ("surv_cap", c_uint64), ("tail_cap", c_uint64),
                 ("no_rank_filter", c_int32), ("no_split", c_int32),
-                ("generic_forms", c_int32), ("ref32", c_int32), ("sched_short", c_int32), ("crowd_grid", c_int32)]
+                ("generic_forms", c_int32), ("ref32", c_int32), ("sched_short", c_int32), ("crowd_grid", c_int32),
+                ("scan_grid", c_int32)]
 
 
 class MPTableOptions(ctypes.Structure):
@@ -376,7 +377,7 @@ class Search:
 
     def set_options(self, tails="auto", defer=True, dense=True, sort="auto", sort_bucket_bits=0,
                     pair_blocks_per_cu=0, hit_cap=0, surv_cap=0, tail_cap=0, rank_filter=True, split=True,
-                    generic=(), ref32=False, sched_short=0, crowd_grid=0):
+                    generic=(), ref32=False, sched_short=0, crowd_grid=0, scan_grid=0):
         """Kernel-path selection, initial list capacities and tuning (mp_search_set_options);
         the defaults are the library's automatic choices.  generic: names of MP_GENERIC ("fix",
         "gap", "pair": the run-time-shape kernel forms, for A/B runs)."""
@@ -388,7 +389,7 @@ class Search:
         o = MPSearchOptions(MP_TAILS[tails], 0 if defer else 1, 0 if dense else 1, MP_SORT[sort],
                             sort_bucket_bits, pair_blocks_per_cu, hit_cap, surv_cap, tail_cap,
                             0 if rank_filter else 1, 0 if split else 1, gbits, 1 if ref32 else 0,
-                            int(sched_short), int(crowd_grid))
+                            int(sched_short), int(crowd_grid), int(scan_grid))
         check(lib().mp_search_set_options(self._h, ctypes.byref(o)))
 
     def set_stage_timing(self, on: bool):

@@ -2694,7 +2694,7 @@ MP_EXPORT int mp_search_set_options(void* search, const mp_search_options* opt) 
         opt->sort > MP_SORT_SCATTER || opt->sort_bucket_bits < 0 || opt->sort_bucket_bits > 16 ||
         opt->pair_blocks_per_cu < 0 || opt->generic_forms < 0 ||
         opt->generic_forms > (int32_t)(MP_GENERIC_FIX | MP_GENERIC_GAP | MP_GENERIC_PAIR) || opt->ref32 < 0 ||
-        opt->ref32 > 1 || opt->sched_short < 0 || opt->sched_short > 64 || opt->crowd_grid < 0)
+        opt->ref32 > 1 || opt->sched_short < 0 || opt->sched_short > 64 || opt->crowd_grid < 0 || opt->scan_grid < 0)
         return fail(MP_E_ARG, "mp_search_set_options: option out of range");
     MP_HIP_CHECK(hipSetDevice(s->genome->device));
     s->opt = *opt;
@@ -2843,12 +2843,20 @@ static void launch_fixed4(int fix, uint32_t grid, hipStream_t st, const ScanArgs
     else hipLaunchKernelGGL((scan_kernel<1, false, 2, true, 0, 2, 0, 3>), dim3(grid), dim3(kBlock), 0, st, a);
 }
 
+// Workgroups of a scan over `tiles` super-steps: one per CU (persistent), at most
+// mp_search_options.scan_grid, at most one per kWaves super-steps.
+static uint32_t scan_grid_of(const Search* s, uint64_t tiles) {
+    uint64_t cap = (uint64_t)s->n_cu * kBlocksPerCU;
+    if (s->opt.scan_grid > 0) cap = std::min<uint64_t>(cap, (uint64_t)s->opt.scan_grid);
+    return (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, cap);
+}
+
 // *ref16: the run's key references are in the 16-B form (the key-group scans; a0.ref16 says
 // whether the genome allows it), as the tail pass must read them.
 static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t tiles, hipStream_t st, bool* tail,
                        uint32_t* ref16) {
     ScanArgs a = a0;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU);
+    const uint32_t grid = scan_grid_of(s, tiles);
     *tail = false;
     *ref16 = 0;
     if (t->gap_len) {  // gapped seed: the key-group path, every passing seed deferred to tail_kernel
@@ -3266,8 +3274,7 @@ MP_EXPORT int mp_search_enqueue(void* search, const mp_range* range, void* strea
         a.sched_short = s->opt.sched_short ? (uint32_t)s->opt.sched_short : (uint32_t)MP_SCHUNK_SHORT;
         // the scan grid's static bucket-tail slots (launch_scan's grid; a dense scan has none,
         // and its run launches no tail pass)
-        a.tail_static = (uint64_t)std::min<uint64_t>((tiles + kWaves - 1) / kWaves, (uint64_t)s->n_cu * kBlocksPerCU) *
-                        kWaves * kStaticRefs;
+        a.tail_static = (uint64_t)scan_grid_of(s, tiles) * kWaves * kStaticRefs;
         // 16-B key references need the position in 40 bits and the sequence in 23 (ref16_make)
         a.ref16 = (g->total < (1ull << 40) && g->n_seq + 1u < (1u << 23) && !s->opt.ref32) ? 1u : 0u;
         // keys over 64 bits, or a forced rocPRIM sort: mode 2

@@ -43,7 +43,7 @@ int main(void) {
     F(mp_search_options, sort) F(mp_search_options, sort_bucket_bits) F(mp_search_options, pair_blocks_per_cu)
     F(mp_search_options, hit_cap) F(mp_search_options, surv_cap) F(mp_search_options, tail_cap)
     F(mp_search_options, no_rank_filter) F(mp_search_options, no_split) F(mp_search_options, generic_forms)
-    F(mp_search_options, ref32) F(mp_search_options, sched_short) F(mp_search_options, crowd_grid)
+    F(mp_search_options, ref32) F(mp_search_options, sched_short) F(mp_search_options, crowd_grid) F(mp_search_options, scan_grid)
     F(mp_table_options, lds_k) F(mp_table_options, no_h12) F(mp_table_options, kgrp4) F(mp_table_options, no_split)
     printf("MP_GENERIC %u %u %u\n", MP_GENERIC_FIX, MP_GENERIC_GAP, MP_GENERIC_PAIR);
     printf("MP_GATHER %d %d\n", MP_GATHER_COPY, MP_GATHER_RCCL);

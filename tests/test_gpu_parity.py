@@ -534,7 +534,7 @@ def _multi_case(W, n_sts, seed):
 
 @pytest.mark.parametrize("W,n_sts,opts", [(8, 3000, {}), (10, 3000, {}), (11, 6000, {}),
                                           (11, 6000, dict(tails="inline")), (11, 6000, dict(defer=False)),
-                                          (12, 6000, {})])
+                                          (12, 6000, {}), (11, 6000, dict(scan_grid=37))])
 def test_sharded_ranges_all_paths(W, n_sts, opts):
     """Owned (seq, k) ranges partition the hit list exactly through every scan path:
     dense_kernel (W=8), the exact-LDS scan (W=10), the ranked drain with full-head deferral
@@ -557,6 +557,10 @@ def test_sharded_ranges_all_paths(W, n_sts, opts):
         s.set_options(**opts)
     whole = s.fetch(s.run())
     assert len(whole) > 100
+    if "scan_grid" in opts:  # a grid of 37 scan workgroups (uneven XCD groups): the default list
+        d = _native.Search(eng.device_table(), genome)
+        assert np.array_equal(d.fetch(d.run()), whole)
+        d.close()
     # cuts: mid super-step, at a hit's k, one and W-1 bases after a hit's k (its seed window
     # lies across the cut), record boundaries
     k0 = int(whole["pos1"][len(whole) // 3])
