@@ -38,6 +38,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       (1/8 of windows pass, about the prefilter's 12% on c3), so the key-group probes, the field
       test and the references run as in the product on a like number of positives
   8   variant 5 with the static round-robin order (no claims): the genome stream alone
+  9   variant 7 with 1/16 of windows passing level 1; 10: with 1/4 (the scan's sensitivity to
+      the level-1 positive rate)
   60  scan_kernel's genome-plane loads non-temporal (the stream kept out of L2's working set:
       the c4 level-2 tables, rank words + 16-B heads, are ~4.1 MB against a 4 MB L2)
 """
@@ -169,6 +171,9 @@ VARIANTS = {
     54: [(_P1, "    if (false)  // ablation 54\n")],
 }
 
+
+VARIANTS[9] = [(VARIANTS[7][0][0], VARIANTS[7][0][1].replace("& 7u", "& 15u").replace("ablation 7", "ablation 9"), "replace")]
+VARIANTS[10] = [(VARIANTS[7][0][0], VARIANTS[7][0][1].replace("& 7u", "& 3u").replace("ablation 7", "ablation 10"), "replace")]
 
 VARIANTS[8] = VARIANTS[5] + [
     ("        if (!sched_dynamic(n_supers, kW)) {\n            stride = waves;", "        if (true) {  // ablation 8\n            stride = waves;", "replace"),
