@@ -234,6 +234,27 @@ def issue_bound(pmc: dict, dur_ns=None):
     return out
 
 
+def agreed_comm(local: int, rank: int, world: int):
+    """The RCCL communicator (merpcr_amd.dist.native_comm), or None on every rank when any
+    rank could not make one: the job then gathers over gloo on the host (slower, same list)
+    instead of failing.  Collective."""
+    import torch.distributed as dist
+    from merpcr_amd.dist import native_comm
+    comm, err = None, None
+    try:
+        comm = native_comm(local)
+    except Exception as e:  # noqa: BLE001 (reported, then every rank takes the same path)
+        err = f"{type(e).__name__}: {e}"
+    errs = [None] * world
+    dist.all_gather_object(errs, err)
+    if any(errs):
+        log(f"[rank {rank}] RCCL communicator unavailable ({[x for x in errs if x][0]}); host gather")
+        if comm is not None:
+            comm.close()
+        return None
+    return comm
+
+
 def cpu_baseline(eng, lens, buf, offs, cfg, hits_dev, budget_s: float, threads: int):
     """Time the C oracle (scalar restatement, `threads` pthreads over k ranges) on whole
     leading records of the same genome, and check its hits against the GPU's."""
@@ -535,7 +556,9 @@ def main():
         # it gathers through gloo on the host instead)
         if gmode == "rccl" and args.rehearse_one_gpu:
             gmode = "host"
-        comm = native_comm(local) if gmode == "rccl" else None
+        comm = agreed_comm(local, rank, world) if gmode == "rccl" else None
+        if gmode == "rccl" and comm is None:
+            gmode = "host"
 
     cfg = dict(synth.CONFIGS[args.config])
     total = int(cfg["total"] * args.scale) // 64 * 64
@@ -614,8 +637,11 @@ def main():
             ipcg = None
             gmode = "host" if args.rehearse_one_gpu else "rccl"
             if gmode == "rccl":
-                comm = native_comm(local)
-                gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)
+                comm = agreed_comm(local, rank, world)
+                if comm is None:
+                    gmode = "host"
+                else:
+                    gathered = torch.empty((1 << 22) * HIT_BYTES, dtype=torch.uint8, device=dev)
 
     # Steps are pipelined two deep (mp_search_enqueue / mp_search_complete on two search
     # handles over the same resident table and genome): step i+1's kernels are queued before

@@ -77,9 +77,17 @@ def native_comm(device: int, group=None):
     import torch.distributed as dist
     from ._native import Comm, comm_unique_id
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    obj = [comm_unique_id() if rank == 0 else None]
+    obj = [None]
+    if rank == 0:  # an error travels in the broadcast, so no rank is left waiting in it
+        try:
+            obj = [("ok", comm_unique_id())]
+        except Exception as e:  # noqa: BLE001 -- re-raised on every rank below
+            obj = [("err", f"rank 0 could not make the RCCL id: {type(e).__name__}: {e}")]
     dist.broadcast_object_list(obj, src=0, group=group)
-    return Comm(obj[0], world, rank, device)
+    kind, payload = obj[0]
+    if kind == "err":
+        raise RuntimeError(payload)
+    return Comm(payload, world, rank, device)
 
 
 class IpcGather:

@@ -7,11 +7,14 @@ C oracle on each rank's owned range.
 
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
 
 from merpcr_amd.dist import HIT_BYTES, as_hits, contig_shards, gather_hits, shard_ranges
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_shard_ranges_tile_the_genome():
@@ -92,3 +95,32 @@ def test_gather_gloo(world):
     for p in procs:
         p.join(timeout=60)
     assert ok and n > 10
+
+
+def _comm_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    import bench
+    comm = bench.agreed_comm(0, rank, world)  # no GPU here: every rank must come back with None
+    q.put((rank, comm is None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_fallback_is_agreed_without_a_gpu():
+    """bench.py's RCCL data plane when a communicator cannot be made (here: no GPU): every
+    rank leaves the collective set-up with None (the job then gathers on the host) instead of
+    one rank raising while another waits in a broadcast."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert got == [(0, True), (1, True)]
