@@ -40,6 +40,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
   8   variant 5 with the static round-robin order (no claims): the genome stream alone
   9   variant 7 with 1/16 of windows passing level 1; 10: with 1/4 (the scan's sensitivity to
       the level-1 positive rate)
+  57  pair_kernel with every survivor's record index folded into the first 1,024 records (their
+      128-B record lines then stay in L2): the bound on what record-line locality could save
   60  scan_kernel's genome-plane loads non-temporal (the stream kept out of L2's working set:
       the c4 level-2 tables, rank words + 16-B heads, are ~4.1 MB against a 4 MB L2)
 """
@@ -169,6 +171,7 @@ VARIANTS = {
          "                const uint32_t wv = ((x ^ (x >> 13)) & 7u) == 0u ? ~0u : 0u;  // ablation 7\n", "replace")],
     55: [(_LPHIT, "            if (hit && t < -1000000) // ablation 55\n")],
     54: [(_P1, "    if (false)  // ablation 54\n")],
+    57: [("    const uint32_t rec = v.z & 0x7FFFFFFFu;\n", "    const uint32_t rec = v.z & 0x3FFu;  // ablation 57\n", "replace")],
 }
 
 
