@@ -42,6 +42,8 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       the level-1 positive rate)
   57  pair_kernel with every survivor's record index folded into the first 1,024 records (their
       128-B record lines then stay in L2): the bound on what record-line locality could save
+  58  pair_kernel's genome loads (the primer-2 stretch and the primer-1 window) non-temporal, so
+      that they do not push the record lines out of L2
   60  scan_kernel's genome-plane loads non-temporal (the stream kept out of L2's working set:
       the c4 level-2 tables, rank words + 16-B heads, are ~4.1 MB against a 4 MB L2)
 """
@@ -171,6 +173,25 @@ VARIANTS = {
          "                const uint32_t wv = ((x ^ (x >> 13)) & 7u) == 0u ? ~0u : 0u;  // ablation 7\n", "replace")],
     55: [(_LPHIT, "            if (hit && t < -1000000) // ablation 55\n")],
     54: [(_P1, "    if (false)  // ablation 54\n")],
+    58: [("                    q0 = gq[2 * (e0 + t)];\n                    q1 = gq[2 * (e0 + t) + 1];\n",
+          "                    {  // ablation 58\n"
+          "                        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));\n"
+          "                        const u64x2* gv = reinterpret_cast<const u64x2*>(a.gpair);\n"
+          "                        const u64x2 t0 = __builtin_nontemporal_load(&gv[2 * (e0 + t)]);\n"
+          "                        const u64x2 t1 = __builtin_nontemporal_load(&gv[2 * (e0 + t) + 1]);\n"
+          "                        q0 = make_ulonglong2(t0.x, t0.y);\n"
+          "                        q1 = make_ulonglong2(t1.x, t1.y);\n"
+          "                    }\n", "replace"),
+         ("        const uint64_t G = ext2p(a.gpair, gpos + c);  // the interleaved planes: one line, not three\n"
+          "        const uint32_t ex = (uint32_t)(ext1p<2>(a.gpair, gpos + c) >> 32);\n",
+          "        const uint64_t gj = gpos + c, w2 = gj >> 5, e2 = gj >> 6;  // ablation 58\n"
+          "        const uint32_t s2 = (uint32_t)(gj & 31) * 2, s1 = (uint32_t)(gj & 63);\n"
+          "        const uint64_t ga = __builtin_nontemporal_load(&a.gpair[((w2 >> 1) << 2) | (w2 & 1)]);\n"
+          "        const uint64_t gb = __builtin_nontemporal_load(&a.gpair[(((w2 + 1) >> 1) << 2) | ((w2 + 1) & 1)]);\n"
+          "        const uint64_t xa = __builtin_nontemporal_load(&a.gpair[(e2 << 2) | 2]);\n"
+          "        const uint64_t xb = __builtin_nontemporal_load(&a.gpair[((e2 + 1) << 2) | 2]);\n"
+          "        const uint64_t G = s2 ? (ga << s2) | (gb >> (64 - s2)) : ga;\n"
+          "        const uint32_t ex = (uint32_t)((s1 ? (xa << s1) | (xb >> (64 - s1)) : xa) >> 32);\n", "replace")],
     57: [("    const uint32_t rec = v.z & 0x7FFFFFFFu;\n", "    const uint32_t rec = v.z & 0x3FFu;  // ablation 57\n", "replace")],
 }
 
