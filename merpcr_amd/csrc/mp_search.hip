@@ -2891,10 +2891,13 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
     const int fix = (a.W == (int)kFixW && a.I == 0 && !t->kgrp_wild && t->kgrp_F == kFixF && a.N <= 1 &&
                      !(s->opt.generic_forms & MP_GENERIC_FIX)) ? a.N + 1 : 0;
     const int fix4 = (a.W == (int)kFixW && a.N <= 2 && !(s->opt.generic_forms & MP_GENERIC_FIX)) ? a.N + 1 : 0;
-    // the forms below that leave key references (kRkf 1 and 2)
-    // (16-B references only for the wide key groups: c4 leaves ~16M, whose traffic they halve;
-    // c3's 5.5M took 12 us longer in tail_kernel, which looks up the bases left per reference)
-    const bool keyref = !dense && !inl && !t->lds_exact && rkf4 && (t->lds_k == 1 || t->lds_k == 2);
+    // the forms below that leave key references (kRkf 1 and 2), in the 16-B form: the wide key
+    // groups' (rkf4) forms whatever defer_full says, the I = 0 / wild key groups' only when the
+    // dispatch below takes them, which needs defer_full -- a table with many full heads runs a
+    // kRkf = 0 form, whose 32-B references the 16-B tail pass would misread (round 6: that
+    // mismatch was the illegal address of the first 16-B attempts)
+    const bool keyref = !dense && !inl && !t->lds_exact && (rkf4 || (rkf && a.defer_full)) &&
+                        (t->lds_k == 1 || t->lds_k == 2);
     a.ref16 = keyref ? a0.ref16 : 0u;
     *ref16 = a.ref16;
     if (dense) {

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 6: 16-B key references for the I = 0 key-group scans too (c3, c2; not the gapped seed):
+# Round 6: 16-B key references for the I = 0 key-group scans too (c3, c2; not the gapped seed),
+# only where the dispatch takes a key-group form (defer_full):
 # the GPU suite once, then same-box A/B against the final build (libmerpcr_hip_r6f.so).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
