@@ -102,6 +102,8 @@ int mp_table_split(void* table, uint32_t* seed_tables, uint32_t* rest_records);
 #define MP_LAYOUT_DENSE 16u    /* dense_kernel structures (W <= 9) */
 #define MP_LAYOUT_SPLIT 32u    /* split seeds (mp_table_split) */
 #define MP_LAYOUT_HASHED 64u   /* hashed presence filter + open-addressed slots (W >= 14) */
+#define MP_LAYOUT_DEFER_FULL 128u /* full-head buckets deferred to tail_kernel; the I = 0 key-group
+                                     scan forms (and their 16-B key references) need it */
 int mp_table_layout(void* table, uint32_t* flags);
 /* Layout choices of a table build.  Every field zero = the library's own choice (what
  * mp_table_create makes); the others exist for A/B runs and for tests that drive each layout

@@ -294,7 +294,8 @@ class Table:
         check(lib().mp_table_split(self._h, ctypes.byref(a), ctypes.byref(b)))
         return {"seed_tables": a.value, "rest_records": b.value}
 
-    LAYOUT = {"lds_exact": 1, "rank": 2, "kgrp": 4, "kgrp4": 8, "dense": 16, "split": 32, "hashed": 64}
+    LAYOUT = {"lds_exact": 1, "rank": 2, "kgrp": 4, "kgrp4": 8, "dense": 16, "split": 32, "hashed": 64,
+              "defer_full": 128}
 
     def layout(self) -> set:
         """The seed structures the table holds (mp_table_layout), by name."""

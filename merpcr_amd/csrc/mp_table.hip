@@ -700,7 +700,8 @@ static int build_table(const mp_params& p, int32_t device, uint32_t n_rec, const
         uint64_t bytes = 0;
         t->layout = (t->lds_exact ? MP_LAYOUT_LDS_EXACT : 0u) | (rk.empty() ? 0u : MP_LAYOUT_RANK) |
                     (kgrp.empty() ? 0u : MP_LAYOUT_KGRP) | (kgrp4.empty() ? 0u : MP_LAYOUT_KGRP4) |
-                    (dgrp.empty() ? 0u : MP_LAYOUT_DENSE) | (slots.empty() ? 0u : MP_LAYOUT_HASHED);
+                    (dgrp.empty() ? 0u : MP_LAYOUT_DENSE) | (slots.empty() ? 0u : MP_LAYOUT_HASHED) |
+                    (t->defer_full ? MP_LAYOUT_DEFER_FULL : 0u);
         if ((rc = upload(&t->filt, filt.data(), filt.size(), &bytes))) break;
         if ((rc = upload(&t->lfilt, lfilt.data(), lfilt.size(), &bytes))) break;
         if ((rc = upload(&t->slots, slots.data(), slots.size(), &bytes))) break;

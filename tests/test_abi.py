@@ -47,6 +47,8 @@ int main(void) {
     F(mp_table_options, lds_k) F(mp_table_options, no_h12) F(mp_table_options, kgrp4) F(mp_table_options, no_split)
     printf("MP_GENERIC %u %u %u\n", MP_GENERIC_FIX, MP_GENERIC_GAP, MP_GENERIC_PAIR);
     printf("MP_GATHER %d %d\n", MP_GATHER_COPY, MP_GATHER_RCCL);
+    printf("MP_LAYOUT %u %u %u %u %u %u %u %u\n", MP_LAYOUT_LDS_EXACT, MP_LAYOUT_RANK, MP_LAYOUT_KGRP, MP_LAYOUT_KGRP4,
+           MP_LAYOUT_DENSE, MP_LAYOUT_SPLIT, MP_LAYOUT_HASHED, MP_LAYOUT_DEFER_FULL);
     return 0;
 }
 """
@@ -69,6 +71,7 @@ def test_option_structs_match_the_header(tmp_path):
             assert (getattr(cls, f).offset, getattr(cls, f).size) == (off, size), (name, f)
     assert [int(x) for x in rows["MP_GENERIC"].split()] == [_native.MP_GENERIC[k] for k in ("fix", "gap", "pair")]
     assert [int(x) for x in rows["MP_GATHER"].split()] == [_native.MP_GATHER[k] for k in ("copy", "rccl")]
+    assert [int(x) for x in rows["MP_LAYOUT"].split()] == list(_native.Table.LAYOUT.values())
 
 
 def test_table_options_out_of_range_is_value_error():

@@ -130,6 +130,30 @@ def test_golden_corpus(name, tails):
     assert not bad, bad[:3]
 
 
+def test_key_group_tables_without_deferral():
+    """Regression for the 16-B key references: an I = 0 key-group table that does
+    not defer its full-head buckets runs a kRkf = 0 scan form, which writes 32-B references,
+    so its tail pass must stay in the 32-B form.  The golden corpus holds such tables (one of
+    them faulted when the choice followed the key groups alone); each gives the reference's
+    lines, and the key-group tables that do defer are there too."""
+    kinds = {"defer": 0, "no_defer": 0}
+    bad = []
+    for i, case in enumerate(load_golden("random_cases.json.gz")["cases"]):
+        eng = _engine(case["params"])
+        with tempfile.TemporaryDirectory() as td:
+            if not _load_sts(eng, case["sts_text"], td):
+                continue
+            lay = eng.device_table().layout()
+            if "kgrp" not in lay:
+                continue
+            recs = _records(case, eng, td)
+        kinds["defer" if "defer_full" in lay else "no_defer"] += 1
+        if _device_lines(eng, recs) != case["output"].splitlines():
+            bad.append((i, case["params"], sorted(lay)))
+    assert not bad, bad[:3]
+    assert kinds["defer"] > 0 and kinds["no_defer"] > 0, kinds
+
+
 @pytest.mark.parametrize("bits", [1, 4])
 def test_device_sort_crowded_buckets(bits):
     """The device-count bucket sort with forced coarse buckets: 2 buckets overflow the
