@@ -2898,7 +2898,10 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
     // mismatch was the illegal address of the first 16-B attempts)
     const bool keyref = !dense && !inl && !t->lds_exact && (rkf4 || (rkf && a.defer_full)) &&
                         (t->lds_k == 1 || t->lds_k == 2);
-    a.ref16 = keyref ? a0.ref16 : 0u;
+    // (a.ref16, the copy's: a split table's caller passes &pa[i].ref16 as `ref16`, the same
+    // object as a0, which the `*ref16 = 0` above has already cleared -- round 6 found the split
+    // seeds' scans writing 32-B references for that reason alone)
+    a.ref16 = keyref ? a.ref16 : 0u;
     *ref16 = a.ref16;
     if (dense) {
         const uint32_t dgrid = (uint32_t)std::min<uint64_t>((tiles + kDenseWaves - 1) / kDenseWaves,
