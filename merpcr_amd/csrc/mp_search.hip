@@ -2860,7 +2860,7 @@ static int launch_scan(Search* s, const Table* t, const ScanArgs& a0, uint64_t t
     *tail = false;
     *ref16 = 0;
     if (t->gap_len) {  // gapped seed: the key-group path, every passing seed deferred to tail_kernel
-        a.ref16 = 0u;  // (32-B references: see keyref below)
+        *ref16 = a.ref16;  // always a key-group form: 16-B references when the genome allows them
         if (!(t->filt_direct && !t->lds_exact && t->kgrp_F >= 2 && a.W >= 11 && a.W <= 13 && a.defer_full))
             return fail(MP_E_STATE, "gapped seed table without key groups");
         // c5's shape (W = 8, N = 1) with its gap as constants; other W 7..9 shapes from the table
