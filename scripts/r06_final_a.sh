@@ -4,5 +4,5 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
-bash scripts/gpu_check.sh r6h2 || exit 1
+bash scripts/gpu_check.sh r6h3 || exit 1
 KRE=scan_kernel bash scripts/profile.sh r06 --steps 20 --warmup 5 || exit 1
