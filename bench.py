@@ -234,6 +234,21 @@ def issue_bound(pmc: dict, dur_ns=None):
     return out
 
 
+def roofline_time(pmc, events_s: float):
+    """The scan stage's time for the roofline (seconds) and where it came from: the isolated
+    dispatches of this command's own kernel-trace pass (rocprofv3's clock, no event between
+    kernels); else a committed profile's isolated mean; else the HIP events (no trace ran: N > 1,
+    a shard, --no-pmc).  A profile's mean over every dispatch never stands in: it includes the
+    pipelined steps' overlapped scans (c3 3.16 ms against 2.06 isolated)."""
+    pmc = pmc or {}
+    if pmc.get("_trace_stage_ns"):
+        return pmc["_trace_stage_ns"] / 1e9, ("rocprofv3 --kernel-trace pass of this command: mean isolated "
+                                              "dispatch of each scan form, forms of a step summed")
+    if pmc.get("avg_duration_ns_trace_isolated"):
+        return pmc["avg_duration_ns_trace_isolated"] / 1e9, "avg_duration_ns_trace_isolated of the committed profile"
+    return events_s, "HIP events (no trace pass)"
+
+
 def agreed_comm(local: int, rank: int, world: int):
     """The RCCL communicator (merpcr_amd.dist.native_comm), or None on every rank when any
     rank could not make one: the job then gathers over gloo on the host (slower, same list)
@@ -881,15 +896,7 @@ def main():
             if prof is not None:
                 pmc, pmc_src = prof, f"profiles/{tag}_pmc.json (committed profile of this build)"
                 traffic = prof["hbm_traffic_bytes_per_launch"]
-    # roofline time: the scan stage's isolated dispatches in the kernel-trace pass (rocprofv3's own
-    # clock, no event between kernels); the HIP events when no trace ran (N > 1, shard, --no-pmc)
-    # (a committed profile's mean over every dispatch includes the pipelined steps' overlapped
-    # ones -- c3 3.16 ms against 2.06 isolated -- so only its isolated mean stands in)
-    trace_ns = (pmc or {}).get("_trace_stage_ns") or (pmc or {}).get("avg_duration_ns_trace_isolated")
-    kern_s = trace_ns / 1e9 if trace_ns else kern_ev_s
-    kern_src = ("rocprofv3 --kernel-trace pass of this command: mean isolated dispatch of each scan form, "
-                "forms of a step summed" if (pmc or {}).get("_trace_stage_ns")
-                else ("avg_duration_ns_trace_isolated of the committed profile" if trace_ns else "HIP events (no trace pass)"))
+    kern_s, kern_src = roofline_time(pmc, kern_ev_s)
     achieved = alg_bytes / kern_s / 1e9 if kern_s > 0 else 0.0
     out = {
         "metric": METRIC,

@@ -74,3 +74,14 @@ def test_trace_stage_time_filters_the_scan_forms(tmp_path):
     assert got["_trace_stage_ns"] == 2100 + 800
     assert sorted(got["_trace_forms"]) == ["void mp::scan_kernel<1, false, 8>(mp::ScanArgs)",
                                            "void mp::scan_kernel<1, false>(mp::ScanArgs)"]
+
+
+def test_roofline_time_never_takes_the_all_dispatch_mean():
+    """The roofline's time: this command's trace pass first, then a committed profile's isolated
+    mean, then the events -- never a profile's mean over every (overlapped) dispatch."""
+    assert bench.roofline_time({"_trace_stage_ns": 2.0e6, "avg_duration_ns_trace_isolated": 2.5e6}, 9e-3)[0] == 2.0e-3
+    t, src = bench.roofline_time({"avg_duration_ns_trace": 3.16e6, "avg_duration_ns_trace_isolated": 2.06e6}, 9e-3)
+    assert t == 2.06e-3 and "isolated" in src
+    t, src = bench.roofline_time({"avg_duration_ns_trace": 3.16e6}, 2.1e-3)
+    assert t == 2.1e-3 and "events" in src
+    assert bench.roofline_time(None, 1e-3) == (1e-3, "HIP events (no trace pass)")
