@@ -558,12 +558,14 @@ def _multi_case(W, n_sts, seed):
 
 @pytest.mark.parametrize("W,n_sts,opts", [(8, 3000, {}), (10, 3000, {}), (11, 6000, {}),
                                           (11, 6000, dict(tails="inline")), (11, 6000, dict(defer=False)),
-                                          (12, 6000, {}), (11, 6000, dict(scan_grid=37))])
+                                          (12, 6000, {}), (11, 6000, dict(scan_grid=37)),
+                                          (11, 6000, dict(ref32=True)), (8, 3000, dict(ref32=True))])
 def test_sharded_ranges_all_paths(W, n_sts, opts):
     """Owned (seq, k) ranges partition the hit list exactly through every scan path:
-    dense_kernel (W=8), the exact-LDS scan (W=10), the ranked drain with full-head deferral
-    to tail_kernel (W=11 default), inline tails, no deferral; cuts inside super-steps and
-    next to records' seed offsets (k + hash_offset straddling a cut)."""
+    dense_kernel or the split seeds (W=8), the exact-LDS scan (W=10), the key-group scan with
+    its references to tail_kernel (W=11 default; 16-B and, with ref32, 32-B references),
+    inline tails, no deferral; cuts inside super-steps and next to records' seed offsets
+    (k + hash_offset straddling a cut)."""
     from merpcr_amd import _native
     sts_text, seqs = _multi_case(W, n_sts, 30 + W)
     eng = MerPCR(wordsize=W, mismatches=1)
@@ -581,7 +583,9 @@ def test_sharded_ranges_all_paths(W, n_sts, opts):
         s.set_options(**opts)
     whole = s.fetch(s.run())
     assert len(whole) > 100
-    if "scan_grid" in opts:  # a grid of 37 scan workgroups (uneven XCD groups): the default list
+    # a grid of 37 scan workgroups (uneven XCD groups), or the key-group scans' references in the
+    # 32-B form (the default is 16-B since round 6): the default handle's list
+    if "scan_grid" in opts or "ref32" in opts:
         d = _native.Search(eng.device_table(), genome)
         assert np.array_equal(d.fetch(d.run()), whole)
         d.close()
