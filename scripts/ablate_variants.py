@@ -44,6 +44,11 @@ occur exactly once).  Hit counts of a variant are meaningless; only its scan tim
       128-B record lines then stay in L2): the bound on what record-line locality could save
   58  pair_kernel's genome loads (the primer-2 stretch and the primer-1 window) non-temporal, so
       that they do not push the record lines out of L2
+  11  a level 1.5 in the L1 for the I = 0 key groups, emulated: each level-1 positive first
+      loads a word of a 32 KiB region (the first 32 KiB of the prefilter's global copy, which
+      every CU reads, so it can stay in the CU's L1) by a hash of its key, then only 5/8 of the
+      positives (by another hash) issue their key-group probe -- what a 32 KiB Bloom filter of
+      the keys would pass; 12: the same loads, every positive probed (their cost alone)
   60  scan_kernel's genome-plane loads non-temporal (the stream kept out of L2's working set:
       the c4 level-2 tables, rank words + 16-B heads, are ~4.1 MB against a 4 MB L2)
 """
@@ -202,6 +207,30 @@ VARIANTS[10] = [(VARIANTS[7][0][0], VARIANTS[7][0][1].replace("& 7u", "& 3u").re
 VARIANTS[8] = VARIANTS[5] + [
     ("        if (!sched_dynamic(n_supers, kW)) {\n            stride = waves;", "        if (true) {  // ablation 8\n            stride = waves;", "replace"),
 ]
+
+def _l15(pass_rule):
+    return [
+        ("                uint32_t pk[kP], po[kP];\n",
+         "                uint32_t pk[kP], po[kP];\n                uint32_t kq[kP], l1w[kP];  // ablation 11/12\n", "replace"),
+        ("                                rw[q] = a.kgrp[v ? (key >> 4) : 0u];\n",
+         "                                kq[q] = v ? key : 0xFFFFFFFFu;  // ablation 11/12\n"
+         "                                l1w[q] = a.lfilt[v ? ((key * 0x9E3779B1u) >> 19) : 0u];\n", "replace"),
+        ("                prefetch(nx, ss);  // after this round's probes (every round: see prefetch)\n",
+         "                if constexpr (kRkf == 1) {  // ablation 11/12: the key-group probes after the L1 words\n"
+         "#pragma unroll\n"
+         "                    for (int q = 0; q < kP; ++q) {\n"
+         "                        if ((uint32_t)q * 64u < nr) {\n"
+         "                            const uint32_t key = kq[q];\n"
+         "                            const bool v2 = key != 0xFFFFFFFFu && l1w[q] != 0xDEADBEEFu && " + pass_rule + ";\n"
+         "                            rw[q] = a.kgrp[v2 ? (key >> 4) : 0u];\n"
+         "                        }\n"
+         "                    }\n"
+         "                }\n"),
+    ]
+
+
+VARIANTS[11] = _l15("(((key * 0x85EBCA6Bu) >> 29) < 5u)")
+VARIANTS[12] = _l15("true")
 
 VARIANTS[42] = VARIANTS[40] + [
     ("            ss = nx;\n            continue;\n        }\n        uint32_t hits = probe32",
